@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s (whole node) of the MI355X path tracer on BASELINE.json configs[1] —
+Cornell box, 1920x1080, 256 spp (16x16 stratified, jittered), diffuse + NEE, max depth 5.
+
+One *step* = every GPU renders its pixel tiles (32x32 tiles, tile t -> rank t % N) for `spp_per_step * N`
+sample indices, accumulating into its device-resident film; the N films are then reduced to rank 0 with
+one RCCL reduce over xGMI.  Per-GPU work per step is fixed (weak scaling): W*H*spp_per_step samples.
+
+Prints ONE JSON line on rank 0 (contract in the task statement): metric/value/unit, roofline of the dominant
+kernel (closest-hit octree traversal, algorithmic bytes per SURVEY.md §8(d) / its HIP-event launch time),
+and the CPU baseline (the oracle's C++ restatement on host cores, bounded sample, N=1 rank 0 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from computational_ray_tracer_amd import scene  # noqa: E402
+from computational_ray_tracer_amd.renderer import Renderer  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+TRAFFIC_FILE = ROOT / "profiles" / "traffic.json"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=4)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--spp-per-step", type=int, default=8)
+    p.add_argument("--res", type=str, default="1920x1080")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    return p.parse_args()
+
+
+def algorithmic_bytes_trace(st):
+    """closest-hit trace = 40 B per ray cast (read o,d 24 + write hit 16)
+    + 32 B per node box test + 40 B per triangle test (36 B vertices + 4 B leaf ref)."""
+    return 40 * st["rays"] + 32 * st["nodes_tested"] + 40 * st["tris_tested"]
+
+
+def cpu_baseline(cfg, seconds):
+    """Oracle (C++ restatement, `port`) on host threads, bounded sample: a horizontal band of full rows of
+    the same 1080p Cornell frame, 1 sample index, sized to ~`seconds` of CPU work."""
+    from oracle.oracle import OracleScene
+    threads = min(16, os.cpu_count() or 1)
+    o = OracleScene(cfg)
+    W, H = cfg.film.res
+    spp = cfg.sampler.spp()
+    rows, nidx = 8, 1
+    while True:
+        y0 = H // 2 - rows // 2
+        pix = np.arange(y0 * W, (y0 + rows) * W, dtype=np.int32)
+        t0 = time.perf_counter()
+        o.render(0, nidx, nthreads=threads, pixel_ids=pix)
+        dt = time.perf_counter() - t0
+        if dt > seconds * 0.5 or (rows >= H and nidx >= spp):
+            break
+        grow = max(2.0, seconds / max(dt, 1e-3))
+        if rows < H:
+            rows = min(H, int(rows * grow))
+        else:
+            nidx = min(spp, int(nidx * grow))
+    n = len(pix) * nidx
+    ms = n / dt / 1e6
+    return {"value": round(ms, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle C++ restatement (same octree BFS, watertight test, path integrator), {n} samples = "
+                      f"{rows} full rows of the {W}x{H} Cornell frame x sample indices 0..{nidx - 1}, "
+                      f"{threads} threads, {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    W, H = (int(x) for x in a.res.split("x"))
+    cfg = scene.cfg_cornell(res=(W, H), spp_side=16, max_depth=5)
+    spp = cfg.sampler.spp()
+    r = Renderer(cfg, device=torch.cuda.current_device())
+    r.set_shard(32, world, rank)
+    film = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    per_step = a.spp_per_step * world
+    cursor = [0]
+
+    def step():
+        i0 = cursor[0]
+        i1 = min(spp, i0 + per_step)
+        r.render_pass_device(i0, i1, film.data_ptr(), stream.cuda_stream)
+        cursor[0] = 0 if i1 >= spp else i1
+        if world > 1:
+            dist.reduce(film, dst=0)  # RCCL over xGMI (each pixel owned by one rank: exact sum)
+        return (i1 - i0)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    r.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx_done = 0
+    for _ in range(a.steps):
+        idx_done += step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    st = r.stats()
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        tot = torch.tensor([st["samples"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot)
+        total_samples = float(tot.item())
+    else:
+        total_samples = float(st["samples"])
+    value = total_samples / dt / 1e6
+    # roofline of the dominant kernel (closest-hit traversal): algorithmic bytes / average launch time
+    launches = max(1, st["launches_trace"])
+    avg_ms = st["ms_trace"] / launches
+    bytes_per_launch = algorithmic_bytes_trace(st) / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    if TRAFFIC_FILE.exists():
+        try:
+            traffic = json.loads(TRAFFIC_FILE.read_text()).get("k_trace_closest_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "Msamples/s (whole node) at 1920x1080; achieved HBM GB/s vs roofline",
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (procedural Cornell box scene, no datasets)",
+        "config": {"workload": f"BASELINE configs[1]: Cornell box {W}x{H} @ {spp} spp (16x16 stratified jittered), "
+                               f"diffuse + NEE, max depth 5, 1 quad light, 36 triangles",
+                   "res": [W, H], "spp_total": spp, "spp_per_step_per_gpu": a.spp_per_step, "max_depth": 5,
+                   "parallelism": f"pixel-tile shards x{world} (32x32 tiles) + RCCL film reduce"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_trace_closest", "avg_launch_ms": round(avg_ms, 4),
+                     "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+        "stage_ms": {k: round(st[k], 2) for k in ("ms_generate", "ms_trace", "ms_shade", "ms_shadow", "ms_film")},
+        "counters": {k: st[k] for k in ("samples", "rays", "shadow_rays", "nodes_tested", "tris_tested",
+                                        "shadow_nodes_tested", "shadow_tris_tested", "hits")},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds)
+        out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

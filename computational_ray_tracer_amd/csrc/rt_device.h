@@ -1,0 +1,333 @@
+// Device-side building blocks of the MI355X ray-tracing inner loop (gfx950, wave64).
+//
+// Every function restates one reference function (file:line cited) with the SAME float operation order
+// as the CPU oracle, compiled with -ffp-contract=off: FMA appears only where the reference calls std::fma
+// (DifferenceOfProducts helpers.h:56-62, EvaluatePolynomial helpers.h:117-126).  Transcendentals are
+// evaluated in double and rounded to float (documented build choice).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_internal.h"
+
+namespace rtmi {
+
+#define RT_DEV __device__ __forceinline__
+
+RT_DEV float f_cos(float x) { return (float)cos((double)x); }
+RT_DEV float f_sin(float x) { return (float)sin((double)x); }
+RT_DEV float f_atanh(float x) { return (float)atanh((double)x); }
+RT_DEV float f_cosh(float x) { return (float)cosh((double)x); }
+
+// helpers.h:50-54
+RT_DEV float gamma_n(int n) {
+    const float me = 0x1p-24f;  // numeric_limits<float>::epsilon() * 0.5
+    return ((float)n * me) / (1.0f - (float)n * me);
+}
+// glm scalar min/max/clamp
+RT_DEV float gmax(float x, float y) { return (x < y) ? y : x; }
+RT_DEV float gmin(float x, float y) { return (y < x) ? y : x; }
+RT_DEV float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
+// helpers.h:56-62
+RT_DEV float dop(float a, float b, float c, float d) {
+    float cd = c * d;
+    float x = __builtin_fmaf(a, b, -cd);
+    float e = __builtin_fmaf(-c, d, cd);
+    return x + e;
+}
+// std::max({a,b,c}) — first largest
+RT_DEV float max3f(float a, float b, float c) {
+    float m = a;
+    if (m < b) m = b;
+    if (m < c) m = c;
+    return m;
+}
+RT_DEV float lerpf_(float x, float a, float b) { return (1 - x) * a + x * b; }  // helpers.h:154-157
+
+struct V3 { float x, y, z; };
+RT_DEV V3 v3(float x, float y, float z) { return {x, y, z}; }
+RT_DEV V3 vadd(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+RT_DEV V3 vsub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+RT_DEV V3 vmul(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+RT_DEV float vdot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }           // glm dot vec3
+RT_DEV V3 vcross(V3 a, V3 b) { return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+RT_DEV V3 vnorm(V3 v) { float s = 1.0f / sqrtf(vdot(v, v)); return vmul(v, s); }      // glm normalize
+
+// glm mat4*vec4 = (m0*x + m1*y) + (m2*z + m3*w), column-major m[c*4+r]
+RT_DEV void mat4_mul(const float* M, float x, float y, float z, float w, float o[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float a0 = M[0 * 4 + r] * x, a1 = M[1 * 4 + r] * y, a2 = M[2 * 4 + r] * z, a3 = M[3 * 4 + r] * w;
+        o[r] = (a0 + a1) + (a2 + a3);
+    }
+}
+
+// ------------------------------------------------------------------ hashing + PCG32 (integer exact)
+RT_DEV uint64_t murmur_mix_block(uint64_t h, uint64_t k) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    k *= m; k ^= k >> 47; k *= m;
+    h ^= k; h *= m;
+    return h;
+}
+RT_DEV uint64_t murmur_final(uint64_t h) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    h ^= h >> 47; h *= m; h ^= h >> 47;
+    return h;
+}
+// hash.h:96-104 Hash(ivec2 p, int seed) — 12-byte key: one 8-byte block (x | y<<32) + 4-byte tail (seed)
+RT_DEV uint64_t hash_pixel(int x, int y, int seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = 0ull ^ (12ull * m);
+    h = murmur_mix_block(h, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)y << 32));
+    h ^= (uint64_t)(uint32_t)seed;  // tail bytes key[8..11], hash.h:47-55
+    h *= m;
+    return murmur_final(h);
+}
+// Hash(ivec2 p, int dim, int seed) — 16-byte key: two blocks
+RT_DEV uint64_t hash_pixel_dim(int x, int y, int dim, int seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = 0ull ^ (16ull * m);
+    h = murmur_mix_block(h, (uint64_t)(uint32_t)x | ((uint64_t)(uint32_t)y << 32));
+    h = murmur_mix_block(h, (uint64_t)(uint32_t)dim | ((uint64_t)(uint32_t)seed << 32));
+    return murmur_final(h);
+}
+RT_DEV uint64_t mix_bits(uint64_t v) {  // hash.h:67-74
+    v ^= (v >> 31); v *= 0x7fb5d329728ea185ull;
+    v ^= (v >> 27); v *= 0x81dadef4bc2dd44dull;
+    v ^= (v >> 33);
+    return v;
+}
+// HelperFunctions.h:175-203
+RT_DEV int permutation_element(uint32_t i, uint32_t l, uint32_t p) {
+    uint32_t w = l - 1;
+    w |= w >> 1; w |= w >> 2; w |= w >> 4; w |= w >> 8; w |= w >> 16;
+    do {
+        i ^= p; i *= 0xe170893du; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8; i *= 0x0929eb3fu;
+        i ^= p >> 23; i ^= (i & w) >> 1; i *= 1u | p >> 27; i *= 0x6935fa69u; i ^= (i & w) >> 11;
+        i *= 0x74dcb303u; i ^= (i & w) >> 2; i *= 0x9e501cc3u; i ^= (i & w) >> 2; i *= 0xc860a3dfu;
+        i &= w; i ^= i >> 5;
+    } while (i >= l);
+    return (int)((i + p) % l);
+}
+
+struct Pcg {  // rng.h:24-144
+    uint64_t state, inc;
+    RT_DEV uint32_t next() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dull + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    RT_DEV float uniform() {  // rng.h:122-124, OneMinusEpsilon == 1.0f
+        float v = (float)next() * 0x1p-32f;
+        return (1.0f < v) ? 1.0f : v;  // std::min<float>(1, v)
+    }
+    RT_DEV void set_sequence(uint64_t seq) {  // rng.h:36-39, 113-119
+        uint64_t seed = mix_bits(seq);
+        state = 0u;
+        inc = (seq << 1u) | 1u;
+        next();
+        state += seed;
+        next();
+    }
+    RT_DEV void advance(uint64_t delta) {  // rng.h:131-144
+        uint64_t curMult = 0x5851f42d4c957f2dull, curPlus = inc, accMult = 1u, accPlus = 0u;
+        while (delta > 0) {
+            if (delta & 1) { accMult *= curMult; accPlus = accPlus * curMult + curPlus; }
+            curPlus = (curMult + 1) * curPlus;
+            curMult *= curMult;
+            delta /= 2;
+        }
+        state = accMult * state + accPlus;
+    }
+};
+
+// samplers.h:38-136 — Independent / Stratified sampler state of one camera sample
+struct Smp {
+    Pcg rng;
+    int px, py, index, dim;
+    // samplers.h:80-93 / 47-51 (caller guarantees the stratified jitter==false index < spp precondition)
+    RT_DEV void start(const DevSampler& S, int x, int y, int idx, int d) {
+        px = x; py = y; index = idx; dim = d;
+        rng.set_sequence(hash_pixel(x, y, S.seed));
+        rng.advance((uint64_t)idx * 65536ull + (uint64_t)d);
+    }
+    RT_DEV float get1d(const DevSampler& S) {  // samplers.h:95-104
+        if (S.kind == 0) return rng.uniform();
+        uint64_t h = hash_pixel_dim(px, py, dim, S.seed);
+        int stratum = permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
+        ++dim;
+        float delta = S.jitter ? rng.uniform() : 0.5f;
+        return ((float)stratum + delta) / (float)S.spp;
+    }
+    RT_DEV void get2d(const DevSampler& S, float& u0, float& u1) {  // samplers.h:107-123
+        if (S.kind == 0) { u0 = rng.uniform(); u1 = rng.uniform(); return; }
+        if (index >= S.spp) { u0 = 0; u1 = 0; return; }
+        uint64_t h = hash_pixel_dim(px, py, dim, S.seed);
+        int stratum = permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
+        dim += 2;
+        int x = stratum % S.xs, y = stratum / S.xs;
+        float dx = S.jitter ? rng.uniform() : 0.5f;
+        float dy = S.jitter ? rng.uniform() : 0.5f;
+        u0 = ((float)x + dx) / (float)S.xs;
+        u1 = ((float)y + dy) / (float)S.ys;
+    }
+};
+
+// ------------------------------------------------------------------------------ sampling warps
+RT_DEV float visible_pdf(float lambda) {  // Sampling.h:63-67
+    if (lambda < 360 || lambda > 830) return 0;
+    float c = f_cosh(0.0072f * (lambda - 538));
+    return (float)((double)0.0039398042f / ((double)c * (double)c));
+}
+RT_DEV float sample_visible_wavelength(float u) {  // Sampling.h:69-71
+    return 538 - 138.888889f * f_atanh(0.85691062f - 1.82750197f * u);
+}
+RT_DEV float sample_linear(float u, float a, float b) {  // Sampling.h:205-211
+    if (u == 0 && a == 0) return 0;
+    float x = (u * (a + b)) / (a + sqrtf(lerpf_(u, a * a, b * b)));
+    return (1.0f < x) ? 1.0f : x;
+}
+RT_DEV float sample_tent(float u, float r) {  // Sampling.h:228-235 with the coin taken from u (build-defined)
+    if (u < 0.5f) {
+        float up = u * 2.0f; up = (1.0f < up) ? 1.0f : up;
+        return -r + r * sample_linear(up, 0, 1);
+    }
+    float up = (u - 0.5f) * 2.0f; up = (1.0f < up) ? 1.0f : up;
+    return r * sample_linear(up, 1, 0);
+}
+RT_DEV void disk_concentric(float u0, float u1, float& ox, float& oy) {  // Sampling.h:383-403
+    float x = 2.0f * u0 - 1.0f, y = 2.0f * u1 - 1.0f;
+    if (x == 0 && y == 0) { ox = 0; oy = 0; return; }
+    float theta, r;
+    if (fabsf(x) > fabsf(y)) { r = x; theta = 0.78539816339744830961f * (y / x); }
+    else { r = y; theta = 1.57079632679489661923f - 0.78539816339744830961f * (x / y); }
+    ox = r * f_cos(theta);
+    oy = r * f_sin(theta);
+}
+
+// ------------------------------------------------------------------------------------ spectra
+RT_DEV float dense_query(const float* tab, float lambda) {  // spectrum.h:386-398 / 430-437
+    long off = (long)roundf(lambda) - 360;  // std::lround: half away from zero
+    if (off < 0 || off >= kSpecN) return 0;
+    return tab[off];
+}
+RT_DEV float piecewise_query(const float* lam, const float* val, int n, float lambda) {  // spectrum.cpp:60-71
+    if (n == 0 || lambda < lam[0] || lambda > lam[n - 1]) return 0;
+    long size = (long)n - 2, first = 1;  // helpers.h:159-172 FindInterval
+    while (size > 0) {
+        long half = size >> 1, middle = first + half;
+        bool r = lam[middle] <= lambda;
+        first = r ? middle + 1 : first;
+        size = r ? size - (half + 1) : half;
+    }
+    long o = first - 1;
+    o = o < 0 ? 0 : (o > n - 2 ? n - 2 : o);
+    float t = (lambda - lam[o]) / (lam[o + 1] - lam[o]);
+    return lerpf_(t, val[o], val[o + 1]);
+}
+RT_DEV float sigmoid_eval(float c0, float c1, float c2, float lambda) {  // color.h:373-399
+    float x = __builtin_fmaf(lambda, __builtin_fmaf(lambda, c0, c1), c2);
+    if (__builtin_isinf(x)) return x > 0 ? 1 : 0;
+    return .5f + x / (2 * sqrtf(1 + (x * x)));
+}
+// pixelsensor.h:81-87 XYZ sensor ToSensorRGB (SafeDiv by pdf, Average, * imagingRatio)
+RT_DEV void to_sensor_rgb(const DevSpectra* sp, const float L_[8], const float lam[8], const float pdf[8], float ir,
+                          float rgb[3]) {
+    float L[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) L[i] = (pdf[i] != 0) ? L_[i] / pdf[i] : 0.f;
+    const float* bars[3] = {sp->X, sp->Y, sp->Z};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float sum = dense_query(bars[c], lam[0]) * L[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) sum += dense_query(bars[c], lam[i]) * L[i];
+        rgb[c] = ir * (sum / 8);
+    }
+}
+
+// ------------------------------------------------------------------------------ geometry tests
+// Per-ray precomputation for the watertight test (Shapes.h:1138-1160): the permutation and shear depend
+// only on the ray, so they are hoisted (bit-identical to recomputing them per triangle).
+struct TriRay {
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+    float ox, oy, oz;     // ray origin, permuted
+};
+RT_DEV float sel3(int k, float x, float y, float z) { return k == 0 ? x : (k == 1 ? y : z); }
+RT_DEV TriRay make_triray(V3 o, V3 d) {
+    TriRay t;
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    t.kz = (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);  // helpers.h:64-66
+    t.kx = t.kz + 1; if (t.kx == 3) t.kx = 0;
+    t.ky = t.kx + 1; if (t.ky == 3) t.ky = 0;
+    float dx = sel3(t.kx, d.x, d.y, d.z), dy = sel3(t.ky, d.x, d.y, d.z), dz = sel3(t.kz, d.x, d.y, d.z);
+    t.Sx = -dx / dz; t.Sy = -dy / dz; t.Sz = 1 / dz;
+    t.ox = sel3(t.kx, o.x, o.y, o.z); t.oy = sel3(t.ky, o.x, o.y, o.z); t.oz = sel3(t.kz, o.x, o.y, o.z);
+    return t;
+}
+// Shapes.h:1101-1260 Triangle::BasicIntersect on pre-transformed world vertices (degenerate triangles were
+// removed from the tiles at upload, Shapes.h:1131).  Returns true and (b0,b1,b2,t) on a hit.
+RT_DEV bool tri_intersect(const TriRay& R, float tMax, float4 A, float4 B, float4 Cc, float& b0, float& b1, float& b2,
+                          float& tt) {
+    // vertices p0=(A.x,A.y,A.z) p1=(A.w,B.x,B.y) p2=(B.z,B.w,C.x); translate after permuting (same ops)
+    float p0x = sel3(R.kx, A.x, A.y, A.z) - R.ox, p0y = sel3(R.ky, A.x, A.y, A.z) - R.oy, p0z = sel3(R.kz, A.x, A.y, A.z) - R.oz;
+    float p1x = sel3(R.kx, A.w, B.x, B.y) - R.ox, p1y = sel3(R.ky, A.w, B.x, B.y) - R.oy, p1z = sel3(R.kz, A.w, B.x, B.y) - R.oz;
+    float p2x = sel3(R.kx, B.z, B.w, Cc.x) - R.ox, p2y = sel3(R.ky, B.z, B.w, Cc.x) - R.oy, p2z = sel3(R.kz, B.z, B.w, Cc.x) - R.oz;
+    p0x += R.Sx * p0z; p0y += R.Sy * p0z;
+    p1x += R.Sx * p1z; p1y += R.Sy * p1z;
+    p2x += R.Sx * p2z; p2y += R.Sy * p2z;
+    float e0 = dop(p1x, p2y, p1y, p2x);
+    float e1 = dop(p2x, p0y, p2y, p0x);
+    float e2 = dop(p0x, p1y, p0y, p1x);
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {  // Shapes.h:1174-1184
+        e0 = (float)((double)p2y * (double)p1x - (double)p2x * (double)p1y);
+        e1 = (float)((double)p0y * (double)p2x - (double)p0x * (double)p2y);
+        e2 = (float)((double)p1y * (double)p0x - (double)p1x * (double)p0y);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0z *= R.Sz; p1z *= R.Sz; p2z *= R.Sz;
+    float tScaled = e0 * p0z + e1 * p1z + e2 * p2z;
+    if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
+    else if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
+    float invDet = 1 / det;
+    float t = tScaled * invDet;
+    if (__builtin_isnan(t)) return false;
+    float maxZt = max3f(fabsf(p0z), fabsf(p1z), fabsf(p2z));
+    float deltaZ = gamma_n(3) * maxZt;
+    float maxXt = max3f(fabsf(p0x), fabsf(p1x), fabsf(p2x));
+    float maxYt = max3f(fabsf(p0y), fabsf(p1y), fabsf(p2y));
+    float deltaX = gamma_n(5) * (maxXt + maxZt);
+    float deltaY = gamma_n(5) * (maxYt + maxZt);
+    float deltaE = 2 * (gamma_n(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    float maxE = max3f(fabsf(e0), fabsf(e1), fabsf(e2));
+    float deltaT = 3 * (gamma_n(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * fabsf(invDet);
+    if (t <= deltaT) return false;
+    b0 = e0 * invDet; b1 = e1 * invDet; b2 = e2 * invDet;
+    tt = t;
+    return true;
+}
+
+// Shapes.h:100-124 Bounds3::IntersectP.  1/d is hoisted (same value as computed per node); the per-axis
+// early return is folded into one final compare (min_t only grows, max_t only shrinks, NaN axes are no-ops).
+RT_DEV bool box_hit(float4 a, float4 b, V3 o, V3 inv, float tMax) {
+    const float g = 1 + 2 * gamma_n(3);
+    float mn = 0, mx = tMax;
+    float tn, tf, s;
+    tn = (a.x - o.x) * inv.x; tf = (b.x - o.x) * inv.x;
+    if (tn > tf) { s = tn; tn = tf; tf = s; }
+    tf *= g; mn = tn > mn ? tn : mn; mx = tf < mx ? tf : mx;
+    tn = (a.y - o.y) * inv.y; tf = (b.y - o.y) * inv.y;
+    if (tn > tf) { s = tn; tn = tf; tf = s; }
+    tf *= g; mn = tn > mn ? tn : mn; mx = tf < mx ? tf : mx;
+    tn = (a.z - o.z) * inv.z; tf = (b.z - o.z) * inv.z;
+    if (tn > tf) { s = tn; tn = tf; tf = s; }
+    tf *= g; mn = tn > mn ? tn : mn; mx = tf < mx ? tf : mx;
+    return !(mn > mx);
+}
+
+}  // namespace rtmi

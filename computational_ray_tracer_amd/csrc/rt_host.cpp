@@ -1,0 +1,1054 @@
+// librtmi355x — host side of the drop-in C-ABI (include/rtmi355x.h).
+//
+// Owns: the HIP context/stream, the scene preparation the reference does on the host before its render loop
+// (TriModel world transform + back-face flags, Shapes.h:1282-1380; Octtree_Model::CreateOcttree with the
+// Möller overlap test, Octtree_Model.h:33-63/180-367, AABB_triangle_Moller.h:187-474; Spectra::Init,
+// spectrum.cpp:2612-2634), the flattening of that octree into the HBM layout of rt_internal.h, and the
+// orchestration of the wavefront kernels of rt_kernels.hip for one render pass.
+//
+// There is no CPU fallback: every pass runs on the MI355X; rt_create fails without a gfx950 device.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <queue>
+#include <string>
+#include <vector>
+
+#include "../../include/rtmi355x.h"
+#include "../data/spectra_data.h"
+#include "rt_internal.h"
+
+using namespace rtmi;
+
+namespace {
+
+// ------------------------------------------------------------------------------ host float math
+// glm operation order, float, -ffp-contract=off (same contract as the device code)
+struct F3 { float x, y, z; float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); } };
+inline F3 f3add(F3 a, F3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline F3 f3sub(F3 a, F3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline F3 f3mul(F3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline float f3dot(F3 a, F3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+inline F3 f3cross(F3 a, F3 b) { return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+inline F3 f3norm(F3 v) { float s = 1.0f / std::sqrt(f3dot(v, v)); return f3mul(v, s); }
+inline void m4v(const float* M, float x, float y, float z, float w, float o[4]) {
+    for (int r = 0; r < 4; ++r) {
+        float a0 = M[0 * 4 + r] * x, a1 = M[1 * 4 + r] * y, a2 = M[2 * 4 + r] * z, a3 = M[3 * 4 + r] * w;
+        o[r] = (a0 + a1) + (a2 + a3);
+    }
+}
+inline F3 m3v(const float* M, F3 v) {
+    float o[3];
+    for (int r = 0; r < 3; ++r) o[r] = (M[0 * 3 + r] * v.x + M[1 * 3 + r] * v.y) + M[2 * 3 + r] * v.z;
+    return {o[0], o[1], o[2]};
+}
+
+// ---------------------------------------------------------------------------------- spectra (host)
+// spectrum.cpp:60-71 PiecewiseLinearSpectrum::Query with helpers.h:159-172 FindInterval
+struct PLS {
+    std::vector<float> l, v;
+    float query(float lambda) const {
+        if (l.empty() || lambda < l.front() || lambda > l.back()) return 0;
+        long size = (long)l.size() - 2, first = 1;
+        while (size > 0) {
+            long half = size >> 1, middle = first + half;
+            bool r = l[middle] <= lambda;
+            first = r ? middle + 1 : first;
+            size = r ? size - (half + 1) : half;
+        }
+        long o = std::min(std::max(first - 1, 0L), (long)l.size() - 2);
+        float t = (lambda - l[o]) / (l[o + 1] - l[o]);
+        return (1 - t) * v[o] + t * v[o + 1];
+    }
+};
+struct DenseS {
+    std::vector<float> v;  // 360..830
+    float query(float lambda) const {
+        long off = std::lround(lambda) - 360;
+        return (off < 0 || off >= (long)v.size()) ? 0.f : v[off];
+    }
+};
+template <class S>
+DenseS to_dense(const S& s) {
+    DenseS d;
+    d.v.resize(kSpecN);
+    for (int l = 360; l <= 830; ++l) d.v[l - 360] = s.query((float)l);
+    return d;
+}
+template <class A, class B>
+float inner_product(const A& f, const B& g) {  // spectrum.h:762-768
+    float acc = 0;
+    for (float lambda = 360; lambda <= 830; ++lambda) acc += f.query(lambda) * g.query(lambda);
+    return acc;
+}
+struct HostSpectra {
+    DenseS X, Y, Z, D65d;
+    PLS D65, F1;
+    PLS interleaved(const float* s, int n, bool normalize) const {  // spectrum.cpp:134-165 FromInterleaved
+        PLS p;
+        if (s[0] > 360) { p.l.push_back(359); p.v.push_back(s[1]); }
+        for (int i = 0; i < n / 2; ++i) { p.l.push_back(s[2 * i]); p.v.push_back(s[2 * i + 1]); }
+        if (p.l.back() < 830) { p.l.push_back(831); p.v.push_back(p.v.back()); }
+        if (normalize) {
+            float sc = 106.856895f / inner_product(p, Y);
+            for (float& x : p.v) x *= sc;
+        }
+        return p;
+    }
+    void init() {
+        auto cie = [](const float* t) {
+            PLS p;
+            p.l.assign(rtdata::cie_lambda, rtdata::cie_lambda + 471);
+            p.v.assign(t, t + 471);
+            return to_dense(p);
+        };
+        X = cie(rtdata::cie_x); Y = cie(rtdata::cie_y); Z = cie(rtdata::cie_z);
+        D65 = interleaved(rtdata::illum_d65, rtdata::illum_d65_n, true);
+        F1 = interleaved(rtdata::illum_f1, rtdata::illum_f1_n, true);
+        D65d = to_dense(D65);
+    }
+};
+
+// ------------------------------------------------------------------ Möller triangle / box overlap (host)
+// AABB_triangle_Moller.h:187-474 (AxisTest_Z0 never rejects: the quirk at :342 is kept)
+bool axis_ok(float pa, float pb, float rad) {
+    float mn, mx;
+    if (pa < pb) { mn = pa; mx = pb; } else { mn = pb; mx = pa; }
+    return !(mn > rad || mx < -rad);
+}
+bool axis_ok_z12(float p1, float p2, float rad) {
+    float mn, mx;
+    if (p2 < p1) { mn = p2; mx = p1; } else { mn = p1; mx = p2; }
+    return !(mn > rad || mx < -rad);
+}
+bool tri_box_overlap(F3 c, F3 h, F3 t0, F3 t1, F3 t2) {
+    F3 v0 = f3sub(t0, c), v1 = f3sub(t1, c), v2 = f3sub(t2, c);
+    F3 e0 = f3sub(v1, v0), e1 = f3sub(v2, v1), e2 = f3sub(v0, v2);
+    float fex, fey, fez;
+    fex = std::fabs(e0.x); fey = std::fabs(e0.y); fez = std::fabs(e0.z);
+    if (!axis_ok(e0.z * v0.y - e0.y * v0.z, e0.z * v2.y - e0.y * v2.z, fez * h.y + fey * h.z)) return false;   // X01
+    if (!axis_ok(-e0.z * v0.x + e0.x * v0.z, -e0.z * v2.x + e0.x * v2.z, fez * h.x + fex * h.z)) return false; // Y02
+    if (!axis_ok_z12(e0.y * v1.x - e0.x * v1.y, e0.y * v2.x - e0.x * v2.y, fey * h.x + fex * h.y)) return false; // Z12
+    fex = std::fabs(e1.x); fey = std::fabs(e1.y); fez = std::fabs(e1.z);
+    if (!axis_ok(e1.z * v0.y - e1.y * v0.z, e1.z * v2.y - e1.y * v2.z, fez * h.y + fey * h.z)) return false;   // X01
+    if (!axis_ok(-e1.z * v0.x + e1.x * v0.z, -e1.z * v2.x + e1.x * v2.z, fez * h.x + fex * h.z)) return false; // Y02
+    // Z0: never rejects (reference returns true on both paths)
+    fex = std::fabs(e2.x); fey = std::fabs(e2.y); fez = std::fabs(e2.z);
+    if (!axis_ok(e2.z * v0.y - e2.y * v0.z, e2.z * v1.y - e2.y * v1.z, fez * h.y + fey * h.z)) return false;   // X2
+    if (!axis_ok(-e2.z * v0.x + e2.x * v0.z, -e2.z * v1.x + e2.x * v1.z, fez * h.x + fex * h.z)) return false; // Y1
+    if (!axis_ok_z12(e2.y * v1.x - e2.x * v1.y, e2.y * v2.x - e2.x * v2.y, fey * h.x + fex * h.y)) return false; // Z12
+    auto mm = [](float a, float b, float c, float& mn, float& mx) {
+        mn = mx = a;
+        if (b < mn) mn = b;
+        if (b > mx) mx = b;
+        if (c < mn) mn = c;
+        if (c > mx) mx = c;
+    };
+    float mn, mx;
+    mm(v0.x, v1.x, v2.x, mn, mx);
+    if (mn > h.x || mx < -h.x) return false;
+    mm(v0.y, v1.y, v2.y, mn, mx);
+    if (mn > h.y || mx < -h.y) return false;
+    mm(v0.z, v1.z, v2.z, mn, mx);
+    if (mn > h.z || mx < -h.z) return false;
+    F3 nrm = f3cross(e0, e1);  // planeBoxOverlap
+    float vmin[3], vmax[3];
+    for (int q = 0; q < 3; ++q) {
+        float v = v0[q], nq = nrm[q], mb = h[q];
+        if (nq > 0.0f) { vmin[q] = -mb - v; vmax[q] = mb - v; }
+        else { vmin[q] = mb - v; vmax[q] = -mb - v; }
+    }
+    if (f3dot(nrm, {vmin[0], vmin[1], vmin[2]}) > 0.0f) return false;
+    if (f3dot(nrm, {vmax[0], vmax[1], vmax[2]}) >= 0.0f) return true;
+    return false;
+}
+
+// ------------------------------------------------------------------------------- octree builder
+// Octtree_Model.h:33-63 CreateOcttree, 180-277 AddTriangle, 279-358 Split, 361-367 tri_boundsIntersection
+struct OctBuild {
+    struct Node { F3 mn, mx; int first_child = -1; std::vector<int> tris; };
+    std::vector<Node> nodes;
+    const std::vector<F3>* tri3 = nullptr;  // 3 world vertices per triangle
+    int capacity = 40;
+
+    bool overlap(int t, const Node& n) const {
+        F3 half = {(n.mx.x - n.mn.x) / 2.0f, (n.mx.y - n.mn.y) / 2.0f, (n.mx.z - n.mn.z) / 2.0f};
+        F3 c = f3add(n.mn, half);
+        const F3* p = &(*tri3)[3 * (size_t)t];
+        return tri_box_overlap(c, half, p[0], p[1], p[2]);
+    }
+    void split(int id) {
+        F3 mn = nodes[id].mn, mx = nodes[id].mx;
+        F3 h = {(mx.x - mn.x) / 2.0f, (mx.y - mn.y) / 2.0f, (mx.z - mn.z) / 2.0f};
+        F3 C = f3add(mn, h);
+        h = f3add(h, {0.01f, 0.01f, 0.01f});
+        // child order: top fl, fr, bl, br, bottom fl, fr, bl, br (Octtree_Model.h:287-300)
+        const F3 lo[8] = {{-h.x, 0, -h.z}, {0, 0, -h.z}, {-h.x, 0, 0}, {0, 0, 0},
+                          {-h.x, -h.y, -h.z}, {0, -h.y, -h.z}, {-h.x, -h.y, 0}, {0, -h.y, 0}};
+        const F3 hi[8] = {{0, h.y, 0}, {h.x, h.y, 0}, {0, h.y, h.z}, {h.x, h.y, h.z},
+                          {0, 0, 0}, {h.x, 0, 0}, {0, 0, h.z}, {h.x, 0, h.z}};
+        Node ch[8];
+        for (int k = 0; k < 8; ++k) { ch[k].mn = f3add(C, lo[k]); ch[k].mx = f3add(C, hi[k]); }
+        for (int t : nodes[id].tris)
+            for (int k = 0; k < 8; ++k)
+                if (overlap(t, ch[k])) ch[k].tris.push_back(t);
+        size_t cnt = nodes[id].tris.size();
+        for (int k = 0; k < 8; ++k)
+            if (ch[k].tris.size() == cnt) return;  // abort rule (Octtree_Model.h:331-340)
+        int first = (int)nodes.size();
+        for (int k = 0; k < 8; ++k) nodes.push_back(std::move(ch[k]));
+        nodes[id].first_child = first;
+        nodes[id].tris.clear();
+        nodes[id].tris.shrink_to_fit();
+    }
+    void add(int t) {
+        std::queue<int> q;
+        q.push(0);
+        while (!q.empty()) {
+            int cur = q.front();
+            q.pop();
+            if (!overlap(t, nodes[cur])) continue;
+            if (nodes[cur].first_child < 0) {
+                nodes[cur].tris.push_back(t);
+                if ((int)nodes[cur].tris.size() >= capacity) split(cur);
+            } else {
+                for (int k = 0; k < 8; ++k) q.push(nodes[cur].first_child + k);
+            }
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------- buffers
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool have_scene = false, have_cam = false, have_smp = false, have_film = false, have_integ = false;
+    rt_camera_desc cam{};
+    rt_sampler_desc smp{};
+    rt_film_desc film{};
+    rt_integrator_desc integ{};
+    // scene (host mirrors kept for export)
+    int n_tris = 0;
+    std::vector<float> h_bounds;
+    std::vector<int32_t> h_child, h_leaf_first, h_leaf_count, h_refs;
+    rt_octree_info info{};
+    bool cull = false;
+    DevScene dsc{};
+    std::vector<void*> scene_allocs;
+    // spectra + resolve matrices
+    HostSpectra hs;
+    DevSpectra* d_spec = nullptr;
+    float resolveA[9], resolveB[9];
+    float* d_resolve = nullptr;
+    // pixel work list
+    int tile = 32, n_shards = 1, shard_id = 0;
+    bool work_dirty = true;
+    int n_work = 0;
+    int* d_work = nullptr;
+    // workspace (grown on demand)
+    size_t cap = 0;
+    float4 *rayO = nullptr, *rayD = nullptr, *lamA = nullptr, *lamB = nullptr, *pdfA = nullptr, *pdfB = nullptr;
+    float4 *hitB = nullptr, *qO = nullptr, *qD = nullptr, *sO = nullptr, *sD = nullptr;
+    float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr, *LdA = nullptr, *LdB = nullptr;
+    int *slot = nullptr, *hitPrim = nullptr, *qSlot = nullptr, *sSlot = nullptr, *dim = nullptr;
+    uint4* rng = nullptr;
+    int* d_qcount = nullptr;   // [0],[1] ping-pong queues, [2] shadow
+    unsigned long long* d_ctr = nullptr;
+    float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
+    size_t film_cap = 0;
+    int grid = 0;              // persistent grid size (blocks)
+    // stats
+    rt_stats stats{};
+    struct Ev { hipEvent_t a, b; int stage; };
+    std::vector<Ev> pending;
+    std::vector<hipEvent_t> pool;
+};
+
+namespace {
+
+int fail(rt_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+#define HIPCHK(c, call)                                                                                   \
+    do {                                                                                                  \
+        hipError_t _e = (call);                                                                           \
+        if (_e != hipSuccess)                                                                             \
+            return fail((c), _e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP,                             \
+                        std::string(#call) + ": " + hipGetErrorString(_e));                               \
+    } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+    return hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T));
+}
+
+void free_scene(rt_ctx* c) {
+    for (void* p : c->scene_allocs) hipFree(p);
+    c->scene_allocs.clear();
+    c->dsc = DevScene{};
+    c->have_scene = false;
+}
+
+void free_workspace(rt_ctx* c) {
+    void* ptrs[] = {c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->qO, c->qD, c->sO, c->sD,
+                    c->betaA, c->betaB, c->LA, c->LB, c->LdA, c->LdB, c->slot, c->hitPrim, c->qSlot, c->sSlot,
+                    c->dim, c->rng};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    c->rayO = c->rayD = c->lamA = c->lamB = c->pdfA = c->pdfB = c->hitB = c->qO = c->qD = c->sO = c->sD = nullptr;
+    c->betaA = c->betaB = c->LA = c->LB = c->LdA = c->LdB = nullptr;
+    c->slot = c->hitPrim = c->qSlot = c->sSlot = c->dim = nullptr;
+    c->rng = nullptr;
+    c->cap = 0;
+}
+
+int ensure_workspace(rt_ctx* c, size_t n, bool path) {
+    if (c->cap >= n && (!path || c->betaA)) return RT_OK;
+    free_workspace(c);
+    // queue arrays are sized 2n (ping-pong) in path mode
+    HIPCHK(c, dalloc(&c->rayO, 2 * n)); HIPCHK(c, dalloc(&c->rayD, 2 * n)); HIPCHK(c, dalloc(&c->slot, 2 * n));
+    HIPCHK(c, dalloc(&c->lamA, n)); HIPCHK(c, dalloc(&c->lamB, n));
+    HIPCHK(c, dalloc(&c->pdfA, n)); HIPCHK(c, dalloc(&c->pdfB, n));
+    HIPCHK(c, dalloc(&c->hitB, n)); HIPCHK(c, dalloc(&c->hitPrim, n));
+    if (path) {
+        HIPCHK(c, dalloc(&c->sO, n)); HIPCHK(c, dalloc(&c->sD, n)); HIPCHK(c, dalloc(&c->sSlot, n));
+        HIPCHK(c, dalloc(&c->betaA, n)); HIPCHK(c, dalloc(&c->betaB, n));
+        HIPCHK(c, dalloc(&c->LA, n)); HIPCHK(c, dalloc(&c->LB, n));
+        HIPCHK(c, dalloc(&c->LdA, n)); HIPCHK(c, dalloc(&c->LdB, n));
+        HIPCHK(c, dalloc(&c->dim, n)); HIPCHK(c, dalloc(&c->rng, n));
+    }
+    c->cap = n;
+    return RT_OK;
+}
+
+hipEvent_t ev_get(rt_ctx* c) {
+    if (!c->pool.empty()) {
+        hipEvent_t e = c->pool.back();
+        c->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+void ev_mark(rt_ctx* c, hipStream_t st, int stage, hipEvent_t a) {
+    hipEvent_t b = ev_get(c);
+    hipEventRecord(b, st);
+    c->pending.push_back({a, b, stage});
+}
+hipEvent_t ev_start(rt_ctx* c, hipStream_t st) {
+    hipEvent_t a = ev_get(c);
+    hipEventRecord(a, st);
+    return a;
+}
+enum { ST_GEN = 0, ST_TRACE, ST_SHADE, ST_SHADOW, ST_FILM };
+
+void harvest(rt_ctx* c) {
+    for (auto& e : c->pending) {
+        float ms = 0;
+        hipEventSynchronize(e.b);
+        hipEventElapsedTime(&ms, e.a, e.b);
+        switch (e.stage) {
+            case ST_GEN: c->stats.ms_generate += ms; break;
+            case ST_TRACE: c->stats.ms_trace += ms; c->stats.launches_trace += 1; break;
+            case ST_SHADE: c->stats.ms_shade += ms; break;
+            case ST_SHADOW: c->stats.ms_shadow += ms; c->stats.launches_shadow += 1; break;
+            default: c->stats.ms_film += ms; break;
+        }
+        c->pool.push_back(e.a);
+        c->pool.push_back(e.b);
+    }
+    c->pending.clear();
+}
+
+// Owned pixels in tile order: tile_size² tiles in row-major tile order, tile t owned iff t % n == id;
+// inside a tile 8×8 micro-tiles (one wave64 = one micro-tile → coherent rays), row-major inside.
+int build_work(rt_ctx* c) {
+    if (!c->work_dirty && c->d_work) return RT_OK;
+    int W = c->film.res_x, H = c->film.res_y, T = c->tile;
+    int tx = (W + T - 1) / T, ty = (H + T - 1) / T;
+    std::vector<int> px;
+    px.reserve((size_t)W * H / std::max(1, c->n_shards) + T * T);
+    for (int t = 0; t < tx * ty; ++t) {
+        if (t % c->n_shards != c->shard_id) continue;
+        int x0 = (t % tx) * T, y0 = (t / tx) * T;
+        for (int my = 0; my < T; my += 8)
+            for (int mx = 0; mx < T; mx += 8)
+                for (int yy = 0; yy < 8; ++yy)
+                    for (int xx = 0; xx < 8; ++xx) {
+                        int x = x0 + mx + xx, y = y0 + my + yy;
+                        if (mx + xx < T && my + yy < T && x < W && y < H) px.push_back(y * W + x);
+                    }
+    }
+    if (c->d_work) hipFree(c->d_work);
+    c->d_work = nullptr;
+    HIPCHK(c, dalloc(&c->d_work, px.size()));
+    HIPCHK(c, hipMemcpy(c->d_work, px.data(), px.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->n_work = (int)px.size();
+    c->work_dirty = false;
+    return RT_OK;
+}
+
+DevCamera dev_camera(const rt_camera_desc& d) {
+    DevCamera c;
+    std::memcpy(c.r2c, d.raster_to_camera, 64);
+    std::memcpy(c.c2w, d.camera_to_world, 64);
+    c.lens_radius = d.lens_radius;
+    c.focal_distance = d.focal_distance;
+    return c;
+}
+DevSampler dev_sampler(const rt_sampler_desc& d) {
+    DevSampler s;
+    s.kind = d.kind; s.xs = d.x_samples; s.ys = d.y_samples; s.jitter = d.jitter; s.seed = d.seed;
+    s.spp = d.kind == RT_SAMPLER_INDEPENDENT ? d.x_samples : d.x_samples * d.y_samples;
+    return s;
+}
+DevFilm dev_film(const rt_film_desc& d) {
+    DevFilm f;
+    f.res_x = d.res_x; f.res_y = d.res_y; f.filter = d.filter;
+    f.rx = d.filter_radius[0]; f.ry = d.filter_radius[1]; f.imaging_ratio = d.imaging_ratio;
+    return f;
+}
+
+ShadeRefIO shade_ref_io(rt_ctx* c) {
+    ShadeRefIO io{};
+    float a = c->integ.albedo_rgb[0];
+    io.albedo_c2 = (a - .5f) / std::sqrt(a * (1 - a));  // color.cpp:35-37
+    float g = 1.0f / (2.0f * 1.0f);                      // RGBIlluminant(1,1,1): scale = 2*max = 2, rgb/scale = .5
+    io.illum_c2 = (g - .5f) / std::sqrt(g * (1 - g));
+    io.illum_scale = 2.0f;
+    return io;
+}
+
+int check_ready(rt_ctx* c) {
+    if (!c) return RT_E_ARG;
+    if (!c->have_scene || !c->have_cam || !c->have_smp || !c->have_film || !c->have_integ)
+        return fail(c, RT_E_STATE, "scene, camera, sampler, film and integrator must be set before rendering");
+    return RT_OK;
+}
+
+// one render pass over [ib, ie) into the device film
+int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    if (ib < 0 || ie < ib) return fail(c, RT_E_ARG, "invalid index range");
+    DevSampler smp = dev_sampler(c->smp);
+    if (c->smp.kind == RT_SAMPLER_STRATIFIED && !c->smp.jitter && ie > smp.spp)
+        return fail(c, RT_E_ARG, "StratifiedSampler without jitter supports indices < SamplesPerPixel (samplers.h:83-87)");
+    if ((rc = build_work(c))) return rc;
+    if (ie == ib || c->n_work == 0) return RT_OK;
+    bool path = c->integ.kind == RT_INTEGRATOR_PATH;
+    const size_t target = path ? (size_t)8 << 20 : (size_t)16 << 20;  // samples in flight per batch
+    int B = (int)std::max<size_t>(1, target / (size_t)c->n_work);
+    B = std::min(B, ie - ib);
+    size_t nmax = (size_t)B * c->n_work;
+    if ((rc = ensure_workspace(c, nmax, path))) return rc;
+    DevCamera cam = dev_camera(c->cam);
+    DevFilm fd = dev_film(c->film);
+    for (int b0 = ib; b0 < ie; b0 += B) {
+        int nIdx = std::min(B, ie - b0);
+        int nS = nIdx * c->n_work;
+        SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
+        GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB,
+                  path ? c->rng : nullptr, c->dim, c->betaA, c->betaB, c->LA, c->LB};
+        hipEvent_t e0 = ev_start(c, st);
+        HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
+        ev_mark(c, st, ST_GEN, e0);
+        if (!path) {
+            TraceIO tio{c->rayO, c->rayD, nullptr, nS, c->cull ? 1 : 0, c->hitB, c->hitPrim};
+            e0 = ev_start(c, st);
+            HIPCHK(c, launch_trace_closest(st, 0, c->dsc.qcap, c->dsc, tio, c->d_ctr));
+            ev_mark(c, st, ST_TRACE, e0);
+            ShadeRefIO sio = shade_ref_io(c);
+            sio.work_pixels = c->d_work; sio.n_pixels = c->n_work; sio.n_index = nIdx;
+            sio.rayD = c->rayD; sio.lamA = c->lamA; sio.lamB = c->lamB; sio.pdfA = c->pdfA; sio.pdfB = c->pdfB;
+            sio.hitB = c->hitB; sio.hitPrim = c->hitPrim; sio.film = film;
+            e0 = ev_start(c, st);
+            HIPCHK(c, launch_ref_shade_film(st, 0, c->dsc, c->d_spec, fd, sio, c->d_ctr));
+            ev_mark(c, st, ST_FILM, e0);
+        } else {
+            int cur = 0;
+            HIPCHK(c, hipMemcpyAsync(c->d_qcount, &nS, sizeof(int), hipMemcpyHostToDevice, st));
+            for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
+                if (depth == c->integ.max_depth && depth > 0) break;  // that step could only add counters
+                int nxt = cur ^ 1;
+                float4* cO = c->rayO + (size_t)cur * nmax;
+                float4* cD = c->rayD + (size_t)cur * nmax;
+                int* cS = c->slot + (size_t)cur * nmax;
+                HIPCHK(c, hipMemsetAsync(c->d_qcount + nxt, 0, sizeof(int), st));
+                HIPCHK(c, hipMemsetAsync(c->d_qcount + 2, 0, sizeof(int), st));
+                TraceIO tio{cO, cD, c->d_qcount + cur, 0, 0, c->hitB, c->hitPrim};
+                e0 = ev_start(c, st);
+                HIPCHK(c, launch_trace_closest(st, c->grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
+                ev_mark(c, st, ST_TRACE, e0);
+                PathIO pio{};
+                pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = c->d_qcount + cur;
+                pio.hitB = c->hitB; pio.hitPrim = c->hitPrim;
+                pio.nO = c->rayO + (size_t)nxt * nmax; pio.nD = c->rayD + (size_t)nxt * nmax;
+                pio.nSlot = c->slot + (size_t)nxt * nmax; pio.nCount = c->d_qcount + nxt;
+                pio.sO = c->sO; pio.sD = c->sD; pio.sSlot = c->sSlot; pio.sCount = c->d_qcount + 2;
+                pio.rng = c->rng; pio.dim = c->dim; pio.betaA = c->betaA; pio.betaB = c->betaB;
+                pio.LA = c->LA; pio.LB = c->LB; pio.LdA = c->LdA; pio.LdB = c->LdB;
+                pio.lamA = c->lamA; pio.lamB = c->lamB; pio.pdfA = c->pdfA; pio.pdfB = c->pdfB;
+                pio.depth = depth; pio.max_depth = c->integ.max_depth;
+                e0 = ev_start(c, st);
+                HIPCHK(c, launch_path_shade(st, c->grid, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
+                ev_mark(c, st, ST_SHADE, e0);
+                ShadowIO shio{c->sO, c->sD, c->sSlot, c->d_qcount + 2, c->LA, c->LB, c->LdA, c->LdB};
+                e0 = ev_start(c, st);
+                HIPCHK(c, launch_trace_shadow(st, c->grid, c->dsc.qcap, c->dsc, shio, c->d_ctr));
+                ev_mark(c, st, ST_SHADOW, e0);
+                cur = nxt;
+            }
+            PathFilmIO fio{c->d_work, c->n_work, nIdx, c->LA, c->LB, c->lamA, c->lamB, c->pdfA, c->pdfB, film};
+            e0 = ev_start(c, st);
+            HIPCHK(c, launch_path_film(st, 0, c->d_spec, fd, fio, c->d_ctr));
+            ev_mark(c, st, ST_FILM, e0);
+        }
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+// =========================================================================================== C-ABI
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_create(const rt_options* opt, rt_ctx** out) {
+    if (!out) return RT_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return RT_E_NODEVICE;
+    int dev = opt ? opt->device : 0;
+    if (dev < 0 || dev >= ndev) return RT_E_ARG;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return RT_E_HIP;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RT_E_NODEVICE;
+    rt_ctx* c = new rt_ctx();
+    c->device = dev;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return RT_E_HIP;
+    }
+    c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
+    c->hs.init();
+    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 4) != hipSuccess ||
+        dalloc(&c->d_ctr, (size_t)C_NCOUNTERS) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
+        rt_destroy(c);
+        return RT_E_OOM;
+    }
+    DevSpectra ds{};
+    std::memcpy(ds.X, c->hs.X.v.data(), 4 * kSpecN);
+    std::memcpy(ds.Y, c->hs.Y.v.data(), 4 * kSpecN);
+    std::memcpy(ds.Z, c->hs.Z.v.data(), 4 * kSpecN);
+    std::memcpy(ds.D65, c->hs.D65d.v.data(), 4 * kSpecN);
+    ds.f1_n = (int)c->hs.F1.l.size();
+    std::memcpy(ds.f1_lambda, c->hs.F1.l.data(), 4 * ds.f1_n);
+    std::memcpy(ds.f1_value, c->hs.F1.v.data(), 4 * ds.f1_n);
+    hipMemcpy(c->d_spec, &ds, sizeof(ds), hipMemcpyHostToDevice);
+    hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * C_NCOUNTERS);
+    // a20 resolve matrices: XYZFromSensorRGB (WhiteBalance of identical whites, color.h:616-628) and the sRGB
+    // RGBFromXYZ (colorspace.cpp:13-28) — glm float order
+    {
+        auto inv3 = [](const float* a, float* o) {
+            auto m = [&](int col, int row) { return a[col * 3 + row]; };
+            float ood = 1.0f / (+m(0, 0) * (m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) -
+                                m(1, 0) * (m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) +
+                                m(2, 0) * (m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)));
+            o[0] = +(m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) * ood;
+            o[3] = -(m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2)) * ood;
+            o[6] = +(m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1)) * ood;
+            o[1] = -(m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) * ood;
+            o[4] = +(m(0, 0) * m(2, 2) - m(2, 0) * m(0, 2)) * ood;
+            o[7] = -(m(0, 0) * m(2, 1) - m(2, 0) * m(0, 1)) * ood;
+            o[2] = +(m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)) * ood;
+            o[5] = -(m(0, 0) * m(1, 2) - m(1, 0) * m(0, 2)) * ood;
+            o[8] = +(m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1)) * ood;
+        };
+        auto mul3 = [](const float* A, const float* B, float* o) {
+            for (int col = 0; col < 3; ++col)
+                for (int r = 0; r < 3; ++r)
+                    o[col * 3 + r] = (A[0 * 3 + r] * B[col * 3 + 0] + A[1 * 3 + r] * B[col * 3 + 1]) + A[2 * 3 + r] * B[col * 3 + 2];
+        };
+        auto xyz_of = [&](const PLS& s) {
+            float X = inner_product(c->hs.X, s), Y = inner_product(c->hs.Y, s), Z = inner_product(c->hs.Z, s);
+            return F3{X / 106.856895f, Y / 106.856895f, Z / 106.856895f};
+        };
+        auto xyY = [](float x, float y) { return y == 0 ? F3{0, 0, 0} : F3{x * 1.0f / y, 1.0f, (1 - x - y) * 1.0f / y}; };
+        F3 W = xyz_of(c->hs.D65);
+        float wx = W.x / (W.x + W.y + W.z), wy = W.y / (W.x + W.y + W.z);
+        F3 R = xyY((float).64, (float).33), G = xyY((float).3, (float).6), Bp = xyY((float).15, (float).06);
+        float rgb[9] = {R.x, R.y, R.z, G.x, G.y, G.z, Bp.x, Bp.y, Bp.z}, irgb[9];
+        inv3(rgb, irgb);
+        F3 Cw = m3v(irgb, W);
+        float dg[9] = {Cw.x, 0, 0, 0, Cw.y, 0, 0, 0, Cw.z}, xyzFromRgb[9];
+        mul3(rgb, dg, xyzFromRgb);
+        inv3(xyzFromRgb, c->resolveB);
+        float lmsFromXyz[9] = {(float)0.8951, (float)-0.7502, (float)0.0389, (float)0.2664, (float)1.7135,
+                               (float)-0.0685, (float)-0.1614, (float)0.0367, (float)1.0296};
+        float xyzFromLms[9] = {(float)0.986993, (float)0.432305, (float)-0.00852866, (float)-0.147054, (float)0.51836,
+                               (float)0.0400428, (float)0.159963, (float)0.0492912, (float)0.968487};
+        F3 src = xyY(wx, wy), dst = xyY(wx, wy);
+        F3 sl = m3v(lmsFromXyz, src), dl = m3v(lmsFromXyz, dst);
+        float corr[9] = {dl.x / sl.x, 0, 0, 0, dl.y / sl.y, 0, 0, 0, dl.z / sl.z}, t1[9];
+        mul3(xyzFromLms, corr, t1);
+        mul3(t1, lmsFromXyz, c->resolveA);
+        float both[18];
+        std::memcpy(both, c->resolveA, 36);
+        std::memcpy(both + 9, c->resolveB, 36);
+        hipMemcpy(c->d_resolve, both, sizeof(both), hipMemcpyHostToDevice);
+    }
+    *out = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    harvest(c);
+    for (hipEvent_t e : c->pool) hipEventDestroy(e);
+    free_scene(c);
+    free_workspace(c);
+    void* ptrs[] = {c->d_spec, c->d_qcount, c->d_ctr, c->d_resolve, c->d_work, c->d_film};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
+    if (!c || !s) return RT_E_ARG;
+    if (s->n_triangles <= 0 || s->n_vertices <= 0 || !s->positions || !s->indices)
+        return fail(c, RT_E_ARG, "scene needs positions and indices");
+    if (s->cull_backfaces && !s->normals) return fail(c, RT_E_ARG, "back-face culling needs vertex normals");
+    for (int t = 0; t < 3 * s->n_triangles; ++t)
+        if (s->indices[t] >= (uint32_t)s->n_vertices) return fail(c, RT_E_ARG, "triangle index out of range");
+    if (s->tri_material)
+        for (int t = 0; t < s->n_triangles; ++t)
+            if (s->tri_material[t] < 0 || s->tri_material[t] >= std::max(1, s->n_materials))
+                return fail(c, RT_E_ARG, "material id out of range");
+    if (s->n_lights > 1) return fail(c, RT_E_ARG, "one quad light supported in this build (DESIGN.md §Path mode)");
+    if (s->n_lights == 1 && (s->lights[0].material < 0 || s->lights[0].material >= s->n_materials))
+        return fail(c, RT_E_ARG, "light material out of range");
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    free_scene(c);
+    const int nt = s->n_triangles, nv = s->n_vertices;
+    // world vertices: ObjectToRender * vec4(p,1) per vertex (= the per-test transform, Shapes.h:1117-1122)
+    std::vector<F3> wv(nv);
+    for (int i = 0; i < nv; ++i) {
+        float o[4];
+        m4v(s->object_to_render, s->positions[3 * i], s->positions[3 * i + 1], s->positions[3 * i + 2], 1.f, o);
+        wv[i] = {o[0], o[1], o[2]};
+    }
+    std::vector<F3> tri3(3 * (size_t)nt);
+    for (int t = 0; t < nt; ++t)
+        for (int k = 0; k < 3; ++k) tri3[3 * (size_t)t + k] = wv[s->indices[3 * t + k]];
+    // back-face flags (Shapes.h:1339-1380) and degenerate flags (Shapes.h:1131)
+    std::vector<uint8_t> back(nt, 0), degen(nt, 0);
+    c->cull = s->cull_backfaces != 0;
+    F3 look = f3norm({s->cull_look[0], s->cull_look[1], s->cull_look[2]});
+    for (int t = 0; t < nt; ++t) {
+        const F3* p = &tri3[3 * (size_t)t];
+        F3 cr = f3cross(f3sub(p[2], p[0]), f3sub(p[1], p[0]));
+        degen[t] = f3dot(cr, cr) == 0;
+        if (c->cull) {
+            F3 n[3];
+            for (int k = 0; k < 3; ++k) {
+                uint32_t v = s->indices[3 * t + k];
+                n[k] = {s->normals[3 * v], s->normals[3 * v + 1], s->normals[3 * v + 2]};
+            }
+            F3 sum = f3add(f3add(n[0], n[1]), n[2]);
+            F3 N = f3norm({sum.x / 3.0f, sum.y / 3.0f, sum.z / 3.0f});
+            N = f3norm(m3v(s->normal_to_render, N));
+            back[t] = f3dot(look, N) > 0;
+        }
+    }
+    // root bounds: TriModel::Bounds (Shapes.h:1390-1397): object-space min/max (max starts at FLT_MIN, :1292)
+    // then Bounds3::Transform (Shapes.h:60-98, same FLT_MIN quirk)
+    const float FMAX = std::numeric_limits<float>::max(), FMIN = std::numeric_limits<float>::min();
+    F3 omn = {FMAX, FMAX, FMAX}, omx = {FMIN, FMIN, FMIN};
+    for (int i = 0; i < nv; ++i) {
+        const float* p = s->positions + 3 * i;
+        omn = {std::min(omn.x, p[0]), std::min(omn.y, p[1]), std::min(omn.z, p[2])};
+        omx = {std::max(omx.x, p[0]), std::max(omx.y, p[1]), std::max(omx.z, p[2])};
+    }
+    const F3 corners[8] = {{omn.x, omn.y, omn.z}, {omn.x, omx.y, omn.z}, {omn.x, omx.y, omx.z}, {omn.x, omn.y, omx.z},
+                           {omx.x, omx.y, omx.z}, {omx.x, omn.y, omx.z}, {omx.x, omn.y, omn.z}, {omx.x, omx.y, omn.z}};
+    F3 rmn = {FMAX, FMAX, FMAX}, rmx = {FMIN, FMIN, FMIN};
+    for (const F3& q : corners) {
+        float o[4];
+        m4v(s->object_to_render, q.x, q.y, q.z, 1.f, o);
+        rmn = {std::min(rmn.x, o[0]), std::min(rmn.y, o[1]), std::min(rmn.z, o[2])};
+        rmx = {std::max(rmx.x, o[0]), std::max(rmx.y, o[1]), std::max(rmx.z, o[2])};
+    }
+    // octree build (all triangles, culled and degenerate included — the reference inserts every triangle)
+    OctBuild ob;
+    ob.tri3 = &tri3;
+    ob.capacity = s->octree_capacity > 0 ? s->octree_capacity : 40;
+    OctBuild::Node root;
+    root.mn = rmn;
+    root.mx = rmx;
+    ob.nodes.push_back(root);
+    for (int t = 0; t < nt; ++t) ob.add(t);
+    const int nn = (int)ob.nodes.size();
+    // flatten: node SoA + two tile sets
+    std::vector<float4> nA(nn), nB(nn);
+    std::vector<int2> lr0(nn), lr1(nn);
+    std::vector<float4> tiles0, tiles1;
+    c->h_bounds.assign(6 * (size_t)nn, 0.f);
+    c->h_child.assign(nn, -1);
+    c->h_leaf_first.assign(nn, 0);
+    c->h_leaf_count.assign(nn, 0);
+    c->h_refs.clear();
+    auto push_tile = [&](std::vector<float4>& v, int t) {
+        const F3* p = &tri3[3 * (size_t)t];
+        int bits = t;
+        float fid;
+        std::memcpy(&fid, &bits, 4);
+        v.push_back(make_float4(p[0].x, p[0].y, p[0].z, p[1].x));
+        v.push_back(make_float4(p[1].y, p[1].z, p[2].x, p[2].y));
+        v.push_back(make_float4(p[2].z, fid, 0.f, 0.f));
+    };
+    for (int i = 0; i < nn; ++i) {
+        const auto& N = ob.nodes[i];
+        int child = N.first_child;
+        float fc;
+        std::memcpy(&fc, &child, 4);
+        nA[i] = make_float4(N.mn.x, N.mn.y, N.mn.z, fc);
+        nB[i] = make_float4(N.mx.x, N.mx.y, N.mx.z, 0.f);
+        float* b = &c->h_bounds[6 * (size_t)i];
+        b[0] = N.mn.x; b[1] = N.mn.y; b[2] = N.mn.z; b[3] = N.mx.x; b[4] = N.mx.y; b[5] = N.mx.z;
+        c->h_child[i] = child;
+        c->h_leaf_first[i] = (int)c->h_refs.size();
+        c->h_leaf_count[i] = (int)N.tris.size();
+        lr0[i] = make_int2((int)tiles0.size() / 3, 0);
+        lr1[i] = make_int2((int)tiles1.size() / 3, 0);
+        for (int t : N.tris) {
+            c->h_refs.push_back(t);
+            if (degen[t]) continue;
+            push_tile(tiles0, t);
+            lr0[i].y++;
+            if (!back[t]) { push_tile(tiles1, t); lr1[i].y++; }
+        }
+    }
+    // BFS group-queue bound: max over depth d of (#internal nodes at d-1 + #internal nodes at d)
+    std::vector<int> depth(nn, 0), internal_at;
+    int maxd = 0;
+    for (int i = 0; i < nn; ++i) {
+        if (ob.nodes[i].first_child >= 0)
+            for (int k = 0; k < 8; ++k) depth[ob.nodes[i].first_child + k] = depth[i] + 1;
+        maxd = std::max(maxd, depth[i]);
+    }
+    internal_at.assign(maxd + 2, 0);
+    for (int i = 0; i < nn; ++i)
+        if (ob.nodes[i].first_child >= 0) internal_at[depth[i]]++;
+    int bound = 0;
+    for (int d = 0; d <= maxd; ++d) bound = std::max(bound, (d > 0 ? internal_at[d - 1] : 0) + internal_at[d]);
+    int qcap = 1;
+    if (ob.nodes[0].first_child >= 0) {
+        const int caps[] = {16, 64, 256, 1024};
+        qcap = 0;
+        for (int cp : caps)
+            if (cp >= bound) { qcap = cp; break; }
+        if (!qcap) return fail(c, RT_E_LIMIT, "octree BFS frontier bound " + std::to_string(bound) + " exceeds 1024 groups");
+    }
+    c->info.n_nodes = nn;
+    c->info.n_leaf_refs = (int)c->h_refs.size();
+    c->info.max_queue_groups = bound;
+    c->info.depth = maxd;
+    c->n_tris = nt;
+    // per-triangle shading data
+    std::vector<float4> tw(3 * (size_t)nt), tn(3 * (size_t)nt);
+    for (int t = 0; t < nt; ++t)
+        for (int k = 0; k < 3; ++k) {
+            const F3& p = tri3[3 * (size_t)t + k];
+            tw[3 * (size_t)t + k] = make_float4(p.x, p.y, p.z, 0.f);
+            uint32_t v = s->indices[3 * t + k];
+            tn[3 * (size_t)t + k] = s->normals ? make_float4(s->normals[3 * v], s->normals[3 * v + 1], s->normals[3 * v + 2], 0.f)
+                                               : make_float4(0.f, 0.f, 1.f, 0.f);
+        }
+    std::vector<int> tm(nt, 0);
+    if (s->tri_material) tm.assign(s->tri_material, s->tri_material + nt);
+    std::vector<float4> mats;
+    for (int i = 0; i < s->n_materials; ++i)
+        mats.push_back(make_float4(s->materials[i].sigmoid[0], s->materials[i].sigmoid[1], s->materials[i].sigmoid[2],
+                                   s->materials[i].emission_scale));
+    if (mats.empty()) mats.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+    // upload
+    auto up = [&](const void* src, size_t bytes, void** dst) -> int {
+        void* p = nullptr;
+        HIPCHK(c, hipMalloc(&p, std::max<size_t>(bytes, 16)));
+        c->scene_allocs.push_back(p);
+        if (bytes) HIPCHK(c, hipMemcpy(p, src, bytes, hipMemcpyHostToDevice));
+        *dst = p;
+        return RT_OK;
+    };
+    void *pA, *pB, *pl0, *pl1, *pt0, *pt1 = nullptr, *ptw, *ptn, *ptm, *pm;
+    int rc;
+    if ((rc = up(nA.data(), nA.size() * 16, &pA)) || (rc = up(nB.data(), nB.size() * 16, &pB)) ||
+        (rc = up(lr0.data(), lr0.size() * 8, &pl0)) || (rc = up(lr1.data(), lr1.size() * 8, &pl1)) ||
+        (rc = up(tiles0.data(), tiles0.size() * 16, &pt0)) || (rc = up(tiles1.data(), tiles1.size() * 16, &pt1)) ||
+        (rc = up(tw.data(), tw.size() * 16, &ptw)) || (rc = up(tn.data(), tn.size() * 16, &ptn)) ||
+        (rc = up(tm.data(), tm.size() * 4, &ptm)) || (rc = up(mats.data(), mats.size() * 16, &pm)))
+        return rc;
+    DevScene& d = c->dsc;
+    d.nodeA = (const float4*)pA; d.nodeB = (const float4*)pB;
+    d.leafRange[0] = (const int2*)pl0; d.leafRange[1] = (const int2*)pl1;
+    d.tiles[0] = (const float4*)pt0; d.tiles[1] = (const float4*)pt1;
+    d.triWorld = (const float4*)ptw; d.triNormal = (const float4*)ptn;
+    d.triMaterial = (const int*)ptm; d.materials = (const float4*)pm;
+    d.n_nodes = nn;
+    d.qcap = qcap;
+    d.n_lights = s->n_lights;
+    if (s->n_lights == 1) {
+        const rt_quad_light& q = s->lights[0];
+        for (int k = 0; k < 3; ++k) {
+            d.light0.p[k] = q.p[k]; d.light0.e1[k] = q.e1[k]; d.light0.e2[k] = q.e2[k]; d.light0.n[k] = q.n[k];
+        }
+        F3 cr = f3cross({q.e1[0], q.e1[1], q.e1[2]}, {q.e2[0], q.e2[1], q.e2[2]});
+        d.light0.area = std::sqrt(f3dot(cr, cr));
+        d.light0.material = q.material;
+    }
+    c->have_scene = true;
+    return RT_OK;
+}
+
+int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
+    if (!c || !d) return RT_E_ARG;
+    if (d->type != RT_CAMERA_PERSPECTIVE) return fail(c, RT_E_ARG, "only the PerspectiveCamera is supported");
+    c->cam = *d;
+    c->have_cam = true;
+    return RT_OK;
+}
+
+int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
+    if (!c || !d) return RT_E_ARG;
+    if (d->kind != RT_SAMPLER_INDEPENDENT && d->kind != RT_SAMPLER_STRATIFIED) return fail(c, RT_E_ARG, "unknown sampler");
+    if (d->x_samples <= 0 || (d->kind == RT_SAMPLER_STRATIFIED && d->y_samples <= 0))
+        return fail(c, RT_E_ARG, "samples per pixel must be positive");
+    c->smp = *d;
+    c->have_smp = true;
+    return RT_OK;
+}
+
+int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
+    if (!c || !d) return RT_E_ARG;
+    if (d->res_x <= 0 || d->res_y <= 0 || (d->filter != RT_FILTER_BOX && d->filter != RT_FILTER_TRIANGLE))
+        return fail(c, RT_E_ARG, "invalid film");
+    if ((size_t)d->res_x * d->res_y > ((size_t)1 << 27)) return fail(c, RT_E_LIMIT, "film too large");
+    c->film = *d;
+    c->have_film = true;
+    c->work_dirty = true;
+    return RT_OK;
+}
+
+int rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
+    if (!c || !d) return RT_E_ARG;
+    if (d->kind != RT_INTEGRATOR_REFERENCE && d->kind != RT_INTEGRATOR_PATH) return fail(c, RT_E_ARG, "unknown integrator");
+    if (d->max_depth < 0 || d->max_depth > 64) return fail(c, RT_E_ARG, "max_depth out of range");
+    if (d->kind == RT_INTEGRATOR_REFERENCE &&
+        !(d->albedo_rgb[0] == d->albedo_rgb[1] && d->albedo_rgb[1] == d->albedo_rgb[2] && d->albedo_rgb[0] > 0 &&
+          d->albedo_rgb[0] < 1))
+        return fail(c, RT_E_ARG, "reference Li albedo must be a grey in (0,1): the RGB->spectrum table is absent "
+                                 "(color.cpp:114), only the uniform branch color.cpp:35-37 exists");
+    c->integ = *d;
+    c->have_integ = true;
+    return RT_OK;
+}
+
+int rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
+    if (!c || tile_size <= 0 || tile_size % 8 || n_shards <= 0 || shard_id < 0 || shard_id >= n_shards)
+        return c ? fail(c, RT_E_ARG, "invalid shard (tile_size must be a positive multiple of 8)") : RT_E_ARG;
+    c->tile = tile_size;
+    c->n_shards = n_shards;
+    c->shard_id = shard_id;
+    c->work_dirty = true;
+    return RT_OK;
+}
+
+int rt_render_pass_device(rt_ctx* c, int ib, int ie, void* d_film, void* stream) {
+    if (!c || !d_film) return RT_E_ARG;
+    hipSetDevice(c->device);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return render_device(c, ib, ie, (float4*)d_film, st);
+}
+
+int rt_render_pass(rt_ctx* c, int ib, int ie, rt_pixel* film) {
+    if (!c || !film) return RT_E_ARG;
+    int rc = check_ready(c);
+    if (rc) return rc;
+    hipSetDevice(c->device);
+    size_t n = (size_t)c->film.res_x * c->film.res_y;
+    if (c->film_cap < n) {
+        if (c->d_film) hipFree(c->d_film);
+        c->d_film = nullptr;
+        HIPCHK(c, dalloc(&c->d_film, n));
+        c->film_cap = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_film, film, n * 16, hipMemcpyHostToDevice, c->stream));
+    if ((rc = render_device(c, ib, ie, c->d_film, c->stream))) return rc;
+    HIPCHK(c, hipMemcpyAsync(film, c->d_film, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) {
+    if (!c || !film || !out) return RT_E_ARG;
+    if (!c->have_film) return fail(c, RT_E_STATE, "film not set");
+    hipSetDevice(c->device);
+    size_t n = (size_t)c->film.res_x * c->film.res_y;
+    float4* df = nullptr;
+    unsigned char* dout = nullptr;
+    HIPCHK(c, dalloc(&df, n));
+    if (dalloc(&dout, 3 * n) != hipSuccess) { hipFree(df); return fail(c, RT_E_OOM, "resolve buffer"); }
+    int rc = RT_OK;
+    if (hipMemcpy(df, film, n * 16, hipMemcpyHostToDevice) != hipSuccess ||
+        launch_resolve(c->stream, (int)n, df, c->d_resolve, c->d_resolve + 9, dout) != hipSuccess ||
+        hipMemcpyAsync(out, dout, 3 * n, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = fail(c, RT_E_HIP, "resolve failed");
+    hipFree(df);
+    hipFree(dout);
+    return rc;
+}
+
+int rt_get_stats(rt_ctx* c, rt_stats* out) {
+    if (!c || !out) return RT_E_ARG;
+    hipSetDevice(c->device);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipDeviceSynchronize());
+    harvest(c);
+    unsigned long long h[C_NCOUNTERS];
+    HIPCHK(c, hipMemcpy(h, c->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+    rt_stats s = c->stats;
+    s.nodes_tested = (int64_t)h[C_NODES];
+    s.tris_tested = (int64_t)h[C_TRIS];
+    s.hits = (int64_t)h[C_HITS];
+    s.rays = (int64_t)h[C_RAYS];
+    s.shadow_rays = (int64_t)h[C_SHADOW];
+    s.shadow_nodes_tested = (int64_t)h[C_SNODES];
+    s.shadow_tris_tested = (int64_t)h[C_STRIS];
+    s.samples = (int64_t)h[C_SAMPLES];
+    *out = s;
+    return RT_OK;
+}
+
+int rt_reset_stats(rt_ctx* c) {
+    if (!c) return RT_E_ARG;
+    hipSetDevice(c->device);
+    HIPCHK(c, hipDeviceSynchronize());
+    harvest(c);
+    c->stats = rt_stats{};
+    HIPCHK(c, hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * C_NCOUNTERS));
+    return RT_OK;
+}
+
+int rt_octree_get_info(rt_ctx* c, rt_octree_info* out) {
+    if (!c || !out) return RT_E_ARG;
+    if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
+    *out = c->info;
+    return RT_OK;
+}
+
+int rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32_t* leaf_first, int32_t* leaf_count, int32_t* refs) {
+    if (!c) return RT_E_ARG;
+    if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
+    if (bounds) std::memcpy(bounds, c->h_bounds.data(), c->h_bounds.size() * 4);
+    if (child) std::memcpy(child, c->h_child.data(), c->h_child.size() * 4);
+    if (leaf_first) std::memcpy(leaf_first, c->h_leaf_first.data(), c->h_leaf_first.size() * 4);
+    if (leaf_count) std::memcpy(leaf_count, c->h_leaf_count.data(), c->h_leaf_count.size() * 4);
+    if (refs) std::memcpy(refs, c->h_refs.data(), c->h_refs.size() * 4);
+    return RT_OK;
+}
+
+int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_cull, int32_t* prim, float* bt) {
+    if (!c || n < 0 || (n && (!ro || !rd || !prim || !bt))) return RT_E_ARG;
+    if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
+    if (n == 0) return RT_OK;
+    hipSetDevice(c->device);
+    std::vector<float4> o(n), d(n);
+    for (int i = 0; i < n; ++i) {
+        o[i] = make_float4(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2], 0.f);
+        d[i] = make_float4(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2], 0.f);
+    }
+    float4 *dO = nullptr, *dD = nullptr, *dH = nullptr;
+    int* dP = nullptr;
+    int rc = RT_OK;
+    if (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dH, n) || dalloc(&dP, n)) rc = fail(c, RT_E_OOM, "debug trace buffers");
+    if (!rc) {
+        TraceIO io{dO, dD, nullptr, n, (use_cull && c->cull) ? 1 : 0, dH, dP};
+        if (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+            launch_trace_closest(c->stream, 0, c->dsc.qcap, c->dsc, io, c->d_ctr) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(prim, dP, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(bt, dH, 16 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(c, RT_E_HIP, std::string("debug trace: ") + hipGetErrorString(hipGetLastError()));
+    }
+    hipFree(dO); hipFree(dD); hipFree(dH); hipFree(dP);
+    if (!rc)
+        for (int i = 0; i < n; ++i)
+            if (prim[i] < 0) bt[4 * i] = bt[4 * i + 1] = bt[4 * i + 2] = bt[4 * i + 3] = 0.f;
+    return rc;
+}
+
+int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out) {
+    int rc = check_ready(c);
+    if (rc) return rc;
+    if (n < 0 || (n && (!pixel_ids || !indices || !out))) return fail(c, RT_E_ARG, "bad arguments");
+    if (c->integ.kind != RT_INTEGRATOR_REFERENCE) return fail(c, RT_E_ARG, "records are for the reference integrator");
+    if (n == 0) return RT_OK;
+    int npx = c->film.res_x * c->film.res_y;
+    DevSampler smp = dev_sampler(c->smp);
+    for (int i = 0; i < n; ++i) {
+        if (pixel_ids[i] < 0 || pixel_ids[i] >= npx || indices[i] < 0) return fail(c, RT_E_ARG, "sample out of range");
+        if (c->smp.kind == RT_SAMPLER_STRATIFIED && !c->smp.jitter && indices[i] >= smp.spp)
+            return fail(c, RT_E_ARG, "StratifiedSampler without jitter supports indices < SamplesPerPixel");
+    }
+    hipSetDevice(c->device);
+    if ((rc = ensure_workspace(c, (size_t)n, false))) return rc;
+    int *dp = nullptr, *di = nullptr;
+    float* dout = nullptr;
+    static_assert(sizeof(rt_sample_record) == 39 * 4, "record layout");
+    if (dalloc(&dp, n) || dalloc(&di, n) || dalloc(&dout, (size_t)n * 39)) rc = fail(c, RT_E_OOM, "record buffers");
+    if (!rc) {
+        hipMemcpy(dp, pixel_ids, 4 * (size_t)n, hipMemcpyHostToDevice);
+        hipMemcpy(di, indices, 4 * (size_t)n, hipMemcpyHostToDevice);
+        SampleIds ids{nullptr, 1, 0, dp, di};
+        GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB, nullptr, nullptr,
+                  nullptr, nullptr, nullptr, nullptr};
+        DevFilm fd = dev_film(c->film);
+        TraceIO tio{c->rayO, c->rayD, nullptr, n, c->cull ? 1 : 0, c->hitB, c->hitPrim};
+        ShadeRefIO sio = shade_ref_io(c);
+        sio.rayD = c->rayD; sio.lamA = c->lamA; sio.lamB = c->lamB; sio.pdfA = c->pdfA; sio.pdfB = c->pdfB;
+        sio.hitB = c->hitB; sio.hitPrim = c->hitPrim;
+        RecordIO rio{n, c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->hitPrim, dout, 39};
+        if (launch_generate(c->stream, 0, n, ids, dev_camera(c->cam), smp, fd, go) != hipSuccess ||
+            launch_trace_closest(c->stream, 0, c->dsc.qcap, c->dsc, tio, c->d_ctr) != hipSuccess ||
+            launch_records(c->stream, c->dsc, c->d_spec, fd, sio, rio) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(out, dout, sizeof(rt_sample_record) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(c, RT_E_HIP, std::string("debug samples: ") + hipGetErrorString(hipGetLastError()));
+    }
+    hipFree(dp); hipFree(di); hipFree(dout);
+    return rc;
+}
+
+}  // extern "C"

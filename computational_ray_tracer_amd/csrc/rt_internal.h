@@ -1,0 +1,148 @@
+// Internal POD layouts shared by the host C-ABI layer (rt_host.cpp) and the HIP kernels (rt_kernels.hip).
+//
+// HBM layout (see DESIGN.md §Data layout):
+//   octree nodes      : nodeA[n] = float4(pmin.xyz, bits(first_child | -1)), nodeB[n] = float4(pmax.xyz, 0)
+//                       node order = the reference's creation order (Octtree_Model.h:351), children contiguous
+//   leaf ranges       : int2 leafRange[set][n] = (first tile, count); set 0 = all triangles, set 1 = without
+//                       back-facing triangles (TriModel::ComputeBackFace, Shapes.h:1339-1380)
+//   triangle tiles    : 3 float4 per leaf reference, in leaf order: (p0.xyz,p1.x) (p1.yz,p2.xy) (p2.z,bits(id),0,0)
+//                       world space (ObjectToRender applied once, Shapes.h:1117-1122), degenerate ones dropped
+//   per triangle      : triWorld 3 float4, triNormal 3 float4 (object-space vertex normals), triMaterial int
+//   sample streams    : SoA by sample s = i*n_pixels + j (i = index in batch, j = pixel slot in tile order)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtmi {
+
+static const int kSpecN = 471;      // dense spectra 360..830 nm (spectrum.h:17, 380-381)
+static const int kF1Max = 128;      // piecewise F1 entries (81 + 2 padding, spectrum.cpp:134-165)
+
+struct DevSpectra {                 // Spectra::Init products (spectrum.cpp:2612-2634) + colour space illuminant
+    float X[kSpecN], Y[kSpecN], Z[kSpecN], D65[kSpecN];
+    float f1_lambda[kF1Max], f1_value[kF1Max];
+    int f1_n;
+};
+
+struct DevCamera {
+    float r2c[16], c2w[16];         // column-major
+    float lens_radius, focal_distance;
+};
+
+struct DevSampler {
+    int kind, xs, ys, jitter, seed, spp;
+};
+
+struct DevFilm {
+    int res_x, res_y, filter;
+    float rx, ry, imaging_ratio;
+};
+
+struct DevLight {
+    float p[3], e1[3], e2[3], n[3];
+    float area;
+    int material;
+};
+
+struct DevScene {
+    const float4* nodeA;
+    const float4* nodeB;
+    const int2* leafRange[2];
+    const float4* tiles[2];
+    const float4* triWorld;
+    const float4* triNormal;
+    const int* triMaterial;
+    const float4* materials;        // (c0, c1, c2, emission_scale)
+    int n_nodes;
+    int n_lights;
+    DevLight light0;
+    int qcap;
+};
+
+// device counter slots (u64)
+enum { C_NODES = 0, C_TRIS, C_HITS, C_RAYS, C_SHADOW, C_SAMPLES, C_SNODES, C_STRIS, C_NCOUNTERS = 16 };
+
+}  // namespace rtmi
+
+// ---------------------------------------------------------------------------------------------------
+// Kernel I/O descriptors and host launch wrappers (defined in rt_kernels.hip)
+
+namespace rtmi {
+
+struct SampleIds {
+    const int* work_pixels;  // owned pixel ids in tile order
+    int n_pixels;            // pixels per sample index
+    int index_begin;
+    const int* ex_pixel;     // explicit (pixel, index) pairs (parity entry point) or nullptr
+    const int* ex_index;
+};
+
+struct GenOut {
+    float4* rayO; float4* rayD; int* slot;
+    float4* lamA; float4* lamB; float4* pdfA; float4* pdfB;
+    uint4* rng; int* dim;                                 // path-mode sampler state (nullptr in reference mode)
+    float4* betaA; float4* betaB; float4* LA; float4* LB;
+};
+
+struct TraceIO {
+    const float4* rayO; const float4* rayD;
+    const int* count; int n;  // queue length in device memory (count != nullptr) or fixed n
+    int set;                  // tile set: 0 = all triangles, 1 = back-face culled
+    float4* hitB;             // (b0, b1, b2, t)
+    int* hitPrim;
+};
+
+struct ShadeRefIO {
+    const int* work_pixels; int n_pixels; int n_index;
+    const float4* rayD; const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
+    const float4* hitB; const int* hitPrim;
+    float4* film;
+    float albedo_c2, illum_c2, illum_scale;
+};
+
+struct PathIO {
+    const float4* rayO; const float4* rayD; const int* slot; const int* count;
+    const float4* hitB; const int* hitPrim;
+    float4* nO; float4* nD; int* nSlot; int* nCount;
+    float4* sO; float4* sD; int* sSlot; int* sCount;
+    uint4* rng; int* dim; float4* betaA; float4* betaB; float4* LA; float4* LB; float4* LdA; float4* LdB;
+    const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
+    int depth, max_depth;
+};
+
+struct ShadowIO {
+    const float4* sO; const float4* sD; const int* sSlot; const int* sCount;
+    float4* LA; float4* LB; const float4* LdA; const float4* LdB;
+};
+
+struct PathFilmIO {
+    const int* work_pixels; int n_pixels; int n_index;
+    const float4* LA; const float4* LB; const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
+    float4* film;
+};
+
+struct RecordIO {
+    int n;
+    const float4* rayO; const float4* rayD; const float4* lamA; const float4* lamB; const float4* pdfA;
+    const float4* pdfB; const float4* hitB; const int* hitPrim;
+    float* out; int stride;  // rt_sample_record (floats)
+};
+
+hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& ids, const DevCamera& cam,
+                           const DevSampler& smp, const DevFilm& film, const GenOut& out);
+hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
+                                unsigned long long* ctr);
+hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
+                                 const ShadeRefIO& io, unsigned long long* ctr);
+hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
+                          const ShadeRefIO& sio, const RecordIO& io);
+hipError_t launch_path_shade(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevSampler& smp,
+                             const DevFilm& film, const SampleIds& ids, const PathIO& io, unsigned long long* ctr);
+hipError_t launch_trace_shadow(hipStream_t st, int grid, int qcap, const DevScene& sc, const ShadowIO& io,
+                               unsigned long long* ctr);
+hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
+                            unsigned long long* ctr);
+hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* m_xyz_from_sensor,
+                          const float* m_rgb_from_xyz, unsigned char* out);
+
+}  // namespace rtmi

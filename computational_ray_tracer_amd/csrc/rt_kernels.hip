@@ -1,0 +1,526 @@
+// HIP kernels of the MI355X wavefront ray tracer (gfx950, wave64) + their host launch wrappers.
+//
+// Stage map:
+//   k_generate        a1-a8   sampler → wavelengths → filter → thin-lens camera ray (SoA ray / λ / pdf streams)
+//   k_trace_closest   a9-a12  Octtree_Model::Traverse: exact BFS order, shrinking tMax, watertight test
+//   k_ref_shade_film  a13,a16-a19 reference Li + ToSensorRGB + clamp + Film accumulate (pixel-owned, index order)
+//   k_path_shade      a22     build-defined diffuse path step: emission, NEE shadow-ray emit, cosine BSDF sample
+//   k_trace_shadow    a10-a12 any-hit variant for shadow rays (fixed tMax)
+//   k_path_film       a18-a19 sensor + film for path mode
+//   k_resolve         a20     film → sRGB u8
+// Kernels are persistent-style grid-stride loops over wavefront queues whose lengths live in device memory
+// (no host round trip between bounces); ray compaction is wave64 ballot + one atomic per wave.
+#include <hip/hip_runtime.h>
+
+#include "rt_device.h"
+
+namespace rtmi {
+
+static constexpr int kBlock = 256;
+
+// -------------------------------------------------------------------------------- wave helpers
+__device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// Append the `pred` lanes of a wave to a queue: one atomicAdd per wave, slots in lane order.
+// Every lane of the wave must call it.
+__device__ __forceinline__ int wave_append(int* counter, bool pred) {
+    uint64_t mask = __ballot(pred);
+    if (mask == 0) return -1;
+    int leader = __ffsll((unsigned long long)mask) - 1;
+    int base = 0;
+    if (lane_id() == leader) base = atomicAdd(counter, __popcll(mask));
+    base = __shfl(base, leader);
+    int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    return pred ? base + rank : -1;
+}
+
+__device__ __forceinline__ void count_add(unsigned long long* ctr, int slot, unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane_id() == 0 && v) atomicAdd(ctr + slot, v);
+}
+
+__device__ __forceinline__ void sample_of(const SampleIds& ids, int s, int& pixel, int& index) {
+    if (ids.ex_pixel) { pixel = ids.ex_pixel[s]; index = ids.ex_index[s]; return; }
+    int i = s / ids.n_pixels;
+    int j = s - i * ids.n_pixels;
+    pixel = ids.work_pixels[j];
+    index = ids.index_begin + i;
+}
+// RayTracerTestApp.h:289-291 (raster y in [1, resY], a kept quirk)
+__device__ __forceinline__ void pixel_xy(const DevFilm& film, int pixel, int& x, int& y) {
+    x = pixel % film.res_x;
+    y = (int)((float)film.res_y - floorf((float)pixel / (float)film.res_x));
+}
+
+__device__ __forceinline__ void load8(const float4* a, const float4* b, int s, float v[8]) {
+    float4 p = a[s], q = b[s];
+    v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w; v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
+}
+__device__ __forceinline__ void store8(float4* a, float4* b, int s, const float v[8]) {
+    a[s] = make_float4(v[0], v[1], v[2], v[3]);
+    b[s] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// ===================================================================================== K1 generate
+// RayTracerTestApp.h:305-323: StartPixelSample → SampleVisible(Get1D) → filter.Sample(GetPixel2D) →
+// pixel + .5 + p → PerspectiveCamera::generateRay (Cameras.h:273-297) → Ray::Transform (Shapes.h:37-41).
+__global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
+                                                     DevFilm film, GenOut out) {
+    for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nS; s += gridDim.x * blockDim.x) {
+        int pixel, index, x, y;
+        sample_of(ids, s, pixel, index);
+        pixel_xy(film, pixel, x, y);
+        Smp sm;
+        sm.start(smp, x, y, index, 0);
+        float u = sm.get1d(smp);
+        float lam[8], pdf[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // spectrum.h:322-336
+            float up = u + float(i) / 8;
+            if (up > 1) up -= 1;
+            lam[i] = sample_visible_wavelength(up);
+            pdf[i] = visible_pdf(lam[i]);
+        }
+        float u0, u1;
+        sm.get2d(smp, u0, u1);
+        float fx, fy;
+        if (film.filter == 0) { fx = lerpf_(u0, -film.rx, film.rx); fy = lerpf_(u1, -film.ry, film.ry); }
+        else { fx = sample_tent(u0, film.rx); fy = sample_tent(u1, film.ry); }
+        float posx = ((float)x + .5f) + fx, posy = ((float)y + .5f) + fy;
+        float np[4];
+        mat4_mul(cam.r2c, posx, posy, 0.f, 1.f, np);
+        V3 d = vnorm(v3(np[0] / np[3], np[1] / np[3], np[2] / np[3]));
+        V3 o = v3(0, 0, 0);
+        if (cam.lens_radius > 0) {
+            float a0, a1, dx, dy;
+            sm.get2d(smp, a0, a1);
+            disk_concentric(a0, a1, dx, dy);
+            float lx = cam.lens_radius * dx, ly = cam.lens_radius * dy;
+            float ft = cam.focal_distance / d.z;
+            V3 pf = vadd(o, vmul(d, ft));
+            o = v3(lx, ly, 0);
+            d = vnorm(vsub(pf, o));
+        }
+        float wo[4], wd[4];
+        mat4_mul(cam.c2w, o.x, o.y, o.z, 1.f, wo);
+        mat4_mul(cam.c2w, d.x, d.y, d.z, 0.f, wd);
+        float inv = 1.0f / sqrtf((wd[0] * wd[0] + wd[1] * wd[1]) + (wd[2] * wd[2] + wd[3] * wd[3]));  // glm dot vec4
+        out.rayO[s] = make_float4(wo[0], wo[1], wo[2], 0.f);
+        out.rayD[s] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
+        out.slot[s] = s;
+        store8(out.lamA, out.lamB, s, lam);
+        store8(out.pdfA, out.pdfB, s, pdf);
+        if (out.rng) {
+            out.rng[s] = make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
+                                    (uint32_t)(sm.rng.inc >> 32));
+            out.dim[s] = sm.dim;
+            out.betaA[s] = make_float4(1.f, 1.f, 1.f, 1.f);
+            out.betaB[s] = make_float4(1.f, 1.f, 1.f, 1.f);
+            out.LA[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            out.LB[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+
+// ===================================================================================== K2 traverse
+// Octtree_Model.h:66-127 — FIFO BFS.  The 8 children of an internal node are contiguous, so the queue
+// holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
+// reference's node-level FIFO order exactly.  tMax shrinks on every accepted hit ("t < tMax": the first
+// hit found in BFS order wins ties), so hit ids, barycentrics and t are bit-identical to the reference's.
+template <int QCAP, bool ANYHIT>
+__device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0, float& rb1,
+                                        float& rb2, float& rt, unsigned long long& nn, unsigned long long& nt) {
+    V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
+    TriRay R = make_triray(o, d);
+    float tMax = tMaxInit;
+    int best = -1;
+    const int2* __restrict__ lr = sc.leafRange[set];
+    const float4* __restrict__ tiles = sc.tiles[set];
+    int q[QCAP];
+    int head = 0, tail = 0;
+    int n = 0;       // current node
+    int left = 1;    // nodes left in the current group (root: a group of one)
+    while (true) {
+        ++nn;
+        float4 a = sc.nodeA[n];
+        float4 b = sc.nodeB[n];
+        if (box_hit(a, b, o, inv, tMax)) {
+            int child = __float_as_int(a.w);
+            if (child >= 0) {
+                q[tail & (QCAP - 1)] = child;
+                ++tail;
+            } else {
+                int2 r = lr[n];
+                for (int k = 0; k < r.y; ++k) {
+                    const float4* tp = tiles + 3 * (r.x + k);
+                    float4 A = tp[0], B = tp[1], Cc = tp[2];
+                    ++nt;
+                    float b0, b1, b2, t;
+                    if (tri_intersect(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                        best = __float_as_int(Cc.y);
+                        if (ANYHIT) return best;
+                        tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+                    }
+                }
+            }
+        }
+        if (--left > 0) { ++n; continue; }
+        if (head == tail) break;
+        n = q[head & (QCAP - 1)];
+        ++head;
+        left = 8;
+    }
+    return best;
+}
+
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
+    int n = io.count ? *io.count : io.n;
+    unsigned long long nn = 0, nt = 0, nh = 0, nr = 0;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        float4 o4 = io.rayO[k], d4 = io.rayD[k];
+        float b0 = 0, b1 = 0, b2 = 0, t = 0;
+        int prim = traverse<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f, b0,
+                                         b1, b2, t, nn, nt);
+        io.hitB[k] = make_float4(b0, b1, b2, t);
+        io.hitPrim[k] = prim;
+        nh += prim >= 0;
+        nr += 1;
+    }
+    count_add(ctr, C_NODES, nn);
+    count_add(ctr, C_TRIS, nt);
+    count_add(ctr, C_HITS, nh);
+    count_add(ctr, C_RAYS, nr);
+}
+
+// any-hit shadow rays (build-defined path mode): occluded iff some accepting triangle has t < tMax
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) k_trace_shadow(DevScene sc, ShadowIO io, unsigned long long* ctr) {
+    int n = *io.sCount;
+    unsigned long long nn = 0, nt = 0, nr = 0;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        float4 o4 = io.sO[k], d4 = io.sD[k];
+        float b0, b1, b2, t;
+        int hit = traverse<QCAP, true>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, b0, b1, b2, t, nn, nt);
+        if (hit < 0) {
+            int slot = io.sSlot[k];
+            float L[8], Ld[8];
+            load8(io.LA, io.LB, slot, L);
+            load8(io.LdA, io.LdB, slot, Ld);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) L[i] += Ld[i];
+            store8(io.LA, io.LB, slot, L);
+        }
+        nr += 1;
+    }
+    count_add(ctr, C_SNODES, nn);
+    count_add(ctr, C_STRIS, nt);
+    count_add(ctr, C_SHADOW, nr);
+}
+
+// ======================================================================= K3 reference shading + film
+// RayTracerTestApp.h:218-284 (Li, active branch):  0.3·F1(λ) + clamp(n·(0,0,-1), 0, 1)·(D65(λ)·albedo(λ)),
+// n = object-space interpolated normal flipped against the ray (Shapes.h:1066-1075).
+__device__ __forceinline__ void li_reference(const DevScene& sc, const DevSpectra* sp, const ShadeRefIO& io, int s,
+                                             const float lam[8], float L[8]) {
+    int prim = io.hitPrim[s];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) L[i] = 0.f;
+    if (prim < 0) return;
+    float4 bb = io.hitB[s];
+    float4 n1 = sc.triNormal[3 * prim], n2 = sc.triNormal[3 * prim + 1], n3 = sc.triNormal[3 * prim + 2];
+    V3 n = vnorm(vadd(vadd(vmul(v3(n1.x, n1.y, n1.z), bb.x), vmul(v3(n2.x, n2.y, n2.z), bb.y)),
+                      vmul(v3(n3.x, n3.y, n3.z), bb.z)));
+    float4 d4 = io.rayD[s];
+    V3 rd = vnorm(v3(d4.x, d4.y, d4.z));  // TriangleIntersect::rayd (Shapes.h:1259)
+    if (vdot(n, rd) > 0) n = v3(-n.x, -n.y, -n.z);
+    float cosv = gclamp(vdot(n, v3(0, 0, -1)), 0.0f, 1.0f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float light = (io.illum_scale * sigmoid_eval(0, 0, io.illum_c2, lam[i])) * dense_query(sp->D65, lam[i]);
+        float amb = piecewise_query(sp->f1_lambda, sp->f1_value, sp->f1_n, lam[i]) * 0.3f;
+        float mat = sigmoid_eval(0, 0, io.albedo_c2, lam[i]);
+        float r = 0.0f + amb;
+        r += (light * mat) * cosv;
+        L[i] = r;
+    }
+}
+
+// Film accumulation (RayTracerTestApp.h:330-337): each thread owns one pixel and adds the batch's sample
+// indices in increasing order — the same per-pixel summation order as the reference's passes.
+__global__ void __launch_bounds__(kBlock) k_ref_shade_film(DevScene sc, const DevSpectra* sp, DevFilm film,
+                                                           ShadeRefIO io, unsigned long long* ctr) {
+    unsigned long long ns = 0;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < io.n_pixels; j += gridDim.x * blockDim.x) {
+        int pixel = io.work_pixels[j];
+        float4 f = io.film[pixel];
+        for (int i = 0; i < io.n_index; ++i) {
+            int s = i * io.n_pixels + j;
+            float lam[8], pdf[8], L[8], rgb[3];
+            load8(io.lamA, io.lamB, s, lam);
+            load8(io.pdfA, io.pdfB, s, pdf);
+            li_reference(sc, sp, io, s, lam, L);
+            to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
+            const float w = 1.0f;  // FilterSample::weight (Box and Triangle both return 1)
+            f.x += w * gclamp(rgb[0], 0.0f, 1.0f);
+            f.y += w * gclamp(rgb[1], 0.0f, 1.0f);
+            f.z += w * gclamp(rgb[2], 0.0f, 1.0f);
+            f.w += w;
+            ++ns;
+        }
+        io.film[pixel] = f;
+    }
+    count_add(ctr, C_SAMPLES, ns);
+}
+
+__global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, ShadeRefIO sio, RecordIO io) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= io.n) return;
+    float lam[8], pdf[8], L[8], rgb[3];
+    load8(io.lamA, io.lamB, s, lam);
+    load8(io.pdfA, io.pdfB, s, pdf);
+    li_reference(sc, sp, sio, s, lam, L);
+    to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
+    float* r = io.out + (size_t)s * io.stride;
+    for (int i = 0; i < 8; ++i) { r[i] = lam[i]; r[8 + i] = pdf[i]; }
+    float4 o = io.rayO[s], d = io.rayD[s];
+    r[16] = o.x; r[17] = o.y; r[18] = o.z; r[19] = d.x; r[20] = d.y; r[21] = d.z;
+    int prim = io.hitPrim[s];
+    ((int*)r)[22] = prim;
+    float4 hb = prim < 0 ? make_float4(0, 0, 0, 0) : io.hitB[s];
+    r[23] = hb.x; r[24] = hb.y; r[25] = hb.z; r[26] = hb.w;
+    for (int i = 0; i < 8; ++i) r[27 + i] = L[i];
+    for (int c = 0; c < 3; ++c) r[35 + c] = gclamp(rgb[c], 0.0f, 1.0f);
+    r[38] = 1.0f;
+}
+
+// ============================================================================ path mode (build-defined)
+// One bounce of the diffuse path integrator (DESIGN.md §Path mode; pbrt-v4 SimplePathIntegrator semantics):
+// emitter hit → Le at depth 0 only (one-sided), then terminate; otherwise NEE on the quad light (Get2D,
+// shadow ray emitted to the shadow queue with its pending contribution) and a cosine-hemisphere bounce
+// (Get2D, β *= R) emitted to the next queue.  Sampler state (PCG state + dimension) lives per path slot.
+__global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
+                                                       SampleIds ids, PathIO io, unsigned long long* ctr) {
+    const float InvPi = 0.31830988618379067154f;
+    int n = *io.count;
+    for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        int k = base + threadIdx.x;
+        bool wantShadow = false, wantNext = false;
+        float4 sO = make_float4(0, 0, 0, 0), sD = sO, nO = sO, nD = sO;
+        int slot = -1;
+        if (k < n) {
+            slot = io.slot[k];
+            int prim = io.hitPrim[k];
+            if (prim >= 0) {
+                float lam[8], beta[8];
+                load8(io.lamA, io.lamB, slot, lam);
+                load8(io.betaA, io.betaB, slot, beta);
+                float4 P0 = sc.triWorld[3 * prim], P1 = sc.triWorld[3 * prim + 1], P2 = sc.triWorld[3 * prim + 2];
+                V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
+                V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
+                float4 d4 = io.rayD[k];
+                V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
+                float4 mt = sc.materials[sc.triMaterial[prim]];
+                if (mt.w > 0) {
+                    if (io.depth == 0 && vdot(ng, rayd) < 0) {
+                        float L[8];
+                        load8(io.LA, io.LB, slot, L);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.w * dense_query(sp->D65, lam[i]));
+                        store8(io.LA, io.LB, slot, L);
+                    }
+                } else if (io.depth < io.max_depth) {
+                    V3 nrm = ng;
+                    if (vdot(nrm, rayd) > 0) nrm = v3(-nrm.x, -nrm.y, -nrm.z);
+                    float4 hb = io.hitB[k];
+                    V3 p = vadd(vadd(vmul(p0, hb.x), vmul(p1, hb.y)), vmul(p2, hb.z));
+                    float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
+                    V3 po = vadd(p, vmul(nrm, off));
+                    float R[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.x, mt.y, mt.z, lam[i]);
+                    // restore the sampler of this camera sample
+                    int pixel, index, x, y;
+                    sample_of(ids, slot, pixel, index);
+                    pixel_xy(film, pixel, x, y);
+                    Smp sm;
+                    uint4 rs = io.rng[slot];
+                    sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
+                    sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
+                    sm.px = x; sm.py = y; sm.index = index; sm.dim = io.dim[slot];
+                    // --- NEE on the quad light
+                    float u0, u1;
+                    sm.get2d(smp, u0, u1);
+                    if (sc.n_lights > 0) {
+                        const DevLight& Lq = sc.light0;
+                        V3 pl = vadd(vadd(v3(Lq.p[0], Lq.p[1], Lq.p[2]), vmul(v3(Lq.e1[0], Lq.e1[1], Lq.e1[2]), u0)),
+                                     vmul(v3(Lq.e2[0], Lq.e2[1], Lq.e2[2]), u1));
+                        V3 wv = vsub(pl, po);
+                        float dist2 = vdot(wv, wv);
+                        float dist = sqrtf(dist2);
+                        V3 wi = vmul(wv, 1.0f / dist);
+                        float cs = vdot(nrm, wi);
+                        float cl = -vdot(v3(Lq.n[0], Lq.n[1], Lq.n[2]), wi);
+                        if (cs > 0 && cl > 0) {
+                            float le = sc.materials[Lq.material].w;
+                            float G = (cs * cl) / dist2;
+                            float wgt = G * Lq.area;
+                            float Ld[8];
+#pragma unroll
+                            for (int i = 0; i < 8; ++i)
+                                Ld[i] = ((beta[i] * (R[i] * InvPi)) * (le * dense_query(sp->D65, lam[i]))) * wgt;
+                            store8(io.LdA, io.LdB, slot, Ld);
+                            wantShadow = true;
+                            sO = make_float4(po.x, po.y, po.z, 0.f);
+                            sD = make_float4(wi.x, wi.y, wi.z, dist * 0.999f);
+                        }
+                    }
+                    // --- cosine-hemisphere BSDF sample (Sampling.h:449-454), frame = pbrt CoordinateSystem
+                    sm.get2d(smp, u0, u1);
+                    float dx, dy;
+                    disk_concentric(u0, u1, dx, dy);
+                    float z = 1 - dx * dx - dy * dy;
+                    z = sqrtf(z > 0.f ? z : 0.f);  // SafeSqrt: std::max(0.f, x)
+                    if (z != 0) {
+                        float sign = copysignf(1.0f, nrm.z);
+                        float a = -1 / (sign + nrm.z);
+                        float b = nrm.x * nrm.y * a;
+                        V3 ss = v3(1 + sign * (nrm.x * nrm.x) * a, sign * b, -sign * nrm.x);
+                        V3 tt = v3(b, sign + (nrm.y * nrm.y) * a, -nrm.y);
+                        V3 wi = vadd(vadd(vmul(ss, dx), vmul(tt, dy)), vmul(nrm, z));
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) beta[i] *= R[i];
+                        store8(io.betaA, io.betaB, slot, beta);
+                        wantNext = true;
+                        nO = make_float4(po.x, po.y, po.z, 0.f);
+                        nD = make_float4(wi.x, wi.y, wi.z, 0.f);
+                    }
+                    io.rng[slot] = make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), rs.z, rs.w);
+                    io.dim[slot] = sm.dim;
+                }
+            }
+        }
+        int ks = wave_append(io.sCount, wantShadow);
+        if (wantShadow) { io.sO[ks] = sO; io.sD[ks] = sD; io.sSlot[ks] = slot; }
+        int kn = wave_append(io.nCount, wantNext);
+        if (wantNext) { io.nO[kn] = nO; io.nD[kn] = nD; io.nSlot[kn] = slot; }
+    }
+}
+
+// sensor + film for path mode (pixel-owned, index order)
+__global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevFilm film, PathFilmIO io,
+                                                      unsigned long long* ctr) {
+    unsigned long long ns = 0;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < io.n_pixels; j += gridDim.x * blockDim.x) {
+        int pixel = io.work_pixels[j];
+        float4 f = io.film[pixel];
+        for (int i = 0; i < io.n_index; ++i) {
+            int s = i * io.n_pixels + j;
+            float lam[8], pdf[8], L[8], rgb[3];
+            load8(io.lamA, io.lamB, s, lam);
+            load8(io.pdfA, io.pdfB, s, pdf);
+            load8(io.LA, io.LB, s, L);
+            to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
+            const float w = 1.0f;
+            f.x += w * gclamp(rgb[0], 0.0f, 1.0f);
+            f.y += w * gclamp(rgb[1], 0.0f, 1.0f);
+            f.z += w * gclamp(rgb[2], 0.0f, 1.0f);
+            f.w += w;
+            ++ns;
+        }
+        io.film[pixel] = f;
+    }
+    count_add(ctr, C_SAMPLES, ns);
+}
+
+// a20 resolve (RayTracerTestApp.h:437-451): rgbsum/weightsum → XYZFromSensorRGB → RGBFromXYZ → clamp → u8
+__global__ void k_resolve(int n, const float4* film, const float* __restrict__ A, const float* __restrict__ B,
+                          unsigned char* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float4 f = film[i];
+    float s0 = f.x / f.w, s1 = f.y / f.w, s2 = f.z / f.w;
+    float x[3], r[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x[k] = (A[0 * 3 + k] * s0 + A[1 * 3 + k] * s1) + A[2 * 3 + k] * s2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r[k] = (B[0 * 3 + k] * x[0] + B[1 * 3 + k] * x[1]) + B[2 * 3 + k] * x[2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float v = 255.0f * gclamp(r[k], 0.0f, 1.0f);
+        out[3 * i + k] = (v == v) ? (unsigned char)v : 0;
+    }
+}
+
+// ============================================================================== launch wrappers
+static inline int grid_for(int n, int grid) {
+    int g = (n + kBlock - 1) / kBlock;
+    if (grid > 0 && g > grid) g = grid;
+    return g < 1 ? 1 : g;
+}
+
+hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& ids, const DevCamera& cam,
+                           const DevSampler& smp, const DevFilm& film, const GenOut& out) {
+    hipLaunchKernelGGL(k_generate, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
+                                unsigned long long* ctr) {
+    dim3 g(grid_for(io.count ? grid * kBlock : io.n, grid)), b(kBlock);
+    switch (qcap) {
+        case 1: hipLaunchKernelGGL(k_trace_closest<1>, g, b, 0, st, sc, io, ctr); break;
+        case 16: hipLaunchKernelGGL(k_trace_closest<16>, g, b, 0, st, sc, io, ctr); break;
+        case 64: hipLaunchKernelGGL(k_trace_closest<64>, g, b, 0, st, sc, io, ctr); break;
+        case 256: hipLaunchKernelGGL(k_trace_closest<256>, g, b, 0, st, sc, io, ctr); break;
+        case 1024: hipLaunchKernelGGL(k_trace_closest<1024>, g, b, 0, st, sc, io, ctr); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_shadow(hipStream_t st, int grid, int qcap, const DevScene& sc, const ShadowIO& io,
+                               unsigned long long* ctr) {
+    dim3 g(grid > 0 ? grid : 1), b(kBlock);
+    switch (qcap) {
+        case 1: hipLaunchKernelGGL(k_trace_shadow<1>, g, b, 0, st, sc, io, ctr); break;
+        case 16: hipLaunchKernelGGL(k_trace_shadow<16>, g, b, 0, st, sc, io, ctr); break;
+        case 64: hipLaunchKernelGGL(k_trace_shadow<64>, g, b, 0, st, sc, io, ctr); break;
+        case 256: hipLaunchKernelGGL(k_trace_shadow<256>, g, b, 0, st, sc, io, ctr); break;
+        case 1024: hipLaunchKernelGGL(k_trace_shadow<1024>, g, b, 0, st, sc, io, ctr); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
+                                 const ShadeRefIO& io, unsigned long long* ctr) {
+    hipLaunchKernelGGL(k_ref_shade_film, dim3(grid_for(io.n_pixels, grid)), dim3(kBlock), 0, st, sc, sp, film, io, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
+                          const ShadeRefIO& sio, const RecordIO& io) {
+    hipLaunchKernelGGL(k_records, dim3(grid_for(io.n, 0)), dim3(kBlock), 0, st, sc, sp, film, sio, io);
+    return hipGetLastError();
+}
+
+hipError_t launch_path_shade(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevSampler& smp,
+                             const DevFilm& film, const SampleIds& ids, const PathIO& io, unsigned long long* ctr) {
+    hipLaunchKernelGGL(k_path_shade, dim3(grid > 0 ? grid : 1), dim3(kBlock), 0, st, sc, sp, smp, film, ids, io, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
+                            unsigned long long* ctr) {
+    hipLaunchKernelGGL(k_path_film, dim3(grid_for(io.n_pixels, grid)), dim3(kBlock), 0, st, sp, film, io, ctr);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* a, const float* b, unsigned char* out) {
+    hipLaunchKernelGGL(k_resolve, dim3(grid_for(n, 0)), dim3(kBlock), 0, st, n, film, a, b, out);
+    return hipGetLastError();
+}
+
+}  // namespace rtmi

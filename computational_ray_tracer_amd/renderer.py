@@ -1,0 +1,124 @@
+"""Python host mirror of the reference's render loop (RayTracerTestApp::MainLoop, RayTracerTestApp.h:64-513)
+driving the MI355X C-ABI.  `Renderer.render_pass(index_begin, index_end, film)` is the drop-in for one
+ThreadFunction/evaluate_pixel dispatch over every pixel (RayTracerTestApp.h:347-422)."""
+import ctypes as C
+
+import numpy as np
+
+from . import capi
+
+
+class Renderer:
+    """One rt_ctx bound to one GPU.  Configured from a scene.Config (or the individual descriptors)."""
+
+    def __init__(self, cfg=None, device=0):
+        self.lib = capi.load_library()
+        opt = capi.rt_options()
+        opt.device = device
+        h = C.c_void_p()
+        rc = self.lib.rt_create(C.byref(opt), C.byref(h))
+        if rc != capi.RT_OK:
+            raise capi.RTError("rt_create", rc, "no usable gfx950 device" if rc == capi.RT_E_NODEVICE else "")
+        self.h = h
+        self.cfg = None
+        if cfg is not None:
+            self.configure(cfg)
+
+    def _chk(self, name, rc):
+        if rc != capi.RT_OK:
+            raise capi.RTError(name, rc, self.lib.rt_last_error(self.h).decode())
+
+    def configure(self, cfg):
+        self.cfg = cfg
+        self._scene = cfg.model.desc()
+        self._chk("rt_scene_upload", self.lib.rt_scene_upload(self.h, C.byref(self._scene)))
+        self._chk("rt_camera_set", self.lib.rt_camera_set(self.h, C.byref(cfg.camera.desc())))
+        self._chk("rt_sampler_set", self.lib.rt_sampler_set(self.h, C.byref(cfg.sampler.desc())))
+        self._chk("rt_film_set", self.lib.rt_film_set(self.h, C.byref(cfg.film.desc())))
+        self._chk("rt_integrator_set", self.lib.rt_integrator_set(self.h, C.byref(cfg.integrator.desc())))
+        self.res = cfg.film.res
+
+    def set_shard(self, tile_size, n_shards, shard_id):
+        self._chk("rt_set_shard", self.lib.rt_set_shard(self.h, tile_size, n_shards, shard_id))
+
+    def new_film(self):
+        return np.zeros((self.res[0] * self.res[1], 4), dtype=np.float32)
+
+    def render_pass(self, index_begin, index_end, film=None):
+        """Accumulate sample indices [index_begin, index_end) into `film` (host float32 [W*H, 4])."""
+        if film is None:
+            film = self.new_film()
+        assert film.dtype == np.float32 and film.flags.c_contiguous and film.shape == (self.res[0] * self.res[1], 4)
+        self._chk("rt_render_pass", self.lib.rt_render_pass(self.h, index_begin, index_end,
+                                                            film.ctypes.data_as(C.POINTER(capi.rt_pixel))))
+        return film
+
+    def render_pass_device(self, index_begin, index_end, film_ptr, stream_ptr=None):
+        """Accumulate into a device-resident film (e.g. a torch.cuda float32 [W*H, 4] tensor's data_ptr)."""
+        self._chk("rt_render_pass_device", self.lib.rt_render_pass_device(
+            self.h, index_begin, index_end, C.c_void_p(film_ptr), C.c_void_p(stream_ptr or 0)))
+
+    def resolve(self, film):
+        out = np.zeros((self.res[0] * self.res[1], 3), np.uint8)
+        self._chk("rt_film_resolve", self.lib.rt_film_resolve(self.h, np.ascontiguousarray(film, np.float32).ctypes.data_as(
+            C.POINTER(capi.rt_pixel)), out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out
+
+    def stats(self):
+        s = capi.rt_stats()
+        self._chk("rt_get_stats", self.lib.rt_get_stats(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def reset_stats(self):
+        self._chk("rt_reset_stats", self.lib.rt_reset_stats(self.h))
+
+    def octree(self):
+        info = capi.rt_octree_info()
+        self._chk("rt_octree_get_info", self.lib.rt_octree_get_info(self.h, C.byref(info)))
+        n, r = info.n_nodes, info.n_leaf_refs
+        b = np.zeros((n, 6), np.float32)
+        ch, lf, lc = (np.zeros(n, np.int32) for _ in range(3))
+        refs = np.zeros(max(r, 1), np.int32)
+        P = lambda a, t: a.ctypes.data_as(C.POINTER(t))
+        self._chk("rt_octree_export", self.lib.rt_octree_export(self.h, P(b, C.c_float), P(ch, C.c_int32), P(lf, C.c_int32),
+                                                                P(lc, C.c_int32), P(refs, C.c_int32)))
+        return dict(bounds=b, child=ch, leaf_first=lf, leaf_count=lc, refs=refs[:r], depth=info.depth,
+                    max_queue_groups=info.max_queue_groups)
+
+    def trace(self, ro, rd, use_cull=True):
+        ro = np.ascontiguousarray(ro, np.float32)
+        rd = np.ascontiguousarray(rd, np.float32)
+        n = len(ro)
+        prim = np.zeros(n, np.int32)
+        bt = np.zeros((n, 4), np.float32)
+        P = lambda a, t: a.ctypes.data_as(C.POINTER(t))
+        self._chk("rt_debug_trace", self.lib.rt_debug_trace(self.h, n, P(ro, C.c_float), P(rd, C.c_float), int(use_cull),
+                                                            P(prim, C.c_int32), P(bt, C.c_float)))
+        return prim, bt
+
+    def samples(self, pixel_ids, indices):
+        pixel_ids = np.ascontiguousarray(pixel_ids, np.int32)
+        indices = np.ascontiguousarray(indices, np.int32)
+        out = (capi.rt_sample_record * len(pixel_ids))()
+        P = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))
+        self._chk("rt_debug_samples", self.lib.rt_debug_samples(self.h, len(pixel_ids), P(pixel_ids), P(indices), out))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def records_to_arrays(recs):
+    """rt_sample_record array -> dict of numpy arrays (for bit-exact comparisons)."""
+    raw = np.frombuffer(bytes(recs), dtype=np.float32).reshape(len(recs), 39)
+    return dict(lam=raw[:, 0:8], pdf=raw[:, 8:16], ro=raw[:, 16:19], rd=raw[:, 19:22],
+                prim=raw[:, 22].view(np.int32), b=raw[:, 23:26], t=raw[:, 26], L=raw[:, 27:35], rgb=raw[:, 35:38],
+                weight=raw[:, 38])

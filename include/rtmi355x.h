@@ -1,0 +1,204 @@
+/* =====================================================================================================
+ * rtmi355x.h — the drop-in C-ABI of the MI355X ray-tracing inner loop (librtmi355x.so).
+ *
+ * Replaces the in-process per-pass block of the reference application
+ *     RayTracerTestApp::MainLoop  →  ThreadFunction / evaluate_pixel dispatch + wait
+ *     (Applications/RayTracerTestApp.h:287-422)
+ * which samples (sampler), generates camera rays (CameraBase::generateRay, Cameras.h:179/273-297),
+ * traverses the triangle octree (Octtree_Model::Traverse, Octtree_Model.h:66-127), shades (Li lambda,
+ * RayTracerTestApp.h:218-284) and accumulates sensor RGB into the Film (Film.h:11-20, :336-337).
+ *
+ * Plain C: pointers and sizes only.  All descriptors are deep-copied at upload; the caller owns every
+ * buffer.  Every entry point returns 0 (RT_OK) or a negative rt_status and sets rt_last_error().
+ * No C++ exception crosses this boundary.  One rt_ctx per host thread (calls on a context are
+ * serialised by the caller).  The library needs an MI355X (gfx950): rt_create fails with
+ * RT_E_NODEVICE when none is present — there is no CPU fallback.
+ * ===================================================================================================*/
+#ifndef RTMI355X_H
+#define RTMI355X_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum {
+    RT_OK = 0,
+    RT_E_ARG = -1,      /* invalid argument / descriptor                                   */
+    RT_E_HIP = -2,      /* HIP runtime error (message in rt_last_error)                    */
+    RT_E_RCCL = -3,     /* reserved: collectives run in the caller (torch.distributed)     */
+    RT_E_OOM = -4,      /* device allocation failed                                        */
+    RT_E_STATE = -5,    /* call order: scene/camera/sampler/film not set                   */
+    RT_E_NODEVICE = -6, /* no gfx950 device visible                                        */
+    RT_E_LIMIT = -7     /* scene exceeds a compiled limit (e.g. BFS queue bound)           */
+} rt_status;
+
+typedef struct rt_ctx rt_ctx;
+
+typedef struct {
+    int device;        /* HIP device ordinal                                              */
+    int reserved[7];
+} rt_options;
+
+/* Film pixel, layout-identical to `pixel {glm::vec3 rgbsum; float weightsum;}` (Film.h:6-9). */
+typedef struct { float r, g, b, w; } rt_pixel;
+
+enum { RT_MAT_DIFFUSE = 0 };
+/* Build-defined material (the reference has none: Shading.h:1-21 is a comment stub).
+ * Reflectance is an RGBSigmoidPolynomial (color.h:363-403): R(λ) = s(c0 λ² + c1 λ + c2).
+ * emission_scale > 0 makes the triangle a pure one-sided emitter with Le = scale · stdillum-D65. */
+typedef struct {
+    int type;
+    float sigmoid[3];
+    float emission_scale;
+} rt_material;
+
+/* Build-defined quad area light (Lights.h:1-10 is a comment stub): x = p + u·e1 + v·e2, normal n. */
+typedef struct {
+    float p[3], e1[3], e2[3], n[3];
+    int material;
+} rt_quad_light;
+
+/* TriModel + Octtree_Model inputs (Shapes.h:1272-1491, Octtree_Model.h:33-63). */
+typedef struct {
+    int n_vertices;
+    const float* positions;          /* object space, 3 floats per vertex (MeshCache::Mesh::positions) */
+    const float* normals;            /* object space vertex normals (MeshCache::Mesh::normals)        */
+    int n_triangles;
+    const uint32_t* indices;         /* 3 per triangle                                                 */
+    float object_to_render[16];      /* column-major; = rigidtransform * permutation_y_z (Shapes.h:180) */
+    float normal_to_render[9];       /* column-major mat3(transpose(inverse(ObjectToRender))) (:1364)   */
+    int cull_backfaces;              /* TriModel::ComputeBackFace(look, enable) (Shapes.h:1339-1380)    */
+    float cull_look[3];
+    int octree_capacity;             /* TRIANGLE_CAPACITY (Octtree_Model.h:388); 0 -> 40                */
+    const int32_t* tri_material;     /* per triangle material id, NULL -> 0 (path integrator only)     */
+    int n_materials;
+    const rt_material* materials;
+    int n_lights;
+    const rt_quad_light* lights;
+} rt_scene_desc;
+
+enum { RT_CAMERA_PERSPECTIVE = 0 };
+/* The values CameraBase already holds (Cameras.h:190-210); generateRay = Cameras.h:273-297. */
+typedef struct {
+    int type;
+    float raster_to_camera[16];      /* column-major M_RastertoCamera */
+    float camera_to_world[16];       /* column-major M_CameratoWorld  */
+    float lens_radius;
+    float focal_distance;
+} rt_camera_desc;
+
+enum { RT_SAMPLER_INDEPENDENT = 0, RT_SAMPLER_STRATIFIED = 1 };
+/* pbrt::IndependentSampler(spp, seed) (samplers.h:38-62): x_samples = spp, y_samples ignored.
+ * pbrt::StratifiedSampler(x, y, jitter, seed) (samplers.h:66-136). */
+typedef struct {
+    int kind;
+    int x_samples, y_samples;
+    int jitter;
+    int seed;
+} rt_sampler_desc;
+
+enum { RT_FILTER_BOX = 0, RT_FILTER_TRIANGLE = 1 };
+/* Film (Film.h:11-20) + its filter (filters.h:66-93 Box, 267-296 Triangle with a deterministic coin)
+ * + XYZ PixelSensor (pixelsensor.h:70-87). */
+typedef struct {
+    int res_x, res_y;
+    int filter;
+    float filter_radius[2];
+    float imaging_ratio;             /* 1/CIE_Y_integral in the reference app (RayTracerTestApp.h:149) */
+} rt_film_desc;
+
+enum { RT_INTEGRATOR_REFERENCE = 0, RT_INTEGRATOR_PATH = 1 };
+/* RT_INTEGRATOR_REFERENCE: the Li lambda of RayTracerTestApp.h:218-284 (ambient 0.3·F1 +
+ *   clamp(n·(0,0,-1))·D65·albedo), octree back-face culling honoured.
+ * RT_INTEGRATOR_PATH: build-defined diffuse path tracer with next-event estimation on quad lights
+ *   (Integrator.h:1-14 is a stub; semantics in DESIGN.md §Path mode). */
+typedef struct {
+    int kind;
+    int max_depth;
+    float albedo_rgb[3];             /* reference Li material colour (grey: color.cpp:35-37 branch) */
+} rt_integrator_desc;
+
+typedef struct {
+    int64_t samples;                 /* camera samples evaluated                         */
+    int64_t rays;                    /* closest-hit rays traced                          */
+    int64_t shadow_rays;             /* any-hit rays traced                              */
+    int64_t nodes_tested;            /* octree node box tests by closest-hit rays        */
+    int64_t tris_tested;             /* triangle tests by closest-hit rays               */
+    int64_t shadow_nodes_tested;     /* node box tests by any-hit (shadow) rays          */
+    int64_t shadow_tris_tested;      /* triangle tests by any-hit (shadow) rays          */
+    int64_t hits;                    /* closest-hit rays that hit                        */
+    double ms_generate, ms_trace, ms_shade, ms_shadow, ms_film;  /* HIP-event kernel time */
+    int64_t launches_trace;          /* closest-hit trace launches (per-launch averages) */
+    int64_t launches_shadow;         /* any-hit trace launches                           */
+} rt_stats;
+
+/* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */
+typedef struct {
+    float lambda[8], pdf[8];
+    float ro[3], rd[3];
+    int32_t prim;
+    float b[3], t;
+    float L[8];
+    float rgb[3];
+    float weight;
+} rt_sample_record;
+
+/* Flattened octree as uploaded (node order = reference creation order, Octtree_Model.h:351). */
+typedef struct {
+    int n_nodes;
+    int n_leaf_refs;
+    int max_queue_groups;            /* host-computed bound of the BFS group queue       */
+    int depth;
+} rt_octree_info;
+
+/* ---- lifecycle ---------------------------------------------------------------------------------- */
+int rt_create(const rt_options* opt, rt_ctx** out);
+void rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+int rt_abi_version(void);
+
+/* ---- configuration (each deep-copies its descriptor) -------------------------------------------- */
+int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene);
+int rt_camera_set(rt_ctx* ctx, const rt_camera_desc* cam);
+int rt_sampler_set(rt_ctx* ctx, const rt_sampler_desc* smp);
+int rt_film_set(rt_ctx* ctx, const rt_film_desc* film);
+int rt_integrator_set(rt_ctx* ctx, const rt_integrator_desc* integ);
+/* Pixel-tile sharding for multi-GPU: this context renders tiles t with t % n_shards == shard_id
+ * (tile_size x tile_size pixel tiles in row-major tile order).  Default: one shard. */
+int rt_set_shard(rt_ctx* ctx, int tile_size, int n_shards, int shard_id);
+
+/* ---- the hot path ----------------------------------------------------------------------------- */
+/* Accumulate (+=) sample indices [index_begin, index_end) of every owned pixel into film_inout
+ * (res_x*res_y rt_pixel, host memory), index-ordered per pixel exactly as the reference's passes
+ * (RayTracerTestApp.h:336-337, 420-422).  Blocks until done. */
+int rt_render_pass(rt_ctx* ctx, int index_begin, int index_end, rt_pixel* film_inout);
+/* Same, into a device-resident film (res_x*res_y rt_pixel in HBM) on the given hipStream_t
+ * (NULL = the context's stream).  Returns after enqueueing; the caller synchronises. */
+int rt_render_pass_device(rt_ctx* ctx, int index_begin, int index_end, void* d_film, void* hip_stream);
+
+/* a20 resolve (RayTracerTestApp.h:424-452): rgbsum/weightsum -> XYZFromSensorRGB -> sRGB -> clamp -> u8. */
+int rt_film_resolve(rt_ctx* ctx, const rt_pixel* film, uint8_t* rgb_out);
+
+/* ---- instrumentation ---------------------------------------------------------------------------- */
+int rt_get_stats(rt_ctx* ctx, rt_stats* out);
+int rt_reset_stats(rt_ctx* ctx);
+int rt_octree_get_info(rt_ctx* ctx, rt_octree_info* out);
+/* Copy out the flattened octree: node_bounds[6*n] (pmin,pmax), node_child[n] (first child or -1),
+ * node_leaf_first[n], node_leaf_count[n], leaf_refs[n_leaf_refs] (triangle ids incl. culled ones). */
+int rt_octree_export(rt_ctx* ctx, float* node_bounds, int32_t* node_child, int32_t* node_leaf_first,
+                     int32_t* node_leaf_count, int32_t* leaf_refs);
+
+/* ---- parity entry points (same kernels as the hot path, stage outputs exposed) ------------------ */
+/* K2 alone: closest hit of n world-space rays (ro, rd: 3n floats).  prim[n] (-1 = miss),
+ * bt[4n] = (b0, b1, b2, t).  use_cull follows the reference's back-face flags. */
+int rt_debug_trace(rt_ctx* ctx, int n, const float* ro, const float* rd, int use_cull, int32_t* prim, float* bt);
+/* K1..K3 for n explicit (pixel_id, index) samples (reference integrator). */
+int rt_debug_samples(rt_ctx* ctx, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTMI355X_H */

@@ -1,0 +1,967 @@
+// =====================================================================================================
+//  rtcore — ORACLE.  TEST INFRASTRUCTURE ONLY.
+//
+//  A plain, scalar, AoS C++ restatement of the reference's Monte Carlo ray-tracing inner loop
+//  (GiboDidact/Computational_ray_tracer).  Every function cites the reference file:line it follows.
+//  It is the parity checker for the HIP product path (computational_ray_tracer_amd/) and the
+//  `cpu_baseline` leg of bench.py.  Nothing in the product may include, link or call this file.
+//
+//  Parity status: the reference cannot be compiled here (MSVC-only C++,
+//  glm/assimp/GLFW absent — SURVEY.md §8c), so this restatement is pinned by known-answer tests
+//  (tests/test_oracle_known_answers.py) and by golden fixtures it generated (tests/golden/).
+//  glm operation order is restated explicitly (glm itself is not vendored: parity is unpinned at the
+//  glm boundary).  Transcendentals (cos/sin/atanh/cosh) are evaluated in double and
+//  rounded to float on BOTH sides, a documented build choice (reference calls the float overloads).
+//
+//  Compile with -ffp-contract=off: FMA only where the reference calls std::fma.
+// =====================================================================================================
+#pragma once
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <queue>
+#include <vector>
+
+#include "../computational_ray_tracer_amd/data/spectra_data.h"
+
+namespace rtcore {
+
+// ---------------------------------------------------------------- constants (pch.h:39-46)
+static const float OneMinusEpsilon = 1.0f - std::numeric_limits<float>::min();  // == 1.0f (quirk)
+static const float Pi = 3.14159265358979323846f;
+static const float InvPi = 0.31830988618379067154f;
+static const float PiOver2 = 1.57079632679489661923f;
+static const float PiOver4 = 0.78539816339744830961f;
+static const float CIE_Y_integral = 106.856895f;  // spectrum.h:21
+static const int NSpectrumSamples = 8;             // spectrum.h:19
+
+// helpers.h:50-54 — MachineEpsilon is formed in double then stored as float; gamma(n) in float
+static inline float MachineEpsilon() { return (float)((double)std::numeric_limits<float>::epsilon() * 0.5); }
+static inline float gamma_(int n) {
+    float me = MachineEpsilon();
+    return ((float)n * me) / (1.0f - (float)n * me);
+}
+
+// ------------------------------------------------ transcendentals (documented build choice)
+static inline float cos_f(float x) { return (float)std::cos((double)x); }
+static inline float sin_f(float x) { return (float)std::sin((double)x); }
+static inline float atanh_f(float x) { return (float)std::atanh((double)x); }
+static inline float cosh_f(float x) { return (float)std::cosh((double)x); }
+
+// ------------------------------------------------------------------------- glm restatement
+struct vec2 { float x, y; };
+struct vec3 {
+    float x, y, z;
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+};
+struct vec4 { float x, y, z, w; };
+struct mat4 { float m[16]; };   // column-major: m[col*4+row] (glm layout)
+struct mat3 { float m[9]; };    // column-major
+
+static inline vec3 add(vec3 a, vec3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static inline vec3 sub(vec3 a, vec3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static inline vec3 mul(vec3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+// glm compute_dot<vec3>: tmp = a*b; (tmp.x + tmp.y) + tmp.z
+static inline float dot(vec3 a, vec3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+// glm compute_dot<vec4>: (tmp.x + tmp.y) + (tmp.z + tmp.w)
+static inline float dot4(vec4 a, vec4 b) { return (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w); }
+// glm::cross
+static inline vec3 cross(vec3 a, vec3 b) {
+    return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+}
+// glm::normalize = v * inversesqrt(dot(v,v)), inversesqrt(x) = 1/sqrt(x)
+static inline vec3 normalize(vec3 v) { float s = 1.0f / std::sqrt(dot(v, v)); return mul(v, s); }
+static inline vec4 normalize4(vec4 v) {
+    float s = 1.0f / std::sqrt(dot4(v, v));
+    return {v.x * s, v.y * s, v.z * s, v.w * s};
+}
+// glm mat4*vec4: Add2 = (m0*x + m1*y) + (m2*z + m3*w)
+static inline vec4 mul(const mat4& M, vec4 v) {
+    float o[4];
+    for (int r = 0; r < 4; ++r) {
+        float a0 = M.m[0 * 4 + r] * v.x, a1 = M.m[1 * 4 + r] * v.y;
+        float a2 = M.m[2 * 4 + r] * v.z, a3 = M.m[3 * 4 + r] * v.w;
+        o[r] = (a0 + a1) + (a2 + a3);
+    }
+    return {o[0], o[1], o[2], o[3]};
+}
+// glm mat3*vec3: (m0*x + m1*y) + m2*z
+static inline vec3 mul(const mat3& M, vec3 v) {
+    float o[3];
+    for (int r = 0; r < 3; ++r) o[r] = (M.m[0 * 3 + r] * v.x + M.m[1 * 3 + r] * v.y) + M.m[2 * 3 + r] * v.z;
+    return {o[0], o[1], o[2]};
+}
+// glm::max/min scalar: max(x,y) = (x < y) ? y : x ; min(x,y) = (y < x) ? y : x ; clamp = min(max(x,lo),hi)
+static inline float gmax(float x, float y) { return (x < y) ? y : x; }
+static inline float gmin(float x, float y) { return (y < x) ? y : x; }
+static inline float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
+
+// helpers.h:56-62 DifferenceOfProducts (the one place the path uses FMA)
+static inline float DifferenceOfProducts(float a, float b, float c, float d) {
+    float cd = c * d;
+    float dop = std::fmaf(a, b, -cd);
+    float err = std::fmaf(-c, d, cd);
+    return dop + err;
+}
+// helpers.h:64-71
+static inline int MaxComponentIndex(vec3 t) { return (t.x > t.y) ? ((t.x > t.z) ? 0 : 2) : ((t.y > t.z) ? 1 : 2); }
+static inline float MaxComponentValue(vec3 t) {  // std::max({x,y,z}) keeps the first largest
+    float m = t.x;
+    if (m < t.y) m = t.y;
+    if (m < t.z) m = t.z;
+    return m;
+}
+// helpers.h:154-157
+static inline float Lerp(float x, float a, float b) { return (1 - x) * a + x * b; }
+// helpers.h:159-172
+template <typename P>
+static inline size_t FindInterval(size_t sz, const P& pred) {
+    long size = (long)sz - 2, first = 1;
+    while (size > 0) {
+        size_t half = (size_t)size >> 1, middle = first + half;
+        bool r = pred((int)middle);
+        first = r ? (long)middle + 1 : first;
+        size = r ? size - (long)(half + 1) : (long)half;
+    }
+    long v = first - 1;
+    long hi = (long)sz - 2;
+    return (size_t)(v < 0 ? 0 : (v > hi ? hi : v));
+}
+
+// =============================================================== hashing / RNG (integer exact)
+// hash.h:18-63
+static inline uint64_t MurmurHash64A(const unsigned char* key, size_t len, uint64_t seed) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    const int r = 47;
+    uint64_t h = seed ^ (len * m);
+    const unsigned char* end = key + 8 * (len / 8);
+    while (key != end) {
+        uint64_t k;
+        std::memcpy(&k, key, 8);
+        key += 8;
+        k *= m; k ^= k >> r; k *= m;
+        h ^= k; h *= m;
+    }
+    switch (len & 7) {
+        case 7: h ^= uint64_t(key[6]) << 48; [[fallthrough]];
+        case 6: h ^= uint64_t(key[5]) << 40; [[fallthrough]];
+        case 5: h ^= uint64_t(key[4]) << 32; [[fallthrough]];
+        case 4: h ^= uint64_t(key[3]) << 24; [[fallthrough]];
+        case 3: h ^= uint64_t(key[2]) << 16; [[fallthrough]];
+        case 2: h ^= uint64_t(key[1]) << 8; [[fallthrough]];
+        case 1: h ^= uint64_t(key[0]); h *= m;
+    }
+    h ^= h >> r; h *= m; h ^= h >> r;
+    return h;
+}
+// hash.h:67-74 / HelperFunctions.h:137-144
+static inline uint64_t MixBits(uint64_t v) {
+    v ^= (v >> 31); v *= 0x7fb5d329728ea185ull;
+    v ^= (v >> 27); v *= 0x81dadef4bc2dd44dull;
+    v ^= (v >> 33);
+    return v;
+}
+// hash.h:96-104 — Hash(ivec2 p, int seed): 12-byte packed key; Hash(ivec2 p, int dim, int seed): 16 bytes
+static inline uint64_t Hash(int px, int py, int seed) {
+    unsigned char buf[16];
+    std::memcpy(buf + 0, &px, 4); std::memcpy(buf + 4, &py, 4); std::memcpy(buf + 8, &seed, 4);
+    return MurmurHash64A(buf, 12, 0);
+}
+static inline uint64_t Hash(int px, int py, int dim, int seed) {
+    unsigned char buf[16];
+    std::memcpy(buf + 0, &px, 4); std::memcpy(buf + 4, &py, 4);
+    std::memcpy(buf + 8, &dim, 4); std::memcpy(buf + 12, &seed, 4);
+    return MurmurHash64A(buf, 16, 0);
+}
+// HelperFunctions.h:175-203
+static inline int PermutationElement(uint32_t i, uint32_t l, uint32_t p) {
+    uint32_t w = l - 1;
+    w |= w >> 1; w |= w >> 2; w |= w >> 4; w |= w >> 8; w |= w >> 16;
+    do {
+        i ^= p; i *= 0xe170893du; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8; i *= 0x0929eb3fu;
+        i ^= p >> 23; i ^= (i & w) >> 1; i *= 1u | p >> 27; i *= 0x6935fa69u; i ^= (i & w) >> 11;
+        i *= 0x74dcb303u; i ^= (i & w) >> 2; i *= 0x9e501cc3u; i ^= (i & w) >> 2; i *= 0xc860a3dfu;
+        i &= w; i ^= i >> 5;
+    } while (i >= l);
+    return (int)((i + p) % l);
+}
+
+// rng.h:19-144 — PCG32
+struct RNG {
+    static constexpr uint64_t DefaultState = 0x853c49e6748fea9bull;
+    static constexpr uint64_t DefaultStream = 0xda3e39cb94b95bdbull;
+    static constexpr uint64_t Mult = 0x5851f42d4c957f2dull;
+    uint64_t state = DefaultState, inc = DefaultStream;
+
+    uint32_t UniformU32() {  // rng.h:76-82
+        uint64_t old = state;
+        state = old * Mult + inc;
+        uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+    }
+    void SetSequence(uint64_t seqIndex, uint64_t seed) {  // rng.h:113-119
+        state = 0u;
+        inc = (seqIndex << 1u) | 1u;
+        UniformU32();
+        state += seed;
+        UniformU32();
+    }
+    void SetSequence(uint64_t seqIndex) { SetSequence(seqIndex, MixBits(seqIndex)); }  // rng.h:36-39
+    float UniformF() {  // rng.h:122-124 (OneMinusEpsilon == 1.0f, so the min is a no-op)
+        float v = (float)UniformU32() * 0x1p-32f;
+        return std::min<float>(OneMinusEpsilon, v);
+    }
+    void Advance(int64_t idelta) {  // rng.h:131-144
+        uint64_t curMult = Mult, curPlus = inc, accMult = 1u, accPlus = 0u, delta = (uint64_t)idelta;
+        while (delta > 0) {
+            if (delta & 1) { accMult *= curMult; accPlus = accPlus * curMult + curPlus; }
+            curPlus = (curMult + 1) * curPlus;
+            curMult *= curMult;
+            delta /= 2;
+        }
+        state = accMult * state + accPlus;
+    }
+};
+
+// ============================================================================== samplers
+// samplers.h:38-62 IndependentSampler ; samplers.h:66-136 StratifiedSampler
+struct Sampler {
+    int kind = 1;  // 0 = Independent, 1 = Stratified
+    int xPixelSamples = 1, yPixelSamples = 1, seed = 0;
+    bool jitter = false;
+    RNG rng;
+    int px = 0, py = 0, sampleIndex = 0, dimension = 0;
+
+    int SamplesPerPixel() const { return kind == 0 ? xPixelSamples : xPixelSamples * yPixelSamples; }
+    // returns false where the reference prints "more sampels than pixels for strat" and keeps stale state
+    bool StartPixelSample(int x, int y, int index, int dim) {
+        if (kind == 1 && jitter == false && index >= SamplesPerPixel()) return false;  // samplers.h:83-87
+        px = x; py = y; sampleIndex = index; dimension = dim;
+        rng.SetSequence(Hash(x, y, seed));
+        rng.Advance((int64_t)((uint64_t)index * 65536ull + (uint64_t)dim));
+        return true;
+    }
+    float Get1D() {
+        if (kind == 0) return rng.UniformF();
+        uint64_t hash = Hash(px, py, dimension, seed);                                     // samplers.h:98
+        int stratum = PermutationElement((uint32_t)sampleIndex, (uint32_t)SamplesPerPixel(), (uint32_t)hash);
+        ++dimension;
+        float delta = jitter ? rng.UniformF() : 0.5f;
+        return ((float)stratum + delta) / (float)SamplesPerPixel();
+    }
+    vec2 Get2D() {
+        if (kind == 0) { float a = rng.UniformF(); float b = rng.UniformF(); return {a, b}; }
+        if (sampleIndex >= SamplesPerPixel()) return {0, 0};                                // samplers.h:109-112
+        uint64_t hash = Hash(px, py, dimension, seed);
+        int stratum = PermutationElement((uint32_t)sampleIndex, (uint32_t)SamplesPerPixel(), (uint32_t)hash);
+        dimension += 2;
+        int x = stratum % xPixelSamples, y = stratum / xPixelSamples;
+        float dx = jitter ? rng.UniformF() : 0.5f;
+        float dy = jitter ? rng.UniformF() : 0.5f;
+        return {((float)x + dx) / (float)xPixelSamples, ((float)y + dy) / (float)yPixelSamples};
+    }
+    vec2 GetPixel2D() { return Get2D(); }
+};
+
+// ============================================================================ sampling
+// Sampling.h:63-67
+static inline float VisibleWavelengthsPDF(float lambda) {
+    if (lambda < 360 || lambda > 830) return 0;
+    float c = cosh_f(0.0072f * (lambda - 538));
+    return (float)((double)0.0039398042f / ((double)c * (double)c));
+}
+// Sampling.h:69-71
+static inline float SampleVisibleWavelengths(float u) {
+    return 538 - 138.888889f * atanh_f(0.85691062f - 1.82750197f * u);
+}
+// Sampling.h:205-211
+static inline float SampleLinear(float u, float a, float b) {
+    if (u == 0 && a == 0) return 0;
+    float x = (u * (a + b)) / (a + std::sqrt(Lerp(u, a * a, b * b)));
+    return std::min(x, OneMinusEpsilon);
+}
+// Sampling.h:228-235 with the coin taken deterministically from u (pbrt-v4 SampleDiscrete remap) instead
+// of the global mt19937 (non-deterministic in the reference) — build-defined, documented.
+static inline float SampleTentDet(float u, float r) {
+    if (u < 0.5f) {
+        float up = std::min(u * 2.0f, OneMinusEpsilon);
+        return -r + r * SampleLinear(up, 0, 1);
+    }
+    float up = std::min((u - 0.5f) * 2.0f, OneMinusEpsilon);
+    return r * SampleLinear(up, 1, 0);
+}
+// Sampling.h:383-403
+static inline vec2 SampleUniformDiskConcentric(vec2 u) {
+    vec2 o = {2.0f * u.x - 1.0f, 2.0f * u.y - 1.0f};
+    if (o.x == 0 && o.y == 0) return {0, 0};
+    float theta, r;
+    if (std::fabs(o.x) > std::fabs(o.y)) { r = o.x; theta = PiOver4 * (o.y / o.x); }
+    else { r = o.y; theta = PiOver2 - PiOver4 * (o.x / o.y); }
+    return {r * cos_f(theta), r * sin_f(theta)};
+}
+// Sampling.h:449-454 (+ HelperFunctions SafeSqrt)
+static inline vec3 SampleCosineHemisphere(vec2 u) {
+    vec2 d = SampleUniformDiskConcentric(u);
+    float z = std::sqrt(std::max(0.f, 1 - d.x * d.x - d.y * d.y));
+    return {d.x, d.y, z};
+}
+
+// ============================================================================ spectra
+// spectrum.h:458-496 / spectrum.cpp:60-71 PiecewiseLinearSpectrum
+struct Piecewise {
+    std::vector<float> lambdas, values;
+    float Query(float lambda) const {
+        if (lambdas.empty() || lambda < lambdas.front() || lambda > lambdas.back()) return 0;
+        int o = (int)FindInterval(lambdas.size(), [&](int i) { return lambdas[i] <= lambda; });
+        float t = (lambda - lambdas[o]) / (lambdas[o + 1] - lambdas[o]);
+        return Lerp(t, values[o], values[o + 1]);
+    }
+};
+// spectrum.h:376-456 DenselySampledSpectrum (lambda_min 360, lambda_max 830)
+struct Dense {
+    int lambda_min = 360, lambda_max = 830;
+    std::vector<float> values;
+    float Query(float lambda) const {  // spectrum.h:430-437 / Sample 386-398
+        long offset = std::lround(lambda) - lambda_min;
+        if (offset < 0 || offset >= (long)values.size()) return 0;
+        return values[(size_t)offset];
+    }
+};
+template <typename S>
+static inline Dense MakeDense(const S& s) {  // spectrum.h:412-419
+    Dense d;
+    d.values.resize(471);
+    for (int lambda = 360; lambda <= 830; ++lambda) d.values[lambda - 360] = s.Query((float)lambda);
+    return d;
+}
+// spectrum.h:762-768 InnerProduct (float loop variable, sequential float sum)
+template <typename F, typename G>
+static inline float InnerProduct(const F& f, const G& g) {
+    float integral = 0;
+    for (float lambda = 360; lambda <= 830; ++lambda) integral += f.Query(lambda) * g.Query(lambda);
+    return integral;
+}
+struct Spectra {
+    Dense X, Y, Z;
+    Piecewise D65, F1;   // normalized (FromInterleaved(..., true))
+    Dense D65dense;      // RGBColorSpace::illuminant (colorspace.cpp:13-14 → spectrum.h:412-419)
+    Piecewise FromInterleaved(const float* s, int n, bool normalize) const {  // spectrum.cpp:134-165
+        Piecewise p;
+        int half = n / 2;
+        if (s[0] > 360) { p.lambdas.push_back(360 - 1); p.values.push_back(s[1]); }
+        for (int i = 0; i < half; ++i) { p.lambdas.push_back(s[2 * i]); p.values.push_back(s[2 * i + 1]); }
+        if (p.lambdas.back() < 830) { p.lambdas.push_back(830 + 1); p.values.push_back(p.values.back()); }
+        if (normalize) {
+            float scale = CIE_Y_integral / InnerProduct(p, Y);
+            for (float& v : p.values) v *= scale;   // spectrum.h:464-468 Scale
+        }
+        return p;
+    }
+    void Init() {  // spectrum.cpp:2612-2622 (X/Y/Z dense from piecewise over CIE_lambda), 2624-2634
+        auto dense_from_table = [](const float* vals) {
+            Piecewise p;
+            for (int i = 0; i < 471; ++i) { p.lambdas.push_back(rtdata::cie_lambda[i]); p.values.push_back(vals[i]); }
+            return MakeDense(p);
+        };
+        X = dense_from_table(rtdata::cie_x);
+        Y = dense_from_table(rtdata::cie_y);
+        Z = dense_from_table(rtdata::cie_z);
+        D65 = FromInterleaved(rtdata::illum_d65, rtdata::illum_d65_n, true);
+        F1 = FromInterleaved(rtdata::illum_f1, rtdata::illum_f1_n, true);
+        D65dense = MakeDense(D65);
+    }
+};
+
+// 8-wavelength sampled values (spectrum.h:52-343)
+struct SW { float lambda[8], pdf[8]; };
+struct SS { float v[8]; };
+// spectrum.h:322-336 SampledWavelengths::SampleVisible
+static inline SW SampleVisible(float u) {
+    SW s;
+    for (int i = 0; i < NSpectrumSamples; ++i) {
+        float up = u + float(i) / NSpectrumSamples;
+        if (up > 1) up -= 1;
+        s.lambda[i] = SampleVisibleWavelengths(up);
+        s.pdf[i] = VisibleWavelengthsPDF(s.lambda[i]);
+    }
+    return s;
+}
+// color.h:373-399 RGBSigmoidPolynomial (EvaluatePolynomial via FMA, helpers.h:117-126)
+struct Sigmoid {
+    float c0 = 0, c1 = 0, c2 = 0;
+    static float s(float x) {
+        if (std::isinf(x)) return x > 0 ? 1 : 0;
+        return .5f + x / (2 * std::sqrt(1 + (x * x)));
+    }
+    float operator()(float lambda) const { return s(std::fmaf(lambda, std::fmaf(lambda, c0, c1), c2)); }
+};
+// color.cpp:35-37 uniform-RGB branch of RGBToSpectrumTable (the only branch usable without the missing table)
+static inline Sigmoid SigmoidFromGrey(float g) { return {0, 0, (g - .5f) / std::sqrt(g * (1 - g))}; }
+
+// pixelsensor.h:81-87 ToSensorRGB (XYZ sensor: r_bar=X, g_bar=Y, b_bar=Z), imagingRatio = 1/CIE_Y_integral
+static inline void ToSensorRGB(const Spectra& sp, SS L, const SW& w, float imagingRatio, float rgb[3]) {
+    for (int i = 0; i < 8; ++i) L.v[i] = (w.pdf[i] != 0) ? L.v[i] / w.pdf[i] : 0.f;  // spectrum.h:643-649
+    const Dense* bars[3] = {&sp.X, &sp.Y, &sp.Z};
+    for (int c = 0; c < 3; ++c) {
+        float prod[8];
+        for (int i = 0; i < 8; ++i) prod[i] = bars[c]->Query(w.lambda[i]) * L.v[i];
+        float sum = prod[0];                                   // spectrum.h:238-244 Average
+        for (int i = 1; i < 8; ++i) sum += prod[i];
+        rgb[c] = imagingRatio * (sum / 8);
+    }
+}
+
+// ============================================================================== geometry
+struct Ray { vec3 o, d; };
+// Shapes.h:37-41 Ray::Transform
+static inline Ray TransformRay(Ray r, const mat4& M) {
+    vec4 o4 = mul(M, vec4{r.o.x, r.o.y, r.o.z, 1});
+    vec4 d4 = normalize4(mul(M, vec4{r.d.x, r.d.y, r.d.z, 0}));
+    return {{o4.x, o4.y, o4.z}, {d4.x, d4.y, d4.z}};
+}
+struct Bounds3 { vec3 pmin, pmax; };
+// Shapes.h:100-124 Bounds3::IntersectP
+static inline bool IntersectP(const Bounds3& b, const Ray& ray, float tMax) {
+    float min_t = 0, max_t = tMax;
+    const float g3 = 1 + 2 * gamma_(3);
+    for (int i = 0; i < 3; ++i) {
+        float invRayDir = 1 / ray.d[i];
+        float tNear = ((i == 0 ? b.pmin.x : i == 1 ? b.pmin.y : b.pmin.z) - ray.o[i]) * invRayDir;
+        float tFar = ((i == 0 ? b.pmax.x : i == 1 ? b.pmax.y : b.pmax.z) - ray.o[i]) * invRayDir;
+        if (tNear > tFar) std::swap(tNear, tFar);
+        tFar *= g3;
+        min_t = tNear > min_t ? tNear : min_t;
+        max_t = tFar < max_t ? tFar : max_t;
+        if (min_t > max_t) return false;
+    }
+    return true;
+}
+
+struct TriIsect { float b0, b1, b2, t; };
+// Shapes.h:1101-1260 Triangle::BasicIntersect — pbrt-v4 watertight test on world-space vertices
+static inline bool BasicIntersect(vec3 p0w, vec3 p1w, vec3 p2w, const Ray& ray, float tMax, TriIsect* out) {
+    // Shapes.h:1131 degenerate: pow(length(cross),2) == 0  <=>  dot(c,c) == 0
+    vec3 c = cross(sub(p2w, p0w), sub(p1w, p0w));
+    if (dot(c, c) == 0) return false;
+    vec3 p0t = sub(p0w, ray.o), p1t = sub(p1w, ray.o), p2t = sub(p2w, ray.o);
+    vec3 ad = {std::fabs(ray.d.x), std::fabs(ray.d.y), std::fabs(ray.d.z)};
+    int kz = MaxComponentIndex(ad);
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    vec3 d = {ray.d[kx], ray.d[ky], ray.d[kz]};
+    p0t = {p0t[kx], p0t[ky], p0t[kz]};
+    p1t = {p1t[kx], p1t[ky], p1t[kz]};
+    p2t = {p2t[kx], p2t[ky], p2t[kz]};
+    float Sx = -d.x / d.z, Sy = -d.y / d.z, Sz = 1 / d.z;
+    p0t.x += Sx * p0t.z; p0t.y += Sy * p0t.z;
+    p1t.x += Sx * p1t.z; p1t.y += Sy * p1t.z;
+    p2t.x += Sx * p2t.z; p2t.y += Sy * p2t.z;
+    float e0 = DifferenceOfProducts(p1t.x, p2t.y, p1t.y, p2t.x);
+    float e1 = DifferenceOfProducts(p2t.x, p0t.y, p2t.y, p0t.x);
+    float e2 = DifferenceOfProducts(p0t.x, p1t.y, p0t.y, p1t.x);
+    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {  // Shapes.h:1174-1184 double fallback
+        double p2txp1ty = (double)p2t.x * (double)p1t.y, p2typ1tx = (double)p2t.y * (double)p1t.x;
+        e0 = (float)(p2typ1tx - p2txp1ty);
+        double p0txp2ty = (double)p0t.x * (double)p2t.y, p0typ2tx = (double)p0t.y * (double)p2t.x;
+        e1 = (float)(p0typ2tx - p0txp2ty);
+        double p1txp0ty = (double)p1t.x * (double)p0t.y, p1typ0tx = (double)p1t.y * (double)p0t.x;
+        e2 = (float)(p1typ0tx - p1txp0ty);
+    }
+    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
+    float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0t.z *= Sz; p1t.z *= Sz; p2t.z *= Sz;
+    float tScaled = e0 * p0t.z + e1 * p1t.z + e2 * p2t.z;
+    if (det < 0 && (tScaled >= 0 || tScaled < tMax * det)) return false;
+    else if (det > 0 && (tScaled <= 0 || tScaled > tMax * det)) return false;
+    float invDet = 1 / det;
+    float b0 = e0 * invDet, b1 = e1 * invDet, b2 = e2 * invDet;
+    float t = tScaled * invDet;
+    if (std::isnan(t)) return false;
+    float maxZt = MaxComponentValue({std::fabs(p0t.z), std::fabs(p1t.z), std::fabs(p2t.z)});
+    float deltaZ = gamma_(3) * maxZt;
+    float maxXt = MaxComponentValue({std::fabs(p0t.x), std::fabs(p1t.x), std::fabs(p2t.x)});
+    float maxYt = MaxComponentValue({std::fabs(p0t.y), std::fabs(p1t.y), std::fabs(p2t.y)});
+    float deltaX = gamma_(5) * (maxXt + maxZt);
+    float deltaY = gamma_(5) * (maxYt + maxZt);
+    float deltaE = 2 * (gamma_(2) * maxXt * maxYt + deltaY * maxXt + deltaX * maxYt);
+    float maxE = MaxComponentValue({std::fabs(e0), std::fabs(e1), std::fabs(e2)});
+    float deltaT = 3 * (gamma_(3) * maxE * maxZt + deltaE * maxZt + deltaZ * maxE) * std::fabs(invDet);
+    if (t <= deltaT) return false;
+    *out = {b0, b1, b2, t};
+    return true;
+}
+
+// ------------------------------------------------------------------ Möller triangle/box overlap
+// AABB_triangle_Moller.h:187-474 (incl. the AxisTest_Z0 quirk at :342 that never rejects)
+static inline void FindMinMax(float x0, float x1, float x2, float& mn, float& mx) {
+    mn = mx = x0;
+    if (x1 < mn) mn = x1;
+    if (x1 > mx) mx = x1;
+    if (x2 < mn) mn = x2;
+    if (x2 > mx) mx = x2;
+}
+static inline int planeBoxOverlap(vec3 normal, vec3 vert, vec3 maxbox) {
+    float vmin[3], vmax[3];
+    for (int q = 0; q <= 2; ++q) {
+        float v = vert[q], n = normal[q], mb = maxbox[q];
+        if (n > 0.0f) { vmin[q] = -mb - v; vmax[q] = mb - v; }
+        else { vmin[q] = mb - v; vmax[q] = -mb - v; }
+    }
+    if (dot(normal, {vmin[0], vmin[1], vmin[2]}) > 0.0f) return 0;
+    if (dot(normal, {vmax[0], vmax[1], vmax[2]}) >= 0.0f) return 1;
+    return 0;
+}
+static inline bool triBoxOverlap(vec3 boxcenter, vec3 bh, vec3 t0, vec3 t1, vec3 t2) {
+    vec3 v0 = sub(t0, boxcenter), v1 = sub(t1, boxcenter), v2 = sub(t2, boxcenter);
+    vec3 e0 = sub(v1, v0), e1 = sub(v2, v1), e2 = sub(v0, v2);
+    float mn, mx, p0, p1, p2, rad;
+    auto X01 = [&](float a, float b, float fa, float fb) {
+        p0 = a * v0.y - b * v0.z; p2 = a * v2.y - b * v2.z;
+        if (p0 < p2) { mn = p0; mx = p2; } else { mn = p2; mx = p0; }
+        rad = fa * bh.y + fb * bh.z;
+        return !(mn > rad || mx < -rad);
+    };
+    auto X2 = [&](float a, float b, float fa, float fb) {
+        p0 = a * v0.y - b * v0.z; p1 = a * v1.y - b * v1.z;
+        if (p0 < p1) { mn = p0; mx = p1; } else { mn = p1; mx = p0; }
+        rad = fa * bh.y + fb * bh.z;
+        return !(mn > rad || mx < -rad);
+    };
+    auto Y02 = [&](float a, float b, float fa, float fb) {
+        p0 = -a * v0.x + b * v0.z; p2 = -a * v2.x + b * v2.z;
+        if (p0 < p2) { mn = p0; mx = p2; } else { mn = p2; mx = p0; }
+        rad = fa * bh.x + fb * bh.z;
+        return !(mn > rad || mx < -rad);
+    };
+    auto Y1 = [&](float a, float b, float fa, float fb) {
+        p0 = -a * v0.x + b * v0.z; p1 = -a * v1.x + b * v1.z;
+        if (p0 < p1) { mn = p0; mx = p1; } else { mn = p1; mx = p0; }
+        rad = fa * bh.x + fb * bh.z;
+        return !(mn > rad || mx < -rad);
+    };
+    auto Z0 = [&](float a, float b, float fa, float fb) {  // :334-345 — returns true on both paths
+        p0 = a * v0.x - b * v0.y; p1 = a * v1.x - b * v1.y;
+        if (p0 < p1) { mn = p0; mx = p1; } else { mn = p1; mx = p0; }
+        rad = fa * bh.x + fb * bh.y;
+        return true;
+    };
+    auto Z12 = [&](float a, float b, float fa, float fb) {
+        p1 = a * v1.x - b * v1.y; p2 = a * v2.x - b * v2.y;
+        if (p2 < p1) { mn = p2; mx = p1; } else { mn = p1; mx = p2; }
+        rad = fa * bh.x + fb * bh.y;
+        return !(mn > rad || mx < -rad);
+    };
+    float fex = std::fabs(e0.x), fey = std::fabs(e0.y), fez = std::fabs(e0.z);
+    if (!X01(e0.z, e0.y, fez, fey)) return false;
+    if (!Y02(e0.z, e0.x, fez, fex)) return false;
+    if (!Z12(e0.y, e0.x, fey, fex)) return false;
+    fex = std::fabs(e1.x); fey = std::fabs(e1.y); fez = std::fabs(e1.z);
+    if (!X01(e1.z, e1.y, fez, fey)) return false;
+    if (!Y02(e1.z, e1.x, fez, fex)) return false;
+    if (!Z0(e1.y, e1.x, fey, fex)) return false;
+    fex = std::fabs(e2.x); fey = std::fabs(e2.y); fez = std::fabs(e2.z);
+    if (!X2(e2.z, e2.y, fez, fey)) return false;
+    if (!Y1(e2.z, e2.x, fez, fex)) return false;
+    if (!Z12(e2.y, e2.x, fey, fex)) return false;
+    FindMinMax(v0.x, v1.x, v2.x, mn, mx);
+    if (mn > bh.x || mx < -bh.x) return false;
+    FindMinMax(v0.y, v1.y, v2.y, mn, mx);
+    if (mn > bh.y || mx < -bh.y) return false;
+    FindMinMax(v0.z, v1.z, v2.z, mn, mx);
+    if (mn > bh.z || mx < -bh.z) return false;
+    vec3 normal = cross(e0, e1);
+    if (!planeBoxOverlap(normal, v0, bh)) return false;
+    return true;
+}
+
+// ------------------------------------------------------------------------------ TriModel
+// Shapes.h:1272-1491 + 913-1083 (one mesh).  Positions/normals are object space; ObjectToRender is
+// rigidtransform * permutation_y_z (Shapes.h:175-181), provided by the caller.
+struct TriModel {
+    std::vector<vec3> pos, nrm;         // object space
+    std::vector<uint32_t> idx;          // 3 per triangle
+    mat4 objectToRender;
+    mat3 normalToRender;                // mat3(transpose(inverse(ObjectToRender))), caller-provided
+    std::vector<vec3> wpos;             // ObjectToRender * p (per vertex; = per-test transform Shapes.h:1119)
+    std::vector<uint8_t> back_facing;   // ComputeBackFace flags (empty when culling disabled)
+    bool cull = false;
+    size_t ntri() const { return idx.size() / 3; }
+    void Prepare() {
+        wpos.resize(pos.size());
+        for (size_t i = 0; i < pos.size(); ++i) {
+            vec4 w = mul(objectToRender, vec4{pos[i].x, pos[i].y, pos[i].z, 1});
+            wpos[i] = {w.x, w.y, w.z};
+        }
+    }
+    vec3 P(size_t t, int k) const { return wpos[idx[3 * t + k]]; }
+    // Shapes.h:1339-1380 ComputeBackFace
+    void ComputeBackFace(vec3 look, bool enable) {
+        cull = enable;
+        back_facing.clear();
+        if (!enable) return;
+        vec3 look_dir = normalize(look);
+        back_facing.resize(ntri());
+        for (size_t t = 0; t < ntri(); ++t) {
+            vec3 n1 = nrm[idx[3 * t]], n2 = nrm[idx[3 * t + 1]], n3 = nrm[idx[3 * t + 2]];
+            vec3 s = add(add(n1, n2), n3);
+            vec3 N = normalize({s.x / 3.0f, s.y / 3.0f, s.z / 3.0f});
+            N = normalize(mul(normalToRender, N));
+            back_facing[t] = dot(look_dir, N) > 0 ? 1 : 0;
+        }
+    }
+    // Shapes.h:1390-1397 Bounds(): object-space min/max (max initialised with FLT_MIN — quirk, :1292)
+    // transformed by Bounds3::Transform (Shapes.h:60-98, same FLT_MIN quirk at :80-82)
+    Bounds3 Bounds() const {
+        vec3 mn = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(), std::numeric_limits<float>::max()};
+        vec3 mx = {std::numeric_limits<float>::min(), std::numeric_limits<float>::min(), std::numeric_limits<float>::min()};
+        for (const vec3& p : pos) {
+            mn.x = std::min(mn.x, p.x); mn.y = std::min(mn.y, p.y); mn.z = std::min(mn.z, p.z);
+            mx.x = std::max(mx.x, p.x); mx.y = std::max(mx.y, p.y); mx.z = std::max(mx.z, p.z);
+        }
+        vec3 corners[8] = {{mn.x, mn.y, mn.z}, {mn.x, mx.y, mn.z}, {mn.x, mx.y, mx.z}, {mn.x, mn.y, mx.z},
+                           {mx.x, mx.y, mx.z}, {mx.x, mn.y, mx.z}, {mx.x, mn.y, mn.z}, {mx.x, mx.y, mn.z}};
+        float xm = std::numeric_limits<float>::max(), xM = std::numeric_limits<float>::min();
+        float ym = xm, yM = xM, zm = xm, zM = xM;
+        for (auto& c : corners) {
+            vec4 w = mul(objectToRender, vec4{c.x, c.y, c.z, 1});
+            xm = std::min(xm, w.x); xM = std::max(xM, w.x);
+            ym = std::min(ym, w.y); yM = std::max(yM, w.y);
+            zm = std::min(zm, w.z); zM = std::max(zM, w.z);
+        }
+        return {{xm, ym, zm}, {xM, yM, zM}};
+    }
+};
+
+// --------------------------------------------------------------------------- Octtree_Model
+// Octtree_Model.h:9-388
+struct Octree {
+    struct Node {
+        Bounds3 bounds;
+        std::vector<int> tris;
+        bool leaf = true;
+        int parent = -1;
+        std::vector<int> child;
+    };
+    static const int TRIANGLE_CAPACITY_DEFAULT = 40;  // Octtree_Model.h:388
+    int capacity = TRIANGLE_CAPACITY_DEFAULT;
+    std::vector<Node> nodes;
+    const TriModel* model = nullptr;
+
+    // Octtree_Model.h:361-367
+    bool triBounds(vec3 p0, vec3 p1, vec3 p2, const Bounds3& b) const {
+        vec3 half = {(b.pmax.x - b.pmin.x) / 2.0f, (b.pmax.y - b.pmin.y) / 2.0f, (b.pmax.z - b.pmin.z) / 2.0f};
+        vec3 C = add(b.pmin, half);
+        return triBoxOverlap(C, half, p0, p1, p2);
+    }
+    // Octtree_Model.h:279-358
+    void Split(int id) {
+        Bounds3 B = nodes[id].bounds;
+        float padding = 0.01f;
+        vec3 half = {(B.pmax.x - B.pmin.x) / 2.0f, (B.pmax.y - B.pmin.y) / 2.0f, (B.pmax.z - B.pmin.z) / 2.0f};
+        vec3 C = add(B.pmin, half);
+        half = add(half, {padding, padding, padding});
+        auto box = [&](vec3 a, vec3 b) { return Bounds3{add(C, a), add(C, b)}; };
+        Bounds3 bb[8] = {
+            box({-half.x, 0, -half.z}, {0, half.y, 0}),      box({0, 0, -half.z}, {half.x, half.y, 0}),
+            box({-half.x, 0, 0}, {0, half.y, half.z}),       box({0, 0, 0}, {half.x, half.y, half.z}),
+            box({-half.x, -half.y, -half.z}, {0, 0, 0}),     box({0, -half.y, -half.z}, {half.x, 0, 0}),
+            box({-half.x, -half.y, 0}, {0, 0, half.z}),      box({0, -half.y, 0}, {half.x, 0, half.z})};
+        Node nn[8];
+        for (int n = 0; n < 8; ++n) nn[n].bounds = bb[n];
+        for (int t : nodes[id].tris)
+            for (int n = 0; n < 8; ++n)
+                if (triBounds(model->P(t, 0), model->P(t, 1), model->P(t, 2), nn[n].bounds)) nn[n].tris.push_back(t);
+        int cnt = (int)nodes[id].tris.size();
+        for (int n = 0; n < 8; ++n)
+            if ((int)nn[n].tris.size() == cnt) return;  // abort rule :331-340
+        nodes[id].child.clear();
+        for (int n = 0; n < 8; ++n) {
+            nn[n].parent = id;
+            nodes.push_back(nn[n]);
+            nodes[id].child.push_back((int)nodes.size() - 1);
+        }
+        nodes[id].tris.clear();
+        nodes[id].leaf = false;
+    }
+    // Octtree_Model.h:180-277
+    void AddTriangle(int t) {
+        vec3 p0 = model->P(t, 0), p1 = model->P(t, 1), p2 = model->P(t, 2);
+        std::queue<int> q;
+        q.push(0);
+        while (!q.empty()) {
+            int cur = q.front(); q.pop();
+            if (triBounds(p0, p1, p2, nodes[cur].bounds)) {
+                if (nodes[cur].leaf) {
+                    nodes[cur].tris.push_back(t);
+                    if ((int)nodes[cur].tris.size() >= capacity) Split(cur);
+                } else {
+                    for (int i = 0; i < 8; ++i) q.push(nodes[cur].child[i]);
+                }
+            }
+        }
+    }
+    // Octtree_Model.h:33-63
+    void Create(const TriModel& m, int cap = TRIANGLE_CAPACITY_DEFAULT) {
+        model = &m;
+        capacity = cap;
+        nodes.clear();
+        Node root;
+        root.bounds = m.Bounds();
+        root.parent = 0;
+        nodes.push_back(root);
+        for (size_t t = 0; t < m.ntri(); ++t) AddTriangle((int)t);
+    }
+
+    struct Hit { int tri = -1; TriIsect isect{}; long nodes_tested = 0, tris_tested = 0; };
+    // Octtree_Model.h:66-127 Traverse — BFS with a shrinking tMax, first hit in BFS order wins ties
+    Hit Traverse(const Ray& ray, bool use_cull) const {
+        Hit h;
+        float tMax = std::numeric_limits<float>::max();
+        std::queue<int> q;
+        q.push(0);
+        while (!q.empty()) {
+            int cur = q.front(); q.pop();
+            ++h.nodes_tested;
+            if (IntersectP(nodes[cur].bounds, ray, tMax)) {
+                if (nodes[cur].leaf) {
+                    for (int t : nodes[cur].tris) {
+                        if (use_cull && model->cull && !model->back_facing.empty() && model->back_facing[t]) continue;
+                        ++h.tris_tested;
+                        TriIsect is;
+                        if (BasicIntersect(model->P(t, 0), model->P(t, 1), model->P(t, 2), ray, tMax, &is)) {
+                            if (is.t < tMax) { tMax = is.t; h.tri = t; h.isect = is; }
+                        }
+                    }
+                } else {
+                    for (int i = 0; i < 8; ++i) q.push(nodes[cur].child[i]);
+                }
+            }
+        }
+        return h;
+    }
+    // any-hit with a fixed tMax (path mode shadow rays, build-defined): order-independent answer
+    bool Occluded(const Ray& ray, float tMax) const {
+        std::queue<int> q;
+        q.push(0);
+        while (!q.empty()) {
+            int cur = q.front(); q.pop();
+            if (!IntersectP(nodes[cur].bounds, ray, tMax)) continue;
+            if (nodes[cur].leaf) {
+                for (int t : nodes[cur].tris) {
+                    TriIsect is;
+                    if (BasicIntersect(model->P(t, 0), model->P(t, 1), model->P(t, 2), ray, tMax, &is) && is.t < tMax)
+                        return true;
+                }
+            } else {
+                for (int i = 0; i < 8; ++i) q.push(nodes[cur].child[i]);
+            }
+        }
+        return false;
+    }
+};
+
+// ------------------------------------------------------------------------------- camera
+// Cameras.h:273-297 PerspectiveCamera::generateRay; matrices are the values CameraBase holds
+struct Camera {
+    mat4 rasterToCamera, cameraToWorld;
+    float lensRadius = 0, focalDistance = 0;
+    Ray generateRay(vec2 pixel, Sampler* sampler) const {
+        vec4 np = mul(rasterToCamera, vec4{pixel.x, pixel.y, 0, 1});
+        vec3 near_pos = {np.x / np.w, np.y / np.w, np.z / np.w};
+        Ray ray{{0, 0, 0}, normalize(near_pos)};
+        if (lensRadius > 0 && sampler) {
+            vec2 dsk = SampleUniformDiskConcentric(sampler->Get2D());
+            vec2 lens = {lensRadius * dsk.x, lensRadius * dsk.y};
+            float ft = focalDistance / ray.d.z;
+            vec3 pfocus = add(ray.o, mul(ray.d, ft));
+            ray.o = {lens.x, lens.y, 0};
+            ray.d = normalize(sub(pfocus, ray.o));
+        }
+        return TransformRay(ray, cameraToWorld);
+    }
+};
+
+// ----------------------------------------------------------------------------- filters
+// filters.h:66-93 BoxFilter::Sample ; filters.h:285-290 TriangleFilter::Sample (deterministic coin)
+struct Filter {
+    int kind = 0;  // 0 box, 1 triangle
+    float rx = 0.5f, ry = 0.5f;
+    vec2 Sample(vec2 u, float* weight) const {
+        *weight = 1.0f;
+        if (kind == 0) return {Lerp(u.x, -rx, rx), Lerp(u.y, -ry, ry)};
+        return {SampleTentDet(u.x, rx), SampleTentDet(u.y, ry)};
+    }
+};
+
+// ========================================================================= the integrators
+struct Material { float c[3] = {0, 0, 0}; float emit = 0; };   // sigmoid coeffs + Le = emit * D65
+struct QuadLight { vec3 p, e1, e2, n; float area; int material; };
+
+struct Scene {
+    Spectra spectra;
+    TriModel model;
+    Octree octree;
+    Camera camera;
+    Sampler sampler;
+    Filter filter;
+    int resX = 500, resY = 500;
+    float imagingRatio = 1.0f / CIE_Y_integral;
+    // reference mode (RayTracerTestApp.h:218-284)
+    float albedo_rgb[3] = {0.5f, 0.5f, 0.5f};
+    // path mode (build-defined)
+    std::vector<int> tri_material;
+    std::vector<Material> materials;
+    std::vector<QuadLight> lights;
+    int max_depth = 5;
+};
+
+// Per-sample debug record (for golden fixtures / kernel-level parity)
+struct SampleRecord {
+    float lambda[8], pdf[8];
+    float ro[3], rd[3];
+    int prim;
+    float b[3], t;
+    float L[8];
+    float rgb[3];
+    float weight;
+};
+
+// RayTracerTestApp.h:289-291 — raster coordinate of a pixel id (y in [1, resY], a kept quirk)
+static inline void PixelCoord(int pixel_id, int resX, int resY, int* x, int* y) {
+    *x = pixel_id % resX;
+    *y = (int)((float)resY - std::floor((float)pixel_id / (float)resX));
+}
+
+// RayTracerTestApp.h:218-284 Li (active branch): ambient 0.3*F1 + clamp(n.(0,0,-1))*(light*albedo)
+static inline SS LiReference(const Scene& S, const Ray& ray, const SW& w, SampleRecord* rec, long* counters) {
+    Octree::Hit h = S.octree.Traverse(ray, true);
+    if (counters) { counters[0] += h.nodes_tested; counters[1] += h.tris_tested; counters[2] += (h.tri >= 0); }
+    if (rec) { rec->prim = h.tri; rec->b[0] = h.isect.b0; rec->b[1] = h.isect.b1; rec->b[2] = h.isect.b2; rec->t = h.isect.t; }
+    SS r{};
+    if (h.tri < 0) return r;  // SampledSpectrum(0)
+    const TriModel& m = S.model;
+    // Shapes.h:1066-1075 — object-space interpolated normal, flipped against normalize(ray.d)
+    vec3 n1 = m.nrm[m.idx[3 * h.tri]], n2 = m.nrm[m.idx[3 * h.tri + 1]], n3 = m.nrm[m.idx[3 * h.tri + 2]];
+    vec3 n = normalize(add(add(mul(n1, h.isect.b0), mul(n2, h.isect.b1)), mul(n3, h.isect.b2)));
+    vec3 rayd = normalize(ray.d);  // Shapes.h:1259
+    if (dot(n, rayd) > 0) n = {-n.x, -n.y, -n.z};
+    // color.cpp:35-37 uniform branch; RGBAlbedo(rgb) -> constant s(c2)
+    Sigmoid alb = SigmoidFromGrey(S.albedo_rgb[0]);
+    float cosv = gclamp(dot(n, {0, 0, -1}), 0.0f, 1.0f);
+    for (int i = 0; i < 8; ++i) {
+        float light = (2.0f * 0.5f) * S.spectra.D65dense.Query(w.lambda[i]);  // spectrum.h:621-629 (scale*rsp)*illum
+        float amb = S.spectra.F1.Query(w.lambda[i]) * 0.3f;                    // 0.3f * illumF->Sample
+        float mat = alb(w.lambda[i]);
+        float radiance = 0.0f + amb;                                          // radiance += ambient
+        radiance += (light * mat) * cosv;                                     // radiance += cos*(light*mat)
+        r.v[i] = radiance;
+    }
+    return r;
+}
+
+// Build-defined path integrator (pbrt-v4 SimplePathIntegrator semantics with NEE on quad lights,
+// Lambert R/pi, geometric normals = Shapes.h:1073 fallback, no MIS, no RR).  See DESIGN.md §Path mode.
+static inline SS LiPath(const Scene& S, Ray ray, const SW& w, Sampler& smp, long* counters) {
+    SS L{}, beta;
+    for (int i = 0; i < 8; ++i) beta.v[i] = 1.0f;
+    const TriModel& m = S.model;
+    for (int depth = 0;; ++depth) {
+        Octree::Hit h = S.octree.Traverse(ray, false);
+        if (counters) { counters[0] += h.nodes_tested; counters[1] += h.tris_tested; counters[2] += (h.tri >= 0); counters[3] += 1; }
+        if (h.tri < 0) break;
+        vec3 p0 = m.P(h.tri, 0), p1 = m.P(h.tri, 1), p2 = m.P(h.tri, 2);
+        vec3 dp02 = sub(p0, p2), dp12 = sub(p1, p2);
+        vec3 ng = normalize(cross(dp02, dp12));
+        vec3 rayd = normalize(ray.d);
+        const Material& mat = S.materials[S.tri_material[h.tri]];
+        if (mat.emit > 0) {  // pure emitter: Le on camera rays only (NEE covers later bounces), one-sided
+            if (depth == 0 && dot(ng, rayd) < 0)
+                for (int i = 0; i < 8; ++i) L.v[i] += beta.v[i] * (mat.emit * S.spectra.D65dense.Query(w.lambda[i]));
+            break;
+        }
+        if (depth == S.max_depth) break;
+        vec3 n = ng;
+        if (dot(n, rayd) > 0) n = {-n.x, -n.y, -n.z};
+        vec3 p = add(add(mul(p0, h.isect.b0), mul(p1, h.isect.b1)), mul(p2, h.isect.b2));
+        float ap = MaxComponentValue({std::fabs(p.x), std::fabs(p.y), std::fabs(p.z)});
+        float off = 1e-4f * (1.0f + ap);
+        vec3 po = add(p, mul(n, off));
+        float R[8];
+        Sigmoid sg{mat.c[0], mat.c[1], mat.c[2]};
+        for (int i = 0; i < 8; ++i) R[i] = sg(w.lambda[i]);
+        // --- NEE: one quad light (the first), uniform area sampling
+        vec2 ul = smp.Get2D();
+        if (!S.lights.empty()) {
+            const QuadLight& Lq = S.lights[0];
+            vec3 pl = add(add(Lq.p, mul(Lq.e1, ul.x)), mul(Lq.e2, ul.y));
+            vec3 wv = sub(pl, po);
+            float dist2 = dot(wv, wv);
+            float dist = std::sqrt(dist2);
+            vec3 wi = mul(wv, 1.0f / dist);
+            float cs = dot(n, wi);
+            float cl = -dot(Lq.n, wi);
+            if (counters) counters[4] += 1;
+            if (cs > 0 && cl > 0) {
+                Ray sr{po, wi};
+                if (!S.octree.Occluded(sr, dist * 0.999f)) {
+                    const Material& lm = S.materials[Lq.material];
+                    float G = (cs * cl) / dist2;
+                    float wgt = G * Lq.area;
+                    for (int i = 0; i < 8; ++i) {
+                        float Le = lm.emit * S.spectra.D65dense.Query(w.lambda[i]);
+                        L.v[i] += ((beta.v[i] * (R[i] * InvPi)) * Le) * wgt;
+                    }
+                }
+            }
+        }
+        // --- BSDF sampling: cosine hemisphere around n (frame: Shapes.h:1025-1029 CoordinateSystem)
+        vec2 ub = smp.Get2D();
+        vec3 wl = SampleCosineHemisphere(ub);
+        if (wl.z == 0) break;
+        float sign = std::copysign(1.0f, n.z);
+        float a = -1 / (sign + n.z);
+        float b = n.x * n.y * a;
+        vec3 s = {1 + sign * (n.x * n.x) * a, sign * b, -sign * n.x};
+        vec3 t = {b, sign + (n.y * n.y) * a, -n.y};
+        vec3 wi = add(add(mul(s, wl.x), mul(t, wl.y)), mul(n, wl.z));
+        for (int i = 0; i < 8; ++i) beta.v[i] *= R[i];
+        ray = Ray{po, wi};
+    }
+    return L;
+}
+
+// RayTracerTestApp.h:287-345 evaluate_pixel (film accumulation in place)
+static inline void EvaluatePixel(const Scene& S, Sampler& smp, int pixel_id, int index, bool path_mode, float* px,
+                                 SampleRecord* rec, long* counters) {
+    int x, y;
+    PixelCoord(pixel_id, S.resX, S.resY, &x, &y);
+    if (!smp.StartPixelSample(x, y, index, 0)) return;
+    SW w = SampleVisible(smp.Get1D());
+    vec2 up = smp.GetPixel2D();
+    float fw;
+    vec2 fp = S.filter.Sample(up, &fw);
+    vec2 pos = {((float)x + .5f) + fp.x, ((float)y + .5f) + fp.y};
+    Ray ray = S.camera.generateRay(pos, &smp);
+    SS L = path_mode ? LiPath(S, ray, w, smp, counters) : LiReference(S, ray, w, rec, counters);
+    float rgb[3];
+    ToSensorRGB(S.spectra, L, w, S.imagingRatio, rgb);
+    for (int c = 0; c < 3; ++c) rgb[c] = gclamp(rgb[c], 0.0f, 1.0f);
+    px[0] += fw * rgb[0];
+    px[1] += fw * rgb[1];
+    px[2] += fw * rgb[2];
+    px[3] += fw;
+    if (rec) {
+        std::memcpy(rec->lambda, w.lambda, 32); std::memcpy(rec->pdf, w.pdf, 32);
+        rec->ro[0] = ray.o.x; rec->ro[1] = ray.o.y; rec->ro[2] = ray.o.z;
+        rec->rd[0] = ray.d.x; rec->rd[1] = ray.d.y; rec->rd[2] = ray.d.z;
+        std::memcpy(rec->L, L.v, 32); std::memcpy(rec->rgb, rgb, 12);
+        rec->weight = fw;
+    }
+}
+
+}  // namespace rtcore

@@ -1,0 +1,337 @@
+// ORACLE C entry points — TEST INFRASTRUCTURE ONLY (loaded by tests/, __graft_entry__.smoke() and the
+// cpu_baseline leg of bench.py through ctypes).  Consumes the same POD descriptors as the product ABI
+// (include/rtmi355x.h) so a test can hand identical inputs to both sides.
+#include <atomic>
+#include <thread>
+
+#include "../include/rtmi355x.h"
+#include "rtcore.hpp"
+
+using namespace rtcore;
+
+namespace {
+
+mat4 M4(const float* f) { mat4 m; std::memcpy(m.m, f, 64); return m; }
+mat3 M3(const float* f) { mat3 m; std::memcpy(m.m, f, 36); return m; }
+
+// glm mat3 inverse (cofactor form) and products, float — used only by the a20 resolve matrices
+mat3 inverse3(const mat3& a) {
+    auto m = [&](int c, int r) { return a.m[c * 3 + r]; };
+    float ood = 1.0f / (+m(0, 0) * (m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) - m(1, 0) * (m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) +
+                        m(2, 0) * (m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)));
+    mat3 o;
+    auto set = [&](int c, int r, float v) { o.m[c * 3 + r] = v; };
+    set(0, 0, +(m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) * ood);
+    set(1, 0, -(m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2)) * ood);
+    set(2, 0, +(m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1)) * ood);
+    set(0, 1, -(m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) * ood);
+    set(1, 1, +(m(0, 0) * m(2, 2) - m(2, 0) * m(0, 2)) * ood);
+    set(2, 1, -(m(0, 0) * m(2, 1) - m(2, 0) * m(0, 1)) * ood);
+    set(0, 2, +(m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)) * ood);
+    set(1, 2, -(m(0, 0) * m(1, 2) - m(1, 0) * m(0, 2)) * ood);
+    set(2, 2, +(m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1)) * ood);
+    return o;
+}
+mat3 mul3(const mat3& A, const mat3& B) {
+    mat3 o;
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r)
+            o.m[c * 3 + r] = (A.m[0 * 3 + r] * B.m[c * 3 + 0] + A.m[1 * 3 + r] * B.m[c * 3 + 1]) + A.m[2 * 3 + r] * B.m[c * 3 + 2];
+    return o;
+}
+
+struct OracleScene {
+    Scene S;
+    bool path = false;
+    mat3 xyzFromSensor, rgbFromXyz;
+
+    void InitResolve() {
+        // colorspace.cpp:13-28 sRGB; color.h:616-628 WhiteBalance; pixelsensor.h:70-79
+        auto toXYZ = [&](const Piecewise& s) {
+            float X = InnerProduct(S.spectra.X, s), Y = InnerProduct(S.spectra.Y, s), Z = InnerProduct(S.spectra.Z, s);
+            return vec3{X / CIE_Y_integral, Y / CIE_Y_integral, Z / CIE_Y_integral};
+        };
+        auto xy = [](vec3 c) { return vec2{c.x / (c.x + c.y + c.z), c.y / (c.x + c.y + c.z)}; };
+        auto fromxyY = [](vec2 v) {
+            if (v.y == 0) return vec3{0, 0, 0};
+            return vec3{v.x * 1.0f / v.y, 1.0f, (1 - v.x - v.y) * 1.0f / v.y};
+        };
+        vec3 W = toXYZ(S.spectra.D65);
+        vec2 w = xy(W);
+        vec3 R = fromxyY({(float).64, (float).33}), G = fromxyY({(float).3, (float).6}), B = fromxyY({(float).15, (float).06});
+        mat3 rgb{{R.x, R.y, R.z, G.x, G.y, G.z, B.x, B.y, B.z}};
+        vec3 C = mul(inverse3(rgb), W);
+        mat3 diag{{C.x, 0, 0, 0, C.y, 0, 0, 0, C.z}};
+        mat3 xyzFromRgb = mul3(rgb, diag);
+        rgbFromXyz = inverse3(xyzFromRgb);
+        // WhiteBalance(src = SpectrumToXYZ(D65).xy, dst = sRGB.w): identical whites
+        mat3 LMSFromXYZ{{(float)0.8951, (float)-0.7502, (float)0.0389, (float)0.2664, (float)1.7135, (float)-0.0685,
+                         (float)-0.1614, (float)0.0367, (float)1.0296}};
+        mat3 XYZFromLMS{{(float)0.986993, (float)0.432305, (float)-0.00852866, (float)-0.147054, (float)0.51836,
+                         (float)0.0400428, (float)0.159963, (float)0.0492912, (float)0.968487}};
+        vec2 src = xy(toXYZ(S.spectra.D65));
+        vec3 srcXYZ = fromxyY(src), dstXYZ = fromxyY(w);
+        vec3 srcLMS = mul(LMSFromXYZ, srcXYZ), dstLMS = mul(LMSFromXYZ, dstXYZ);
+        mat3 corr{{dstLMS.x / srcLMS.x, 0, 0, 0, dstLMS.y / srcLMS.y, 0, 0, 0, dstLMS.z / srcLMS.z}};
+        xyzFromSensor = mul3(mul3(XYZFromLMS, corr), LMSFromXYZ);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+uint64_t orc_murmur64a(const uint8_t* key, uint64_t len, uint64_t seed) { return MurmurHash64A(key, (size_t)len, seed); }
+uint64_t orc_mixbits(uint64_t v) { return MixBits(v); }
+uint64_t orc_hash_pixel(int x, int y, int seed) { return Hash(x, y, seed); }
+uint64_t orc_hash_pixel_dim(int x, int y, int dim, int seed) { return Hash(x, y, dim, seed); }
+int orc_permutation_element(uint32_t i, uint32_t l, uint32_t p) { return PermutationElement(i, l, p); }
+
+// mode 0: default-constructed RNG; mode 1: SetSequence(seq) then Advance(advance)
+void orc_pcg_draws(int mode, uint64_t seq, int64_t advance, int n, uint32_t* out) {
+    RNG r;
+    if (mode == 1) { r.SetSequence(seq); r.Advance(advance); }
+    for (int i = 0; i < n; ++i) out[i] = r.UniformU32();
+}
+
+// ops[k] == 1 -> Get1D (1 float), 2 -> Get2D (2 floats).  Returns floats written, -1 if StartPixelSample refused.
+int orc_sampler_draws(const rt_sampler_desc* d, int px, int py, int index, int n_ops, const int* ops, float* out) {
+    Sampler s;
+    s.kind = d->kind; s.xPixelSamples = d->x_samples; s.yPixelSamples = d->y_samples;
+    s.jitter = d->jitter != 0; s.seed = d->seed;
+    if (!s.StartPixelSample(px, py, index, 0)) return -1;
+    int w = 0;
+    for (int k = 0; k < n_ops; ++k) {
+        if (ops[k] == 1) out[w++] = s.Get1D();
+        else { vec2 v = s.Get2D(); out[w++] = v.x; out[w++] = v.y; }
+    }
+    return w;
+}
+
+void orc_sample_visible(float u, float* lambda, float* pdf) {
+    SW s = SampleVisible(u);
+    std::memcpy(lambda, s.lambda, 32);
+    std::memcpy(pdf, s.pdf, 32);
+}
+float orc_visible_pdf(float l) { return VisibleWavelengthsPDF(l); }
+float orc_sample_visible_wavelength(float u) { return SampleVisibleWavelengths(u); }
+void orc_disk_concentric(float u0, float u1, float* out) { vec2 v = SampleUniformDiskConcentric({u0, u1}); out[0] = v.x; out[1] = v.y; }
+float orc_sample_tent(float u, float r) { return SampleTentDet(u, r); }
+
+// Spectra::Init products: dense X/Y/Z/D65 (471 values at 360..830) and the normalized F1 / D65
+// piecewise spectra queried at arbitrary wavelengths.
+void orc_spectra_dense(float* X, float* Y, float* Z, float* D65) {
+    Spectra sp; sp.Init();
+    std::memcpy(X, sp.X.values.data(), 471 * 4); std::memcpy(Y, sp.Y.values.data(), 471 * 4);
+    std::memcpy(Z, sp.Z.values.data(), 471 * 4); std::memcpy(D65, sp.D65dense.values.data(), 471 * 4);
+}
+void orc_spectra_query(int which, int n, const float* lambda, float* out) {
+    static Spectra sp = [] { Spectra s; s.Init(); return s; }();
+    for (int i = 0; i < n; ++i) out[i] = which == 0 ? sp.D65.Query(lambda[i]) : sp.F1.Query(lambda[i]);
+}
+float orc_inner_product_y_d65(void) {
+    Spectra sp; sp.Init();
+    return InnerProduct(sp.D65, sp.Y);
+}
+float orc_sigmoid_eval(float c0, float c1, float c2, float lambda) { return Sigmoid{c0, c1, c2}(lambda); }
+
+int orc_triangle_intersect(const float* p, const float* ro, const float* rd, float tMax, float* out4) {
+    Ray r{{ro[0], ro[1], ro[2]}, {rd[0], rd[1], rd[2]}};
+    TriIsect is;
+    if (!BasicIntersect({p[0], p[1], p[2]}, {p[3], p[4], p[5]}, {p[6], p[7], p[8]}, r, tMax, &is)) return 0;
+    out4[0] = is.b0; out4[1] = is.b1; out4[2] = is.b2; out4[3] = is.t;
+    return 1;
+}
+int orc_tribox_overlap(const float* c, const float* h, const float* p) {
+    return triBoxOverlap({c[0], c[1], c[2]}, {h[0], h[1], h[2]}, {p[0], p[1], p[2]}, {p[3], p[4], p[5]}, {p[6], p[7], p[8]}) ? 1 : 0;
+}
+int orc_bounds_intersect(const float* b, const float* ro, const float* rd, float tMax) {
+    return IntersectP(Bounds3{{b[0], b[1], b[2]}, {b[3], b[4], b[5]}}, Ray{{ro[0], ro[1], ro[2]}, {rd[0], rd[1], rd[2]}}, tMax) ? 1 : 0;
+}
+void orc_camera_ray(const rt_camera_desc* c, const rt_sampler_desc* sd, int px, int py, int index, float fx, float fy,
+                    float* ro, float* rd) {
+    Camera cam{M4(c->raster_to_camera), M4(c->camera_to_world), c->lens_radius, c->focal_distance};
+    Sampler s;
+    s.kind = sd->kind; s.xPixelSamples = sd->x_samples; s.yPixelSamples = sd->y_samples; s.jitter = sd->jitter != 0; s.seed = sd->seed;
+    s.StartPixelSample(px, py, index, 3);
+    Ray r = cam.generateRay({fx, fy}, &s);
+    ro[0] = r.o.x; ro[1] = r.o.y; ro[2] = r.o.z; rd[0] = r.d.x; rd[1] = r.d.y; rd[2] = r.d.z;
+}
+
+void* orc_scene_create(const rt_scene_desc* sc, const rt_camera_desc* cam, const rt_sampler_desc* smp,
+                       const rt_film_desc* film, const rt_integrator_desc* integ) {
+    auto* o = new OracleScene();
+    Scene& S = o->S;
+    S.spectra.Init();
+    TriModel& m = S.model;
+    m.pos.resize(sc->n_vertices); m.nrm.resize(sc->n_vertices);
+    for (int i = 0; i < sc->n_vertices; ++i) {
+        m.pos[i] = {sc->positions[3 * i], sc->positions[3 * i + 1], sc->positions[3 * i + 2]};
+        m.nrm[i] = sc->normals ? vec3{sc->normals[3 * i], sc->normals[3 * i + 1], sc->normals[3 * i + 2]} : vec3{0, 0, 1};
+    }
+    m.idx.assign(sc->indices, sc->indices + 3 * (size_t)sc->n_triangles);
+    m.objectToRender = M4(sc->object_to_render);
+    m.normalToRender = M3(sc->normal_to_render);
+    m.Prepare();
+    m.ComputeBackFace({sc->cull_look[0], sc->cull_look[1], sc->cull_look[2]}, sc->cull_backfaces != 0);
+    S.octree.Create(m, sc->octree_capacity > 0 ? sc->octree_capacity : Octree::TRIANGLE_CAPACITY_DEFAULT);
+    S.tri_material.assign(sc->n_triangles, 0);
+    if (sc->tri_material) S.tri_material.assign(sc->tri_material, sc->tri_material + sc->n_triangles);
+    for (int i = 0; i < sc->n_materials; ++i) {
+        Material mt;
+        for (int k = 0; k < 3; ++k) mt.c[k] = sc->materials[i].sigmoid[k];
+        mt.emit = sc->materials[i].emission_scale;
+        S.materials.push_back(mt);
+    }
+    if (S.materials.empty()) S.materials.push_back(Material{});
+    for (int i = 0; i < sc->n_lights; ++i) {
+        const rt_quad_light& q = sc->lights[i];
+        QuadLight L;
+        L.p = {q.p[0], q.p[1], q.p[2]}; L.e1 = {q.e1[0], q.e1[1], q.e1[2]}; L.e2 = {q.e2[0], q.e2[1], q.e2[2]};
+        L.n = {q.n[0], q.n[1], q.n[2]};
+        vec3 cr = cross(L.e1, L.e2);
+        L.area = std::sqrt(dot(cr, cr));
+        L.material = q.material;
+        S.lights.push_back(L);
+    }
+    S.camera = Camera{M4(cam->raster_to_camera), M4(cam->camera_to_world), cam->lens_radius, cam->focal_distance};
+    S.sampler.kind = smp->kind; S.sampler.xPixelSamples = smp->x_samples; S.sampler.yPixelSamples = smp->y_samples;
+    S.sampler.jitter = smp->jitter != 0; S.sampler.seed = smp->seed;
+    S.resX = film->res_x; S.resY = film->res_y;
+    S.filter.kind = film->filter; S.filter.rx = film->filter_radius[0]; S.filter.ry = film->filter_radius[1];
+    S.imagingRatio = film->imaging_ratio;
+    o->path = integ->kind == RT_INTEGRATOR_PATH;
+    S.max_depth = integ->max_depth;
+    for (int k = 0; k < 3; ++k) S.albedo_rgb[k] = integ->albedo_rgb[k];
+    o->InitResolve();
+    return o;
+}
+void orc_scene_destroy(void* h) { delete static_cast<OracleScene*>(h); }
+
+int orc_octree_info(void* h, int* n_nodes, int* n_refs, int* depth) {
+    auto& T = static_cast<OracleScene*>(h)->S.octree;
+    *n_nodes = (int)T.nodes.size();
+    int r = 0;
+    for (auto& n : T.nodes) r += (int)n.tris.size();
+    *n_refs = r;
+    int dmax = 0;
+    std::vector<int> dep(T.nodes.size(), 0);
+    for (size_t i = 0; i < T.nodes.size(); ++i) {
+        for (int c : T.nodes[i].child) dep[c] = dep[i] + 1;
+        dmax = std::max(dmax, dep[i]);
+    }
+    *depth = dmax;
+    return 0;
+}
+int orc_octree_export(void* h, float* bounds, int* child_first, int* leaf_first, int* leaf_count, int* refs) {
+    auto& T = static_cast<OracleScene*>(h)->S.octree;
+    int r = 0;
+    for (size_t i = 0; i < T.nodes.size(); ++i) {
+        const auto& n = T.nodes[i];
+        bounds[6 * i + 0] = n.bounds.pmin.x; bounds[6 * i + 1] = n.bounds.pmin.y; bounds[6 * i + 2] = n.bounds.pmin.z;
+        bounds[6 * i + 3] = n.bounds.pmax.x; bounds[6 * i + 4] = n.bounds.pmax.y; bounds[6 * i + 5] = n.bounds.pmax.z;
+        if (n.leaf) {
+            child_first[i] = -1;
+        } else {
+            child_first[i] = n.child[0];
+            for (int c = 1; c < 8; ++c)
+                if (n.child[c] != n.child[0] + c) return -1;  // children must be contiguous (Octtree_Model.h:347-353)
+        }
+        leaf_first[i] = r;
+        leaf_count[i] = (int)n.tris.size();
+        for (int t : n.tris) refs[r++] = t;
+    }
+    return 0;
+}
+
+int orc_backface_flags(void* h, uint8_t* out) {
+    auto& m = static_cast<OracleScene*>(h)->S.model;
+    for (size_t t = 0; t < m.ntri(); ++t) out[t] = m.back_facing.empty() ? 0 : m.back_facing[t];
+    return 0;
+}
+
+int orc_trace(void* h, int n, const float* ro, const float* rd, int use_cull, int* prim, float* bt, int64_t* counters) {
+    auto& S = static_cast<OracleScene*>(h)->S;
+    for (int i = 0; i < n; ++i) {
+        Ray r{{ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]}, {rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]}};
+        Octree::Hit hh = S.octree.Traverse(r, use_cull != 0);
+        prim[i] = hh.tri;
+        bt[4 * i] = hh.isect.b0; bt[4 * i + 1] = hh.isect.b1; bt[4 * i + 2] = hh.isect.b2; bt[4 * i + 3] = hh.isect.t;
+        if (hh.tri < 0) { bt[4 * i] = bt[4 * i + 1] = bt[4 * i + 2] = bt[4 * i + 3] = 0; }
+        if (counters) { counters[0] += hh.nodes_tested; counters[1] += hh.tris_tested; }
+    }
+    return 0;
+}
+
+int orc_samples(void* h, int n, const int* pixel_ids, const int* indices, rt_sample_record* out) {
+    auto* o = static_cast<OracleScene*>(h);
+    for (int i = 0; i < n; ++i) {
+        Sampler s = o->S.sampler;
+        float px4[4] = {0, 0, 0, 0};
+        SampleRecord rec{};
+        rec.prim = -1;
+        EvaluatePixel(o->S, s, pixel_ids[i], indices[i], o->path, px4, &rec, nullptr);
+        static_assert(sizeof(SampleRecord) == sizeof(rt_sample_record), "record layout");
+        std::memcpy(&out[i], &rec, sizeof(rec));
+    }
+    return 0;
+}
+
+// Render sample indices [ib, ie) for the given pixels (all pixels if pixel_ids == NULL) into film
+// (4 floats per pixel, res_x*res_y), nthreads host threads with contiguous pixel ranges and a
+// per-thread sampler (RayTracerTestApp.h:372-397).  counters[5]: nodes, tris, hits, rays, shadow rays.
+int orc_render(void* h, int ib, int ie, float* film, int nthreads, int64_t* counters, const int* pixel_ids, int n_pixels) {
+    auto* o = static_cast<OracleScene*>(h);
+    int npx = pixel_ids ? n_pixels : o->S.resX * o->S.resY;
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> pool;
+    std::vector<std::array<long, 5>> cnt(nthreads);
+    int per = npx / nthreads;
+    int begin = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        int end = (t == nthreads - 1) ? npx : begin + per;
+        pool.emplace_back([=, &cnt]() {
+            Sampler s = o->S.sampler;
+            long c[5] = {0, 0, 0, 0, 0};
+            for (int j = begin; j < end; ++j) {
+                int pid = pixel_ids ? pixel_ids[j] : j;
+                for (int idx = ib; idx < ie; ++idx) {
+                    long* cc = c;
+                    if (!o->path) c[3] += 1;
+                    EvaluatePixel(o->S, s, pid, idx, o->path, film + 4 * (size_t)pid, nullptr, cc);
+                }
+            }
+            for (int k = 0; k < 5; ++k) cnt[t][k] = c[k];
+        });
+        begin = end;
+    }
+    for (auto& th : pool) th.join();
+    if (counters)
+        for (auto& c : cnt)
+            for (int k = 0; k < 5; ++k) counters[k] += c[k];
+    return 0;
+}
+
+// a20 resolve: rgbsum/weightsum -> XYZFromSensorRGB -> sRGB RGBFromXYZ -> clamp -> 255*v truncated
+void orc_resolve(void* h, const float* film, uint8_t* out) {
+    auto* o = static_cast<OracleScene*>(h);
+    int n = o->S.resX * o->S.resY;
+    for (int i = 0; i < n; ++i) {
+        float w = film[4 * i + 3];
+        vec3 s = {film[4 * i] / w, film[4 * i + 1] / w, film[4 * i + 2] / w};
+        vec3 xyz = mul(o->xyzFromSensor, s);
+        vec3 rgb = mul(o->rgbFromXyz, xyz);
+        float v[3] = {gclamp(rgb.x, 0.0f, 1.0f), gclamp(rgb.y, 0.0f, 1.0f), gclamp(rgb.z, 0.0f, 1.0f)};
+        for (int c = 0; c < 3; ++c) {
+            float f = 255.0f * v[c];
+            out[3 * i + c] = (f == f) ? (uint8_t)f : 0;  // NaN (empty pixel) -> 0
+        }
+    }
+}
+void orc_resolve_matrices(void* h, float* xyz_from_sensor9, float* rgb_from_xyz9) {
+    auto* o = static_cast<OracleScene*>(h);
+    std::memcpy(xyz_from_sensor9, o->xyzFromSensor.m, 36);
+    std::memcpy(rgb_from_xyz9, o->rgbFromXyz.m, 36);
+}
+
+}  // extern "C"

@@ -1,0 +1,135 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle on the same inputs.
+
+Bar: bit-exact hit primitive ids, barycentrics, t, rays, wavelengths, per-sample
+radiance/RGB and the accumulated film for the reference integrator; bit-exact films for the build-defined
+path integrator (same op order on both sides; tolerance 0, stated per test).
+"""
+import numpy as np
+import pytest
+
+from computational_ray_tracer_amd import scene
+from computational_ray_tracer_amd.renderer import Renderer, records_to_arrays
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def cfg0_small():
+    return scene.cfg0_reference(res=(96, 96), frequency=16, n_index=11)
+
+
+@pytest.fixture(scope="module")
+def pair_small(cfg0_small, oracle_lib):
+    return Renderer(cfg0_small), oracle_lib.OracleScene(cfg0_small)
+
+
+def test_octree_matches_oracle(pair_small):
+    g, o = pair_small
+    a, b = g.octree(), o.octree()
+    assert np.array_equal(bits(a["bounds"]), bits(b["bounds"]))
+    assert np.array_equal(a["child"], b["child"])
+    assert np.array_equal(a["leaf_count"], b["leaf_count"])
+    assert np.array_equal(a["refs"], b["refs"])
+
+
+def _camera_rays(o, n, seed):
+    rng = np.random.default_rng(seed)
+    pix = rng.integers(0, o.res[0] * o.res[1], n)
+    idx = rng.integers(0, 11, n)
+    recs = records_to_arrays(o.samples(pix, idx))
+    return recs["ro"], recs["rd"]
+
+
+@pytest.mark.parametrize("use_cull", [True, False])
+def test_trace_camera_rays_bitexact(pair_small, use_cull):
+    g, o = pair_small
+    ro, rd = _camera_rays(o, 20000, 1)
+    pg, bg = g.trace(ro, rd, use_cull)
+    po, bo, _ = o.trace(ro, rd, use_cull)
+    assert (po >= 0).mean() > 0.2
+    assert np.array_equal(pg, po)
+    assert np.array_equal(bits(bg), bits(bo))
+
+
+def test_trace_random_rays_bitexact(pair_small):
+    g, o = pair_small
+    rng = np.random.default_rng(7)
+    n = 20000
+    # rays from a shell around the mesh towards random points inside its bounds
+    ob = o.octree()["bounds"][0]
+    c = (ob[:3] + ob[3:]) / 2
+    ext = (ob[3:] - ob[:3])
+    ro = (c + rng.normal(size=(n, 3)) * ext).astype(np.float32)
+    tgt = (c + (rng.random((n, 3)) - 0.5) * ext * 0.8).astype(np.float32)
+    d = tgt - ro
+    rd = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    # include axis-aligned directions (d[i] == 0 → ±inf slabs, NaN handling in Bounds3::IntersectP)
+    rd[:50] = np.eye(3, dtype=np.float32)[np.arange(50) % 3] * np.where(np.arange(50) % 2, 1, -1)[:, None]
+    pg, bg = g.trace(ro, rd, False)
+    po, bo, _ = o.trace(ro, rd, False)
+    assert np.array_equal(pg, po)
+    assert np.array_equal(bits(bg), bits(bo))
+
+
+def test_sample_records_bitexact(pair_small):
+    g, o = pair_small
+    rng = np.random.default_rng(3)
+    pix = rng.integers(0, 96 * 96, 4096)
+    idx = rng.integers(0, 11, 4096)
+    rg = records_to_arrays(g.samples(pix, idx))
+    ro_ = records_to_arrays(o.samples(pix, idx))
+    for k in ("lam", "pdf", "ro", "rd", "prim", "b", "L", "rgb", "weight"):
+        assert np.array_equal(np.ascontiguousarray(rg[k]).view(np.uint32), np.ascontiguousarray(ro_[k]).view(np.uint32)), k
+
+
+def test_cfg0_small_film_bitexact(pair_small):
+    g, o = pair_small
+    fg = g.render_pass(0, 11)
+    fo = o.render(0, 11)
+    assert np.array_equal(bits(fg), bits(fo))
+    # progressive passes accumulate exactly like one batched pass (RayTracerTestApp.h:420-422)
+    f2 = g.new_film()
+    for i in range(11):
+        g.render_pass(i, i + 1, f2)
+    assert np.array_equal(bits(f2), bits(fo))
+
+
+def test_cfg0_full_reference_workload_bitexact(oracle_lib):
+    """SURVEY §8(d) CFG0 at full size: 500x500, indices 0..10, ~20k-triangle octree mesh (2.75 M samples)."""
+    cfg = scene.cfg0_reference()
+    g = Renderer(cfg)
+    fg = g.render_pass(0, 11)
+    fo = oracle_lib.OracleScene(cfg).render(0, 11)
+    assert np.array_equal(bits(fg), bits(fo))
+    st = g.stats()
+    assert st["samples"] == 500 * 500 * 11
+
+
+def test_resolve_matches_oracle(pair_small):
+    g, o = pair_small
+    f = o.render(0, 3)
+    assert np.array_equal(g.resolve(f), o.resolve(f))
+
+
+def test_cornell_path_film_bitexact(oracle_lib):
+    cfg = scene.cfg_cornell(res=(64, 64), spp_side=4)
+    g = Renderer(cfg)
+    fg = g.render_pass(0, 16)
+    fo = oracle_lib.OracleScene(cfg).render(0, 16)
+    bad = np.any(bits(fg) != bits(fo), axis=1)
+    assert bad.sum() == 0, f"{bad.sum()} pixels differ; max |diff| {np.abs(fg - fo).max()}"
+
+
+def test_shards_sum_to_full_film(oracle_lib):
+    cfg = scene.cfg_cornell(res=(80, 48), spp_side=2)
+    full = Renderer(cfg).render_pass(0, 4)
+    acc = np.zeros_like(full)
+    for sid in range(3):
+        r = Renderer(cfg)
+        r.set_shard(16, 3, sid)
+        acc += r.render_pass(0, 4)
+    assert np.array_equal(bits(acc), bits(full))
