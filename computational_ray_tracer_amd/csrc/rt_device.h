@@ -14,8 +14,21 @@ namespace rtmi {
 
 #define RT_DEV __device__ __forceinline__
 
-RT_DEV float f_cos(float x) { return (float)cos((double)x); }
-RT_DEV float f_sin(float x) { return (float)sin((double)x); }
+// sin/cos: fixed float algorithm shared (as a definition, not as code) with the oracle — Cody-Waite reduction
+// by pi/2 + Cephes minimax polynomials with explicit fma; ~1 ulp on |x| <= 3pi/4 (concentric disk range).
+RT_DEV void sincos_det(float x, float& s, float& c) {
+    float k = __builtin_rintf(x * 0.636619772367581343f);
+    float r = __builtin_fmaf(-k, 1.57079637050628662109375f, x);
+    r = __builtin_fmaf(-k, -4.37113900018624283e-8f, r);
+    float r2 = r * r;
+    float sp = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f);
+    float sr = __builtin_fmaf(sp * r2, r, r);
+    float cp = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2, 4.166664568298827e-2f);
+    float cr = __builtin_fmaf(cp * r2, r2, __builtin_fmaf(-0.5f, r2, 1.0f));
+    int q = (int)k & 3;
+    s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
+    c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
+}
 RT_DEV float f_atanh(float x) { return (float)atanh((double)x); }
 RT_DEV float f_cosh(float x) { return (float)cosh((double)x); }
 
@@ -203,8 +216,10 @@ RT_DEV void disk_concentric(float u0, float u1, float& ox, float& oy) {  // Samp
     float theta, r;
     if (fabsf(x) > fabsf(y)) { r = x; theta = 0.78539816339744830961f * (y / x); }
     else { r = y; theta = 1.57079632679489661923f - 0.78539816339744830961f * (x / y); }
-    ox = r * f_cos(theta);
-    oy = r * f_sin(theta);
+    float sn, cs;
+    sincos_det(theta, sn, cs);
+    ox = r * cs;
+    oy = r * sn;
 }
 
 // ------------------------------------------------------------------------------------ spectra

@@ -24,6 +24,8 @@ using namespace rtmi;
 
 namespace {
 
+constexpr int kQStride = 64;  // ints between queue counters: 256 B apart, never in one cache line
+
 // ------------------------------------------------------------------------------ host float math
 // glm operation order, float, -ffp-contract=off (same contract as the device code)
 struct F3 { float x, y, z; float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); } };
@@ -263,7 +265,7 @@ struct rt_ctx {
     float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr, *LdA = nullptr, *LdB = nullptr;
     int *slot = nullptr, *hitPrim = nullptr, *qSlot = nullptr, *sSlot = nullptr, *dim = nullptr;
     uint4* rng = nullptr;
-    int* d_qcount = nullptr;   // [0],[1] ping-pong queues, [2] shadow
+    int* d_qcount = nullptr;   // ping-pong queue lengths at [0] and [kQStride] (separate cache lines)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     size_t film_cap = 0;
@@ -487,18 +489,19 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 float4* cO = c->rayO + (size_t)cur * nmax;
                 float4* cD = c->rayD + (size_t)cur * nmax;
                 int* cS = c->slot + (size_t)cur * nmax;
-                HIPCHK(c, hipMemsetAsync(c->d_qcount + nxt, 0, sizeof(int), st));
-                HIPCHK(c, hipMemsetAsync(c->d_qcount + 2, 0, sizeof(int), st));
-                TraceIO tio{cO, cD, c->d_qcount + cur, 0, 0, c->hitB, c->hitPrim};
+                int* qc_cur = c->d_qcount + kQStride * cur;
+                int* qc_nxt = c->d_qcount + kQStride * nxt;
+                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, sizeof(int), st));
+                TraceIO tio{cO, cD, qc_cur, 0, 0, c->hitB, c->hitPrim};
                 e0 = ev_start(c, st);
                 HIPCHK(c, launch_trace_closest(st, c->grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
                 ev_mark(c, st, ST_TRACE, e0);
                 PathIO pio{};
-                pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = c->d_qcount + cur;
+                pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = qc_cur;
                 pio.hitB = c->hitB; pio.hitPrim = c->hitPrim;
                 pio.nO = c->rayO + (size_t)nxt * nmax; pio.nD = c->rayD + (size_t)nxt * nmax;
-                pio.nSlot = c->slot + (size_t)nxt * nmax; pio.nCount = c->d_qcount + nxt;
-                pio.sO = c->sO; pio.sD = c->sD; pio.sSlot = c->sSlot; pio.sCount = c->d_qcount + 2;
+                pio.nSlot = c->slot + (size_t)nxt * nmax; pio.nCount = qc_nxt;
+                pio.sO = c->sO; pio.sD = c->sD; pio.sSlot = c->sSlot; pio.sCount = nullptr;
                 pio.rng = c->rng; pio.dim = c->dim; pio.betaA = c->betaA; pio.betaB = c->betaB;
                 pio.LA = c->LA; pio.LB = c->LB; pio.LdA = c->LdA; pio.LdB = c->LdB;
                 pio.lamA = c->lamA; pio.lamB = c->lamB; pio.pdfA = c->pdfA; pio.pdfB = c->pdfB;
@@ -506,7 +509,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 e0 = ev_start(c, st);
                 HIPCHK(c, launch_path_shade(st, c->grid, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
                 ev_mark(c, st, ST_SHADE, e0);
-                ShadowIO shio{c->sO, c->sD, c->sSlot, c->d_qcount + 2, c->LA, c->LB, c->LdA, c->LdB};
+                ShadowIO shio{c->sO, c->sD, c->sSlot, qc_cur, c->LA, c->LB, c->LdA, c->LdB};
                 e0 = ev_start(c, st);
                 HIPCHK(c, launch_trace_shadow(st, c->grid, c->dsc.qcap, c->dsc, shio, c->d_ctr));
                 ev_mark(c, st, ST_SHADOW, e0);
@@ -546,7 +549,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     }
     c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
     c->hs.init();
-    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 4) != hipSuccess ||
+    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 2 * kQStride) != hipSuccess ||
         dalloc(&c->d_ctr, (size_t)C_NCOUNTERS) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
         rt_destroy(c);
         return RT_E_OOM;

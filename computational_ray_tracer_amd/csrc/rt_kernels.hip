@@ -34,6 +34,27 @@ __device__ __forceinline__ int wave_append(int* counter, bool pred) {
     return pred ? base + rank : -1;
 }
 
+// Block-aggregated append: one atomicAdd per *block* (the queue counters are the contended words —
+// one wave-level atomic per wave saturated a single counter, MI355X_MICROARCH "dequeue" ≈88/µs).
+// Every thread of the block must call it (block-uniform control flow).
+__device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
+    constexpr int NW = kBlock / 64;
+    uint64_t mask = __ballot(pred);
+    int wave = threadIdx.x >> 6;
+    int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    if (lane_id() == 0) lds[wave] = __popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < NW; ++w) { int cw = lds[w]; lds[w] = tot; tot += cw; }
+        lds[NW] = tot ? atomicAdd(counter, tot) : 0;
+    }
+    __syncthreads();
+    int base = lds[NW] + lds[wave];
+    __syncthreads();
+    return pred ? base + rank : -1;
+}
+
 __device__ __forceinline__ void count_add(unsigned long long* ctr, int slot, unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -123,6 +144,18 @@ __global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevC
     }
 }
 
+// Loads through the constant address space: with a wave-uniform index they become s_load (scalar cache).
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ldc4(const float4* p, int i) {
+    f4v v = ((const __attribute__((address_space(4))) f4v*)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ int2 ldc2i(const int2* p, int i) {
+    i2v v = ((const __attribute__((address_space(4))) i2v*)p)[i];
+    return make_int2(v.x, v.y);
+}
+
 // ===================================================================================== K2 traverse
 // Octtree_Model.h:66-127 — FIFO BFS.  The 8 children of an internal node are contiguous, so the queue
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
@@ -137,6 +170,28 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     int best = -1;
     const int2* __restrict__ lr = sc.leafRange[set];
     const float4* __restrict__ tiles = sc.tiles[set];
+    if constexpr (QCAP == 1) {
+        // The whole octree is one leaf (e.g. the 36-triangle Cornell box: 36 < TRIANGLE_CAPACITY): every
+        // lane walks the same triangle list, so it is read through the scalar cache (s_load_dwordx4) into
+        // SGPRs once per wave instead of 64 identical vector loads per triangle.
+        ++nn;
+        bool inside = box_hit(ldc4(sc.nodeA, 0), ldc4(sc.nodeB, 0), o, inv, tMax);
+        int2 r = ldc2i(lr, 0);
+        if (inside) {
+            for (int k = 0; k < r.y; ++k) {
+                int e = 3 * (r.x + k);
+                float4 A = ldc4(tiles, e), B = ldc4(tiles, e + 1), Cc = ldc4(tiles, e + 2);
+                ++nt;
+                float b0, b1, b2, t;
+                if (tri_intersect(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                    best = __float_as_int(Cc.y);
+                    if (ANYHIT) return best;
+                    tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+                }
+            }
+        }
+        return best;
+    }
     int q[QCAP];
     int head = 0, tail = 0;
     int n = 0;       // current node
@@ -197,10 +252,12 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
 // any-hit shadow rays (build-defined path mode): occluded iff some accepting triangle has t < tMax
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_trace_shadow(DevScene sc, ShadowIO io, unsigned long long* ctr) {
-    int n = *io.sCount;
+    int n = *io.sCount;  // length of the path queue the shadow rays were emitted from
     unsigned long long nn = 0, nt = 0, nr = 0;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        float4 o4 = io.sO[k], d4 = io.sD[k];
+        float4 d4 = io.sD[k];
+        if (!(d4.w > 0)) continue;
+        float4 o4 = io.sO[k];
         float b0, b1, b2, t;
         int hit = traverse<QCAP, true>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, b0, b1, b2, t, nn, nt);
         if (hit < 0) {
@@ -303,6 +360,7 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
                                                        SampleIds ids, PathIO io, unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
+    __shared__ int lds[kBlock / 64 + 1];
     int n = *io.count;
     for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         int k = base + threadIdx.x;
@@ -401,9 +459,13 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                 }
             }
         }
-        int ks = wave_append(io.sCount, wantShadow);
-        if (wantShadow) { io.sO[ks] = sO; io.sD[ks] = sD; io.sSlot[ks] = slot; }
-        int kn = wave_append(io.nCount, wantNext);
+        // shadow rays keep the queue position of their path (no compaction: most paths emit one);
+        // sD.w = tMax, 0 marks "no shadow ray"
+        if (k < n) {
+            io.sD[k] = sD;
+            if (wantShadow) { io.sO[k] = sO; io.sSlot[k] = slot; }
+        }
+        int kn = block_append(io.nCount, wantNext, lds);
         if (wantNext) { io.nO[kn] = nO; io.nD[kn] = nD; io.nSlot[kn] = slot; }
     }
 }

@@ -46,8 +46,24 @@ static inline float gamma_(int n) {
 }
 
 // ------------------------------------------------ transcendentals (documented build choice)
-static inline float cos_f(float x) { return (float)std::cos((double)x); }
-static inline float sin_f(float x) { return (float)std::sin((double)x); }
+// sin/cos: a fixed float algorithm (Cody-Waite reduction by pi/2 + Cephes minimax polynomials, explicit
+// fmaf) evaluated identically on host and device; accurate to ~1 ulp on the |x| <= 3pi/4 range the
+// concentric-disk warp (Sampling.h:383-403) produces.  atanh/cosh: double evaluation rounded to float.
+static inline void sincos_det(float x, float* s, float* c) {
+    float k = std::rint(x * 0.636619772367581343f);
+    float r = std::fmaf(-k, 1.57079637050628662109375f, x);
+    r = std::fmaf(-k, -4.37113900018624283e-8f, r);
+    float r2 = r * r;
+    float sp = std::fmaf(std::fmaf(-1.9515295891e-4f, r2, 8.3321608736e-3f), r2, -1.6666654611e-1f);
+    float sr = std::fmaf(sp * r2, r, r);
+    float cp = std::fmaf(std::fmaf(2.443315711809948e-5f, r2, -1.388731625493765e-3f), r2, 4.166664568298827e-2f);
+    float cr = std::fmaf(cp * r2, r2, std::fmaf(-0.5f, r2, 1.0f));
+    int q = (int)k & 3;
+    *s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
+    *c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
+}
+static inline float cos_f(float x) { float s, c; sincos_det(x, &s, &c); return c; }
+static inline float sin_f(float x) { float s, c; sincos_det(x, &s, &c); return s; }
 static inline float atanh_f(float x) { return (float)std::atanh((double)x); }
 static inline float cosh_f(float x) { return (float)std::cosh((double)x); }
 
