@@ -25,6 +25,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 from computational_ray_tracer_amd import scene  # noqa: E402
+from computational_ray_tracer_amd.distributed import reduce_film  # noqa: E402
 from computational_ray_tracer_amd.renderer import Renderer  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -106,7 +107,7 @@ def main():
         r.render_pass_device(i0, i1, film.data_ptr(), stream.cuda_stream)
         cursor[0] = 0 if i1 >= spp else i1
         if world > 1:
-            dist.reduce(film, dst=0)  # RCCL over xGMI (each pixel owned by one rank: exact sum)
+            reduce_film(film, dst=0)  # RCCL over xGMI (each pixel owned by one rank: exact sum)
         return (i1 - i0)
 
     for _ in range(a.warmup):

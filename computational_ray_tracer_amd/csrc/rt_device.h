@@ -272,10 +272,16 @@ struct TriRay {
     float ox, oy, oz;     // ray origin, permuted
 };
 RT_DEV float sel3(int k, float x, float y, float z) { return k == 0 ? x : (k == 1 ? y : z); }
+RT_DEV int dominant_axis(V3 d) {  // helpers.h:64-66 MaxComponentIndex(Abs(d))
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    return (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);
+}
+// KZ >= 0: the caller guarantees dominant_axis(d) == KZ, so the permutation is resolved at compile time
+// (no per-triangle selects); KZ < 0: per-lane permutation.
+template <int KZ>
 RT_DEV TriRay make_triray(V3 o, V3 d) {
     TriRay t;
-    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-    t.kz = (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);  // helpers.h:64-66
+    t.kz = KZ >= 0 ? KZ : dominant_axis(d);
     t.kx = t.kz + 1; if (t.kx == 3) t.kx = 0;
     t.ky = t.kx + 1; if (t.ky == 3) t.ky = 0;
     float dx = sel3(t.kx, d.x, d.y, d.z), dy = sel3(t.ky, d.x, d.y, d.z), dz = sel3(t.kz, d.x, d.y, d.z);
@@ -285,12 +291,15 @@ RT_DEV TriRay make_triray(V3 o, V3 d) {
 }
 // Shapes.h:1101-1260 Triangle::BasicIntersect on pre-transformed world vertices (degenerate triangles were
 // removed from the tiles at upload, Shapes.h:1131).  Returns true and (b0,b1,b2,t) on a hit.
+template <int KZ>
 RT_DEV bool tri_intersect(const TriRay& R, float tMax, float4 A, float4 B, float4 Cc, float& b0, float& b1, float& b2,
                           float& tt) {
+    constexpr int KX = KZ == 0 ? 1 : (KZ == 1 ? 2 : 0), KY = KZ == 0 ? 2 : (KZ == 1 ? 0 : 1);
+    const int kx = KZ >= 0 ? KX : R.kx, ky = KZ >= 0 ? KY : R.ky, kz = KZ >= 0 ? KZ : R.kz;
     // vertices p0=(A.x,A.y,A.z) p1=(A.w,B.x,B.y) p2=(B.z,B.w,C.x); translate after permuting (same ops)
-    float p0x = sel3(R.kx, A.x, A.y, A.z) - R.ox, p0y = sel3(R.ky, A.x, A.y, A.z) - R.oy, p0z = sel3(R.kz, A.x, A.y, A.z) - R.oz;
-    float p1x = sel3(R.kx, A.w, B.x, B.y) - R.ox, p1y = sel3(R.ky, A.w, B.x, B.y) - R.oy, p1z = sel3(R.kz, A.w, B.x, B.y) - R.oz;
-    float p2x = sel3(R.kx, B.z, B.w, Cc.x) - R.ox, p2y = sel3(R.ky, B.z, B.w, Cc.x) - R.oy, p2z = sel3(R.kz, B.z, B.w, Cc.x) - R.oz;
+    float p0x = sel3(kx, A.x, A.y, A.z) - R.ox, p0y = sel3(ky, A.x, A.y, A.z) - R.oy, p0z = sel3(kz, A.x, A.y, A.z) - R.oz;
+    float p1x = sel3(kx, A.w, B.x, B.y) - R.ox, p1y = sel3(ky, A.w, B.x, B.y) - R.oy, p1z = sel3(kz, A.w, B.x, B.y) - R.oz;
+    float p2x = sel3(kx, B.z, B.w, Cc.x) - R.ox, p2y = sel3(ky, B.z, B.w, Cc.x) - R.oy, p2z = sel3(kz, B.z, B.w, Cc.x) - R.oz;
     p0x += R.Sx * p0z; p0y += R.Sy * p0z;
     p1x += R.Sx * p1z; p1y += R.Sy * p1z;
     p2x += R.Sx * p2z; p2y += R.Sy * p2z;

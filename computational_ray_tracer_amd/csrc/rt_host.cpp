@@ -261,9 +261,9 @@ struct rt_ctx {
     // workspace (grown on demand)
     size_t cap = 0;
     float4 *rayO = nullptr, *rayD = nullptr, *lamA = nullptr, *lamB = nullptr, *pdfA = nullptr, *pdfB = nullptr;
-    float4 *hitB = nullptr, *qO = nullptr, *qD = nullptr, *sO = nullptr, *sD = nullptr;
-    float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr, *LdA = nullptr, *LdB = nullptr;
-    int *slot = nullptr, *hitPrim = nullptr, *qSlot = nullptr, *sSlot = nullptr, *dim = nullptr;
+    float4* hitB = nullptr;
+    float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr;
+    int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
     uint4* rng = nullptr;
     int* d_qcount = nullptr;   // ping-pong queue lengths at [0] and [kQStride] (separate cache lines)
     unsigned long long* d_ctr = nullptr;
@@ -304,14 +304,13 @@ void free_scene(rt_ctx* c) {
 }
 
 void free_workspace(rt_ctx* c) {
-    void* ptrs[] = {c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->qO, c->qD, c->sO, c->sD,
-                    c->betaA, c->betaB, c->LA, c->LB, c->LdA, c->LdB, c->slot, c->hitPrim, c->qSlot, c->sSlot,
-                    c->dim, c->rng};
+    void* ptrs[] = {c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->betaA, c->betaB,
+                    c->LA, c->LB, c->slot, c->hitPrim, c->dim, c->rng};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    c->rayO = c->rayD = c->lamA = c->lamB = c->pdfA = c->pdfB = c->hitB = c->qO = c->qD = c->sO = c->sD = nullptr;
-    c->betaA = c->betaB = c->LA = c->LB = c->LdA = c->LdB = nullptr;
-    c->slot = c->hitPrim = c->qSlot = c->sSlot = c->dim = nullptr;
+    c->rayO = c->rayD = c->lamA = c->lamB = c->pdfA = c->pdfB = c->hitB = nullptr;
+    c->betaA = c->betaB = c->LA = c->LB = nullptr;
+    c->slot = c->hitPrim = c->dim = nullptr;
     c->rng = nullptr;
     c->cap = 0;
 }
@@ -325,10 +324,8 @@ int ensure_workspace(rt_ctx* c, size_t n, bool path) {
     HIPCHK(c, dalloc(&c->pdfA, n)); HIPCHK(c, dalloc(&c->pdfB, n));
     HIPCHK(c, dalloc(&c->hitB, n)); HIPCHK(c, dalloc(&c->hitPrim, n));
     if (path) {
-        HIPCHK(c, dalloc(&c->sO, n)); HIPCHK(c, dalloc(&c->sD, n)); HIPCHK(c, dalloc(&c->sSlot, n));
         HIPCHK(c, dalloc(&c->betaA, n)); HIPCHK(c, dalloc(&c->betaB, n));
         HIPCHK(c, dalloc(&c->LA, n)); HIPCHK(c, dalloc(&c->LB, n));
-        HIPCHK(c, dalloc(&c->LdA, n)); HIPCHK(c, dalloc(&c->LdB, n));
         HIPCHK(c, dalloc(&c->dim, n)); HIPCHK(c, dalloc(&c->rng, n));
     }
     c->cap = n;
@@ -501,18 +498,13 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 pio.hitB = c->hitB; pio.hitPrim = c->hitPrim;
                 pio.nO = c->rayO + (size_t)nxt * nmax; pio.nD = c->rayD + (size_t)nxt * nmax;
                 pio.nSlot = c->slot + (size_t)nxt * nmax; pio.nCount = qc_nxt;
-                pio.sO = c->sO; pio.sD = c->sD; pio.sSlot = c->sSlot; pio.sCount = nullptr;
                 pio.rng = c->rng; pio.dim = c->dim; pio.betaA = c->betaA; pio.betaB = c->betaB;
-                pio.LA = c->LA; pio.LB = c->LB; pio.LdA = c->LdA; pio.LdB = c->LdB;
+                pio.LA = c->LA; pio.LB = c->LB;
                 pio.lamA = c->lamA; pio.lamB = c->lamB; pio.pdfA = c->pdfA; pio.pdfB = c->pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 e0 = ev_start(c, st);
-                HIPCHK(c, launch_path_shade(st, c->grid, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
+                HIPCHK(c, launch_path_shade(st, c->grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
                 ev_mark(c, st, ST_SHADE, e0);
-                ShadowIO shio{c->sO, c->sD, c->sSlot, qc_cur, c->LA, c->LB, c->LdA, c->LdB};
-                e0 = ev_start(c, st);
-                HIPCHK(c, launch_trace_shadow(st, c->grid, c->dsc.qcap, c->dsc, shio, c->d_ctr));
-                ev_mark(c, st, ST_SHADOW, e0);
                 cur = nxt;
             }
             PathFilmIO fio{c->d_work, c->n_work, nIdx, c->LA, c->LB, c->lamA, c->lamB, c->pdfA, c->pdfB, film};

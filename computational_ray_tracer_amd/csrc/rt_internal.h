@@ -104,15 +104,9 @@ struct PathIO {
     const float4* rayO; const float4* rayD; const int* slot; const int* count;
     const float4* hitB; const int* hitPrim;
     float4* nO; float4* nD; int* nSlot; int* nCount;
-    float4* sO; float4* sD; int* sSlot; int* sCount;
-    uint4* rng; int* dim; float4* betaA; float4* betaB; float4* LA; float4* LB; float4* LdA; float4* LdB;
+    uint4* rng; int* dim; float4* betaA; float4* betaB; float4* LA; float4* LB;
     const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
     int depth, max_depth;
-};
-
-struct ShadowIO {
-    const float4* sO; const float4* sD; const int* sSlot; const int* sCount;
-    float4* LA; float4* LB; const float4* LdA; const float4* LdB;
 };
 
 struct PathFilmIO {
@@ -136,10 +130,9 @@ hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, c
                                  const ShadeRefIO& io, unsigned long long* ctr);
 hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
                           const ShadeRefIO& sio, const RecordIO& io);
-hipError_t launch_path_shade(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevSampler& smp,
-                             const DevFilm& film, const SampleIds& ids, const PathIO& io, unsigned long long* ctr);
-hipError_t launch_trace_shadow(hipStream_t st, int grid, int qcap, const DevScene& sc, const ShadowIO& io,
-                               unsigned long long* ctr);
+hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
+                             const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
+                             unsigned long long* ctr);
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr);
 hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* m_xyz_from_sensor,

@@ -161,33 +161,46 @@ __device__ __forceinline__ int2 ldc2i(const int2* p, int i) {
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
 // reference's node-level FIFO order exactly.  tMax shrinks on every accepted hit ("t < tMax": the first
 // hit found in BFS order wins ties), so hit ids, barycentrics and t are bit-identical to the reference's.
-template <int QCAP, bool ANYHIT>
+template <int QCAP, bool ANYHIT, int KZ>
 __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0, float& rb1,
                                         float& rb2, float& rt, unsigned long long& nn, unsigned long long& nt) {
     V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
-    TriRay R = make_triray(o, d);
+    TriRay R = make_triray<KZ>(o, d);
     float tMax = tMaxInit;
     int best = -1;
     const int2* __restrict__ lr = sc.leafRange[set];
     const float4* __restrict__ tiles = sc.tiles[set];
     if constexpr (QCAP == 1) {
         // The whole octree is one leaf (e.g. the 36-triangle Cornell box: 36 < TRIANGLE_CAPACITY): every
-        // lane walks the same triangle list, so it is read through the scalar cache (s_load_dwordx4) into
-        // SGPRs once per wave instead of 64 identical vector loads per triangle.
+        // lane walks the same triangle list, so it is read through the scalar cache into SGPRs once per
+        // wave; four triangles (12 x s_load_dwordx4) are fetched per scalar-cache round trip.
         ++nn;
         bool inside = box_hit(ldc4(sc.nodeA, 0), ldc4(sc.nodeB, 0), o, inv, tMax);
         int2 r = ldc2i(lr, 0);
         if (inside) {
-            for (int k = 0; k < r.y; ++k) {
-                int e = 3 * (r.x + k);
-                float4 A = ldc4(tiles, e), B = ldc4(tiles, e + 1), Cc = ldc4(tiles, e + 2);
+            auto test = [&](float4 A, float4 B, float4 Cc) -> bool {
                 ++nt;
                 float b0, b1, b2, t;
-                if (tri_intersect(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                if (tri_intersect<KZ>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
                     best = __float_as_int(Cc.y);
-                    if (ANYHIT) return best;
+                    if (ANYHIT) return true;
                     tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
                 }
+                return false;
+            };
+            int k = 0;
+            for (; k + 4 <= r.y; k += 4) {
+                int e = 3 * (r.x + k);
+                float4 T[12];
+#pragma unroll
+                for (int j = 0; j < 12; ++j) T[j] = ldc4(tiles, e + j);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (test(T[3 * u], T[3 * u + 1], T[3 * u + 2]) && ANYHIT) return best;
+            }
+            for (; k < r.y; ++k) {
+                int e = 3 * (r.x + k);
+                if (test(ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2)) && ANYHIT) return best;
             }
         }
         return best;
@@ -212,7 +225,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     float4 A = tp[0], B = tp[1], Cc = tp[2];
                     ++nt;
                     float b0, b1, b2, t;
-                    if (tri_intersect(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                    if (tri_intersect<KZ>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
                         best = __float_as_int(Cc.y);
                         if (ANYHIT) return best;
                         tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
@@ -229,6 +242,19 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     return best;
 }
 
+// When every active lane of the wave has the same dominant ray axis (camera rays, kz-binned queues) the
+// watertight test's coordinate permutation is resolved at compile time; otherwise per lane.
+template <int QCAP, bool ANYHIT>
+__device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
+                                            float& b2, float& t, unsigned long long& nn, unsigned long long& nt) {
+    int kz = dominant_axis(d);
+    uint64_t act = __ballot(true);
+    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    return traverse<QCAP, ANYHIT, -1>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+}
+
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
     int n = io.count ? *io.count : io.n;
@@ -236,8 +262,8 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         float4 o4 = io.rayO[k], d4 = io.rayD[k];
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
-        int prim = traverse<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f, b0,
-                                         b1, b2, t, nn, nt);
+        int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
+                                             b0, b1, b2, t, nn, nt);
         io.hitB[k] = make_float4(b0, b1, b2, t);
         io.hitPrim[k] = prim;
         nh += prim >= 0;
@@ -247,33 +273,6 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
     count_add(ctr, C_TRIS, nt);
     count_add(ctr, C_HITS, nh);
     count_add(ctr, C_RAYS, nr);
-}
-
-// any-hit shadow rays (build-defined path mode): occluded iff some accepting triangle has t < tMax
-template <int QCAP>
-__global__ void __launch_bounds__(kBlock) k_trace_shadow(DevScene sc, ShadowIO io, unsigned long long* ctr) {
-    int n = *io.sCount;  // length of the path queue the shadow rays were emitted from
-    unsigned long long nn = 0, nt = 0, nr = 0;
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        float4 d4 = io.sD[k];
-        if (!(d4.w > 0)) continue;
-        float4 o4 = io.sO[k];
-        float b0, b1, b2, t;
-        int hit = traverse<QCAP, true>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, b0, b1, b2, t, nn, nt);
-        if (hit < 0) {
-            int slot = io.sSlot[k];
-            float L[8], Ld[8];
-            load8(io.LA, io.LB, slot, L);
-            load8(io.LdA, io.LdB, slot, Ld);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) L[i] += Ld[i];
-            store8(io.LA, io.LB, slot, L);
-        }
-        nr += 1;
-    }
-    count_add(ctr, C_SNODES, nn);
-    count_add(ctr, C_STRIS, nt);
-    count_add(ctr, C_SHADOW, nr);
 }
 
 // ======================================================================= K3 reference shading + film
@@ -355,17 +354,22 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 // ============================================================================ path mode (build-defined)
 // One bounce of the diffuse path integrator (DESIGN.md §Path mode; pbrt-v4 SimplePathIntegrator semantics):
 // emitter hit → Le at depth 0 only (one-sided), then terminate; otherwise NEE on the quad light (Get2D,
-// shadow ray emitted to the shadow queue with its pending contribution) and a cosine-hemisphere bounce
-// (Get2D, β *= R) emitted to the next queue.  Sampler state (PCG state + dimension) lives per path slot.
+// shadow ray traced inline, pending contribution added on a miss) and a cosine-hemisphere bounce
+// (Get2D, β *= R) appended to the next queue.  Sampler state (PCG state + dimension) lives per path slot.
+template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
                                                        SampleIds ids, PathIO io, unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[kBlock / 64 + 1];
     int n = *io.count;
+    unsigned long long snn = 0, snt = 0, nsh = 0;
     for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         int k = base + threadIdx.x;
         bool wantShadow = false, wantNext = false;
-        float4 sO = make_float4(0, 0, 0, 0), sD = sO, nO = sO, nD = sO;
+        float4 nO = make_float4(0, 0, 0, 0), nD = nO;
+        V3 so = v3(0, 0, 0), sd = so;
+        float stmax = 0.f;
+        float Ld[8];
         int slot = -1;
         if (k < n) {
             slot = io.slot[k];
@@ -424,14 +428,13 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                             float le = sc.materials[Lq.material].w;
                             float G = (cs * cl) / dist2;
                             float wgt = G * Lq.area;
-                            float Ld[8];
 #pragma unroll
                             for (int i = 0; i < 8; ++i)
                                 Ld[i] = ((beta[i] * (R[i] * InvPi)) * (le * dense_query(sp->D65, lam[i]))) * wgt;
-                            store8(io.LdA, io.LdB, slot, Ld);
                             wantShadow = true;
-                            sO = make_float4(po.x, po.y, po.z, 0.f);
-                            sD = make_float4(wi.x, wi.y, wi.z, dist * 0.999f);
+                            so = po;
+                            sd = wi;
+                            stmax = dist * 0.999f;
                         }
                     }
                     // --- cosine-hemisphere BSDF sample (Sampling.h:449-454), frame = pbrt CoordinateSystem
@@ -459,15 +462,26 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                 }
             }
         }
-        // shadow rays keep the queue position of their path (no compaction: most paths emit one);
-        // sD.w = tMax, 0 marks "no shadow ray"
-        if (k < n) {
-            io.sD[k] = sD;
-            if (wantShadow) { io.sO[k] = sO; io.sSlot[k] = slot; }
+        // NEE shadow ray, traced inline (any hit, fixed tMax) after the bounce state is written, so only the
+        // pending contribution Ld stays live across the traversal.  No shadow queue in HBM.
+        if (wantShadow) {
+            float b0, b1, b2, t;
+            int hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt);
+            ++nsh;
+            if (hit < 0) {
+                float L[8];
+                load8(io.LA, io.LB, slot, L);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) L[i] += Ld[i];
+                store8(io.LA, io.LB, slot, L);
+            }
         }
         int kn = block_append(io.nCount, wantNext, lds);
         if (wantNext) { io.nO[kn] = nO; io.nD[kn] = nD; io.nSlot[kn] = slot; }
     }
+    count_add(ctr, C_SNODES, snn);
+    count_add(ctr, C_STRIS, snt);
+    count_add(ctr, C_SHADOW, nsh);
 }
 
 // sensor + film for path mode (pixel-owned, index order)
@@ -542,20 +556,6 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
     return hipGetLastError();
 }
 
-hipError_t launch_trace_shadow(hipStream_t st, int grid, int qcap, const DevScene& sc, const ShadowIO& io,
-                               unsigned long long* ctr) {
-    dim3 g(grid > 0 ? grid : 1), b(kBlock);
-    switch (qcap) {
-        case 1: hipLaunchKernelGGL(k_trace_shadow<1>, g, b, 0, st, sc, io, ctr); break;
-        case 16: hipLaunchKernelGGL(k_trace_shadow<16>, g, b, 0, st, sc, io, ctr); break;
-        case 64: hipLaunchKernelGGL(k_trace_shadow<64>, g, b, 0, st, sc, io, ctr); break;
-        case 256: hipLaunchKernelGGL(k_trace_shadow<256>, g, b, 0, st, sc, io, ctr); break;
-        case 1024: hipLaunchKernelGGL(k_trace_shadow<1024>, g, b, 0, st, sc, io, ctr); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
                                  const ShadeRefIO& io, unsigned long long* ctr) {
     hipLaunchKernelGGL(k_ref_shade_film, dim3(grid_for(io.n_pixels, grid)), dim3(kBlock), 0, st, sc, sp, film, io, ctr);
@@ -568,9 +568,18 @@ hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* 
     return hipGetLastError();
 }
 
-hipError_t launch_path_shade(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevSampler& smp,
-                             const DevFilm& film, const SampleIds& ids, const PathIO& io, unsigned long long* ctr) {
-    hipLaunchKernelGGL(k_path_shade, dim3(grid > 0 ? grid : 1), dim3(kBlock), 0, st, sc, sp, smp, film, ids, io, ctr);
+hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
+                             const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
+                             unsigned long long* ctr) {
+    dim3 g(grid > 0 ? grid : 1), b(kBlock);
+    switch (qcap) {
+        case 1: hipLaunchKernelGGL(k_path_shade<1>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
+        case 16: hipLaunchKernelGGL(k_path_shade<16>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
+        case 64: hipLaunchKernelGGL(k_path_shade<64>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
+        case 256: hipLaunchKernelGGL(k_path_shade<256>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
+        case 1024: hipLaunchKernelGGL(k_path_shade<1024>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

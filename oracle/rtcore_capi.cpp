@@ -87,10 +87,12 @@ uint64_t orc_hash_pixel(int x, int y, int seed) { return Hash(x, y, seed); }
 uint64_t orc_hash_pixel_dim(int x, int y, int dim, int seed) { return Hash(x, y, dim, seed); }
 int orc_permutation_element(uint32_t i, uint32_t l, uint32_t p) { return PermutationElement(i, l, p); }
 
-// mode 0: default-constructed RNG; mode 1: SetSequence(seq) then Advance(advance)
+// mode 0: default-constructed RNG; mode 1: SetSequence(seq) then Advance(advance);
+// mode 2: SetSequence(seq, seed = advance) (rng.h:113-119 with an explicit seed, = pcg32_srandom)
 void orc_pcg_draws(int mode, uint64_t seq, int64_t advance, int n, uint32_t* out) {
     RNG r;
     if (mode == 1) { r.SetSequence(seq); r.Advance(advance); }
+    if (mode == 2) r.SetSequence(seq, (uint64_t)advance);
     for (int i = 0; i < n; ++i) out[i] = r.UniformU32();
 }
 

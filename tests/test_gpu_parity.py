@@ -125,11 +125,35 @@ def test_cornell_path_film_bitexact(oracle_lib):
 
 
 def test_shards_sum_to_full_film(oracle_lib):
+    from computational_ray_tracer_amd.distributed import shard_pixels
     cfg = scene.cfg_cornell(res=(80, 48), spp_side=2)
     full = Renderer(cfg).render_pass(0, 4)
     acc = np.zeros_like(full)
     for sid in range(3):
         r = Renderer(cfg)
         r.set_shard(16, 3, sid)
-        acc += r.render_pass(0, 4)
+        part = r.render_pass(0, 4)
+        owned = np.zeros(80 * 48, bool)
+        owned[shard_pixels((80, 48), 16, 3, sid)] = True
+        assert np.array_equal(part[:, 3] > 0, owned)  # the library owns exactly the Python-mirrored tiles
+        acc += part
     assert np.array_equal(bits(acc), bits(full))
+
+
+def test_octree_path_mode_bfs_queue(oracle_lib):
+    """Path integrator on a multi-level octree (BFS group queue in use), bit-exact vs the oracle."""
+    base = scene.cfg0_reference(res=(48, 48), frequency=16, n_index=4)
+    m = base.model
+    m.cull_backfaces = False
+    m.materials = [(scene.CORNELL_WHITE, 0.0), ((0.0, 0.0, 0.0), 40.0)]
+    m.tri_material = np.zeros(len(m.indices), np.int32)
+    m.lights = [dict(p=(-150.0, 250.0, 650.0), e1=(300.0, 0.0, 0.0), e2=(0.0, 0.0, 300.0), n=(0.0, -1.0, 0.0),
+                     material=1)]
+    from computational_ray_tracer_amd import capi
+    cfg = scene.Config("mesh_path", m, base.camera, scene.StratifiedSampler(2, 2, True, 0), base.film,
+                       scene.Integrator(capi.RT_INTEGRATOR_PATH, max_depth=3), 0, 4)
+    g = Renderer(cfg)
+    assert g.octree()["max_queue_groups"] > 1
+    fg = g.render_pass(0, 4)
+    fo = oracle_lib.OracleScene(cfg).render(0, 4)
+    assert np.array_equal(bits(fg), bits(fo))
