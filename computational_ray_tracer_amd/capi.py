@@ -115,7 +115,7 @@ def load_library(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("RTMI_LIB", LIB_PATH))  # RTMI_LIB: A/B kernel variants
     if not p.exists():
         raise RuntimeError(f"{p} is missing: build it with `python __graft_entry__.py build` "
                            "(the MI355X HIP extension is the only implementation of the hot path)")

@@ -306,12 +306,17 @@ RT_DEV bool tri_intersect(const TriRay& R, float tMax, float4 A, float4 B, float
     float e0 = dop(p1x, p2y, p1y, p2x);
     float e1 = dop(p2x, p0y, p2y, p0x);
     float e2 = dop(p0x, p1y, p0y, p1x);
-    if (e0 == 0.0f || e1 == 0.0f || e2 == 0.0f) {  // Shapes.h:1174-1184
+    // Same decisions as Shapes.h:1174-1190, ordered so the common miss (no zero edge, mixed signs) leaves
+    // through a single branch: the double-precision fallback only ever runs when some edge is exactly 0.
+    bool zero = (e0 == 0.0f) | (e1 == 0.0f) | (e2 == 0.0f);
+    bool mixed = ((e0 < 0) | (e1 < 0) | (e2 < 0)) & ((e0 > 0) | (e1 > 0) | (e2 > 0));
+    if (!zero & mixed) return false;
+    if (zero) {  // Shapes.h:1174-1184
         e0 = (float)((double)p2y * (double)p1x - (double)p2x * (double)p1y);
         e1 = (float)((double)p0y * (double)p2x - (double)p0x * (double)p2y);
         e2 = (float)((double)p1y * (double)p0x - (double)p1x * (double)p0y);
+        if (((e0 < 0) | (e1 < 0) | (e2 < 0)) & ((e0 > 0) | (e1 > 0) | (e2 > 0))) return false;
     }
-    if ((e0 < 0 || e1 < 0 || e2 < 0) && (e0 > 0 || e1 > 0 || e2 > 0)) return false;
     float det = e0 + e1 + e2;
     if (det == 0) return false;
     p0z *= R.Sz; p1z *= R.Sz; p2z *= R.Sz;

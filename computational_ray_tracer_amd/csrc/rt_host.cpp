@@ -24,7 +24,6 @@ using namespace rtmi;
 
 namespace {
 
-constexpr int kQStride = 64;  // ints between queue counters: 256 B apart, never in one cache line
 
 // ------------------------------------------------------------------------------ host float math
 // glm operation order, float, -ffp-contract=off (same contract as the device code)
@@ -265,7 +264,7 @@ struct rt_ctx {
     float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr;
     int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
     uint4* rng = nullptr;
-    int* d_qcount = nullptr;   // ping-pong queue lengths at [0] and [kQStride] (separate cache lines)
+    int* d_qcount = nullptr;   // queue q, bin b length at [(3q + b) * kQStride] (separate cache lines)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     size_t film_cap = 0;
@@ -318,8 +317,9 @@ void free_workspace(rt_ctx* c) {
 int ensure_workspace(rt_ctx* c, size_t n, bool path) {
     if (c->cap >= n && (!path || c->betaA)) return RT_OK;
     free_workspace(c);
-    // queue arrays are sized 2n (ping-pong) in path mode
-    HIPCHK(c, dalloc(&c->rayO, 2 * n)); HIPCHK(c, dalloc(&c->rayD, 2 * n)); HIPCHK(c, dalloc(&c->slot, 2 * n));
+    // path mode: queue arrays hold 2 ping-pong queues x 3 dominant-axis bins of n entries each
+    size_t nq = path ? 6 * n : n;
+    HIPCHK(c, dalloc(&c->rayO, nq)); HIPCHK(c, dalloc(&c->rayD, nq)); HIPCHK(c, dalloc(&c->slot, nq));
     HIPCHK(c, dalloc(&c->lamA, n)); HIPCHK(c, dalloc(&c->lamB, n));
     HIPCHK(c, dalloc(&c->pdfA, n)); HIPCHK(c, dalloc(&c->pdfB, n));
     HIPCHK(c, dalloc(&c->hitB, n)); HIPCHK(c, dalloc(&c->hitPrim, n));
@@ -466,7 +466,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
         HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
         ev_mark(c, st, ST_GEN, e0);
         if (!path) {
-            TraceIO tio{c->rayO, c->rayD, nullptr, nS, c->cull ? 1 : 0, c->hitB, c->hitPrim};
+            TraceIO tio{c->rayO, c->rayD, nullptr, nS, 0, c->cull ? 1 : 0, c->hitB, c->hitPrim};
             e0 = ev_start(c, st);
             HIPCHK(c, launch_trace_closest(st, 0, c->dsc.qcap, c->dsc, tio, c->d_ctr));
             ev_mark(c, st, ST_TRACE, e0);
@@ -478,26 +478,29 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
             HIPCHK(c, launch_ref_shade_film(st, 0, c->dsc, c->d_spec, fd, sio, c->d_ctr));
             ev_mark(c, st, ST_FILM, e0);
         } else {
+            // camera rays fill bin 0 of queue 0 (flat order); bins 1, 2 start empty
             int cur = 0;
+            HIPCHK(c, hipMemsetAsync(c->d_qcount, 0, 6 * kQStride * sizeof(int), st));
             HIPCHK(c, hipMemcpyAsync(c->d_qcount, &nS, sizeof(int), hipMemcpyHostToDevice, st));
             for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
                 if (depth == c->integ.max_depth && depth > 0) break;  // that step could only add counters
                 int nxt = cur ^ 1;
-                float4* cO = c->rayO + (size_t)cur * nmax;
-                float4* cD = c->rayD + (size_t)cur * nmax;
-                int* cS = c->slot + (size_t)cur * nmax;
-                int* qc_cur = c->d_qcount + kQStride * cur;
-                int* qc_nxt = c->d_qcount + kQStride * nxt;
-                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, sizeof(int), st));
-                TraceIO tio{cO, cD, qc_cur, 0, 0, c->hitB, c->hitPrim};
+                const size_t qs = 3 * nmax;  // one queue = 3 bins of nmax
+                float4* cO = c->rayO + (size_t)cur * qs;
+                float4* cD = c->rayD + (size_t)cur * qs;
+                int* cS = c->slot + (size_t)cur * qs;
+                int* qc_cur = c->d_qcount + 3 * kQStride * cur;
+                int* qc_nxt = c->d_qcount + 3 * kQStride * nxt;
+                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, 3 * kQStride * sizeof(int), st));
+                TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, c->hitB, c->hitPrim};
                 e0 = ev_start(c, st);
                 HIPCHK(c, launch_trace_closest(st, c->grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
                 ev_mark(c, st, ST_TRACE, e0);
                 PathIO pio{};
                 pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = qc_cur;
                 pio.hitB = c->hitB; pio.hitPrim = c->hitPrim;
-                pio.nO = c->rayO + (size_t)nxt * nmax; pio.nD = c->rayD + (size_t)nxt * nmax;
-                pio.nSlot = c->slot + (size_t)nxt * nmax; pio.nCount = qc_nxt;
+                pio.nO = c->rayO + (size_t)nxt * qs; pio.nD = c->rayD + (size_t)nxt * qs;
+                pio.nSlot = c->slot + (size_t)nxt * qs; pio.nCount = qc_nxt; pio.bstride = nmax;
                 pio.rng = c->rng; pio.dim = c->dim; pio.betaA = c->betaA; pio.betaB = c->betaB;
                 pio.LA = c->LA; pio.LB = c->LB;
                 pio.lamA = c->lamA; pio.lamB = c->lamB; pio.pdfA = c->pdfA; pio.pdfB = c->pdfB;
@@ -541,7 +544,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     }
     c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
     c->hs.init();
-    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 2 * kQStride) != hipSuccess ||
+    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 6 * kQStride) != hipSuccess ||
         dalloc(&c->d_ctr, (size_t)C_NCOUNTERS) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
         rt_destroy(c);
         return RT_E_OOM;
@@ -989,7 +992,7 @@ int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_c
     int rc = RT_OK;
     if (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dH, n) || dalloc(&dP, n)) rc = fail(c, RT_E_OOM, "debug trace buffers");
     if (!rc) {
-        TraceIO io{dO, dD, nullptr, n, (use_cull && c->cull) ? 1 : 0, dH, dP};
+        TraceIO io{dO, dD, nullptr, n, 0, (use_cull && c->cull) ? 1 : 0, dH, dP};
         if (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
             launch_trace_closest(c->stream, 0, c->dsc.qcap, c->dsc, io, c->d_ctr) != hipSuccess ||
@@ -1030,7 +1033,7 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
         GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB, nullptr, nullptr,
                   nullptr, nullptr, nullptr, nullptr};
         DevFilm fd = dev_film(c->film);
-        TraceIO tio{c->rayO, c->rayD, nullptr, n, c->cull ? 1 : 0, c->hitB, c->hitPrim};
+        TraceIO tio{c->rayO, c->rayD, nullptr, n, 0, c->cull ? 1 : 0, c->hitB, c->hitPrim};
         ShadeRefIO sio = shade_ref_io(c);
         sio.rayD = c->rayD; sio.lamA = c->lamA; sio.lamB = c->lamB; sio.pdfA = c->pdfA; sio.pdfB = c->pdfB;
         sio.hitB = c->hitB; sio.hitPrim = c->hitPrim;

@@ -84,11 +84,17 @@ struct GenOut {
     float4* betaA; float4* betaB; float4* LA; float4* LB;
 };
 
+// Ray queues.  A path-mode queue is split into 3 bins by the rays' dominant axis (the watertight test's
+// kz, Shapes.h:1145): bin b holds rays at ray[b*bstride + i], i < count[b*cstride].  Entries are addressed by
+// a flat index k over bin 0, then 1, then 2, so every wave but the two at bin seams sees one kz.
+static const int kQStride = 64;  // ints between queue counters: 256 B apart, never in one cache line
+
 struct TraceIO {
     const float4* rayO; const float4* rayD;
-    const int* count; int n;  // queue length in device memory (count != nullptr) or fixed n
+    const int* count; int n;  // binned queue lengths in device memory (count != nullptr) or one fixed n
+    size_t bstride;           // elements between bins
     int set;                  // tile set: 0 = all triangles, 1 = back-face culled
-    float4* hitB;             // (b0, b1, b2, t)
+    float4* hitB;             // (b0, b1, b2, t) at flat index
     int* hitPrim;
 };
 
@@ -101,9 +107,10 @@ struct ShadeRefIO {
 };
 
 struct PathIO {
-    const float4* rayO; const float4* rayD; const int* slot; const int* count;
-    const float4* hitB; const int* hitPrim;
-    float4* nO; float4* nD; int* nSlot; int* nCount;
+    const float4* rayO; const float4* rayD; const int* slot; const int* count;  // current binned queue
+    const float4* hitB; const int* hitPrim;                                     // at flat index
+    float4* nO; float4* nD; int* nSlot; int* nCount;                            // next binned queue
+    size_t bstride;
     uint4* rng; int* dim; float4* betaA; float4* betaB; float4* LA; float4* LB;
     const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
     int depth, max_depth;
