@@ -362,8 +362,8 @@ void harvest(rt_ctx* c) {
         switch (e.stage) {
             case ST_GEN: c->stats.ms_generate += ms; break;
             case ST_TRACE: c->stats.ms_trace += ms; c->stats.launches_trace += 1; break;
-            case ST_SHADE: c->stats.ms_shade += ms; break;
-            case ST_SHADOW: c->stats.ms_shadow += ms; c->stats.launches_shadow += 1; break;
+            case ST_SHADE: c->stats.ms_shade += ms; c->stats.launches_shade += 1; break;
+            case ST_SHADOW: c->stats.ms_shadow += ms; break;
             default: c->stats.ms_film += ms; break;
         }
         c->pool.push_back(e.a);

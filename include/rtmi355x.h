@@ -130,9 +130,10 @@ typedef struct {
     int64_t shadow_nodes_tested;     /* node box tests by any-hit (shadow) rays          */
     int64_t shadow_tris_tested;      /* triangle tests by any-hit (shadow) rays          */
     int64_t hits;                    /* closest-hit rays that hit                        */
-    double ms_generate, ms_trace, ms_shade, ms_shadow, ms_film;  /* HIP-event kernel time */
+    double ms_generate, ms_trace, ms_shade, ms_shadow, ms_film;  /* HIP-event kernel time; ms_shadow
+                                        stays 0: shadow rays are traced inside the path shade kernel */
     int64_t launches_trace;          /* closest-hit trace launches (per-launch averages) */
-    int64_t launches_shadow;         /* any-hit trace launches                           */
+    int64_t launches_shade;          /* shade launches (path mode: includes the inline shadow rays) */
 } rt_stats;
 
 /* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */
