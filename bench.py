@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--spp-per-step", type=int, default=8)
     p.add_argument("--res", type=str, default="1920x1080")
+    p.add_argument("--config", choices=["cornell", "cfg3"], default="cornell",
+                   help="cornell = BASELINE configs[1] (the metric's workload); cfg3 = configs[2] (98k-tri mesh)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return p.parse_args()
@@ -116,7 +118,15 @@ def main():
     else:
         torch.cuda.set_device(0)
     W, H = (int(x) for x in a.res.split("x"))
-    cfg = scene.cfg_cornell(res=(W, H), spp_side=16, max_depth=5)
+    if a.config == "cornell":
+        cfg = scene.cfg_cornell(res=(W, H), spp_side=16, max_depth=5)
+        workload = (f"BASELINE configs[1]: Cornell box {W}x{H} @ 256 spp (16x16 stratified jittered), "
+                    f"diffuse + NEE, max depth 5, 1 quad light, 36 triangles")
+    else:
+        cfg = scene.cfg3_blob(res=(W, H), spp_side=16, max_depth=5)
+        cfg.sampler = scene.StratifiedSampler(32, 16, True, 0)  # 512 spp
+        workload = (f"BASELINE configs[2]: 98k-triangle procedural mesh in the Cornell box {W}x{H} @ 512 spp "
+                    f"(32x16 stratified jittered), diffuse + NEE, max depth 5, 1 quad light")
     spp = cfg.sampler.spp()
     r = Renderer(cfg, device=torch.cuda.current_device())
     r.set_shard(32, world, rank)
@@ -163,7 +173,9 @@ def main():
     # roofline of the dominant kernel (most HIP-event time in the timed region)
     traffic = None
     if TRAFFIC_FILE.exists():
-        traffic = json.loads(TRAFFIC_FILE.read_text()).get("kernels")
+        tj = json.loads(TRAFFIC_FILE.read_text())
+        if tj.get("config", "cornell") == a.config:  # PMC bytes are only valid for the workload they measured
+            traffic = tj.get("kernels")
     rl = kernel_rooflines(st, traffic)
     dom = max(rl, key=lambda k: rl[k]["total_ms"])
     roofline = dict(rl[dom])
@@ -174,8 +186,7 @@ def main():
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (procedural Cornell box scene, no datasets)",
-        "config": {"workload": f"BASELINE configs[1]: Cornell box {W}x{H} @ {spp} spp (16x16 stratified jittered), "
-                               f"diffuse + NEE, max depth 5, 1 quad light, 36 triangles",
+        "config": {"workload": workload,
                    "res": [W, H], "spp_total": spp, "spp_per_step_per_gpu": a.spp_per_step, "max_depth": 5,
                    "parallelism": f"pixel-tile shards x{world} (32x32 tiles) + RCCL film reduce"},
         "roofline": roofline,

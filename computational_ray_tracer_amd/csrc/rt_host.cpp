@@ -24,6 +24,7 @@ using namespace rtmi;
 
 namespace {
 
+constexpr int kRingMax = 1 << 16;  // largest BFS group FIFO (HBM ring per resident thread, 4 B per entry)
 
 // ------------------------------------------------------------------------------ host float math
 // glm operation order, float, -ffp-contract=off (same contract as the device code)
@@ -758,15 +759,35 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
     internal_at.assign(maxd + 2, 0);
     for (int i = 0; i < nn; ++i)
         if (ob.nodes[i].first_child >= 0) internal_at[depth[i]]++;
+    // Exact worst case of the kernel's group FIFO: replay the BFS with every box test passing (any real ray
+    // pushes a subset of these groups, in the same order, so its queue is never longer at the same point).
     int bound = 0;
-    for (int d = 0; d <= maxd; ++d) bound = std::max(bound, (d > 0 ? internal_at[d - 1] : 0) + internal_at[d]);
+    {
+        std::vector<int> fifo;
+        fifo.reserve(nn);
+        size_t head = 0;
+        int cur = 0, left = 1;
+        while (true) {
+            int fc = ob.nodes[cur].first_child;
+            if (fc >= 0) {
+                fifo.push_back(fc);
+                bound = std::max(bound, (int)(fifo.size() - head));
+            }
+            if (--left > 0) { ++cur; continue; }
+            if (head == fifo.size()) break;
+            cur = fifo[head++];
+            left = 8;
+        }
+    }
     int qcap = 1;
     if (ob.nodes[0].first_child >= 0) {
         const int caps[] = {16, 64, 256, 1024};
         qcap = 0;
         for (int cp : caps)
             if (cp >= bound) { qcap = cp; break; }
-        if (!qcap) return fail(c, RT_E_LIMIT, "octree BFS frontier bound " + std::to_string(bound) + " exceeds 1024 groups");
+        if (!qcap && bound > kRingMax)
+            return fail(c, RT_E_LIMIT, "octree BFS frontier bound " + std::to_string(bound) + " exceeds " +
+                                           std::to_string(kRingMax) + " groups");
     }
     c->info.n_nodes = nn;
     c->info.n_leaf_refs = (int)c->h_refs.size();
@@ -815,6 +836,17 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
     d.triMaterial = (const int*)ptm; d.materials = (const float4*)pm;
     d.n_nodes = nn;
     d.qcap = qcap;
+    if (qcap == 0) {
+        int rs = 1;
+        while (rs < bound) rs <<= 1;
+        d.ring_threads = c->grid * kBlockThreads;
+        d.ring_mask = rs - 1;
+        void* pr = nullptr;
+        if (hipMalloc(&pr, (size_t)d.ring_threads * rs * sizeof(int)) != hipSuccess)
+            return fail(c, RT_E_OOM, "BFS ring of " + std::to_string(rs) + " groups per thread");
+        c->scene_allocs.push_back(pr);
+        d.ring = (int*)pr;
+    }
     d.n_lights = s->n_lights;
     if (s->n_lights == 1) {
         const rt_quad_light& q = s->lights[0];

@@ -56,7 +56,10 @@ struct DevScene {
     int n_nodes;
     int n_lights;
     DevLight light0;
-    int qcap;
+    int qcap;                       // BFS group FIFO size (compiled variants); 0 = global-memory ring below
+    int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
+    int ring_mask;
+    int ring_threads;               // launches with qcap == 0 are clamped to this many threads
 };
 
 // device counter slots (u64)
@@ -87,7 +90,8 @@ struct GenOut {
 // Ray queues.  A path-mode queue is split into 3 bins by the rays' dominant axis (the watertight test's
 // kz, Shapes.h:1145): bin b holds rays at ray[b*bstride + i], i < count[b*cstride].  Entries are addressed by
 // a flat index k over bin 0, then 1, then 2, so every wave but the two at bin seams sees one kz.
-static const int kQStride = 64;  // ints between queue counters: 256 B apart, never in one cache line
+static const int kQStride = 64;
+static const int kBlockThreads = 256;  // threads per block of every kernel  // ints between queue counters: 256 B apart, never in one cache line
 
 struct TraceIO {
     const float4* rayO; const float4* rayD;

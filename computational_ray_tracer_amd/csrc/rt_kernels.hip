@@ -17,7 +17,7 @@
 
 namespace rtmi {
 
-static constexpr int kBlock = 256;
+static constexpr int kBlock = kBlockThreads;
 
 #ifndef RT_TRI_UNROLL
 #define RT_TRI_UNROLL 4      // triangles per scalar-cache batch in single-leaf traversal
@@ -249,7 +249,12 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         }
         return best;
     }
-    int q[QCAP];
+    // group FIFO: a private array (registers / scratch) or, for QCAP == 0, a per-thread ring in HBM whose
+    // size is the host's exact worst-case bound (scenes beyond 1024 groups, e.g. the 98k-triangle CFG3)
+    constexpr bool GQ = QCAP == 0;
+    int q[GQ ? 1 : QCAP];
+    int* gq = GQ ? sc.ring + (blockIdx.x * blockDim.x + threadIdx.x) : nullptr;
+    const int qmask = GQ ? sc.ring_mask : QCAP - 1;
     int head = 0, tail = 0;
     int n = 0;       // current node
     int left = 1;    // nodes left in the current group (root: a group of one)
@@ -260,7 +265,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         if (box_hit(a, b, o, inv, tMax)) {
             int child = __float_as_int(a.w);
             if (child >= 0) {
-                q[tail & (QCAP - 1)] = child;
+                if constexpr (GQ) gq[(size_t)(tail & qmask) * sc.ring_threads] = child;
+                else q[tail & qmask] = child;
                 ++tail;
             } else {
                 int2 r = lr[n];
@@ -279,7 +285,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         }
         if (--left > 0) { ++n; continue; }
         if (head == tail) break;
-        n = q[head & (QCAP - 1)];
+        if constexpr (GQ) n = gq[(size_t)(head & qmask) * sc.ring_threads];
+        else n = q[head & qmask];
         ++head;
         left = 8;
     }
@@ -598,8 +605,11 @@ hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& id
 
 hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
                                 unsigned long long* ctr) {
-    dim3 g(grid_for(io.count ? grid * kBlock : io.n, grid)), b(kBlock);
+    int gb = grid_for(io.count ? grid * kBlock : io.n, grid);
+    if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
+    dim3 g(gb), b(kBlock);
     switch (qcap) {
+        case 0: hipLaunchKernelGGL(k_trace_closest<0>, g, b, 0, st, sc, io, ctr); break;
         case 1: hipLaunchKernelGGL(k_trace_closest<1>, g, b, 0, st, sc, io, ctr); break;
         case 16: hipLaunchKernelGGL(k_trace_closest<16>, g, b, 0, st, sc, io, ctr); break;
         case 64: hipLaunchKernelGGL(k_trace_closest<64>, g, b, 0, st, sc, io, ctr); break;
@@ -625,8 +635,11 @@ hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* 
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
                              unsigned long long* ctr) {
-    dim3 g(grid > 0 ? grid : 1), b(kBlock);
+    int gb = grid > 0 ? grid : 1;
+    if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
+    dim3 g(gb), b(kBlock);
     switch (qcap) {
+        case 0: hipLaunchKernelGGL(k_path_shade<0>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
         case 1: hipLaunchKernelGGL(k_path_shade<1>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
         case 16: hipLaunchKernelGGL(k_path_shade<16>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
         case 64: hipLaunchKernelGGL(k_path_shade<64>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;

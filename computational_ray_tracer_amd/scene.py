@@ -327,7 +327,7 @@ def _box(top, h):
     return q
 
 
-def cornell_box():
+def cornell_box(blocks=True, extra=None):
     """Cornell box as triangles (standard 0..556 mm geometry): 5 walls (10 tris) + light quad (2) +
     short and tall block (12 + 12) = 36 triangles, one quad area light slightly below the ceiling.
     World space directly (rigid transform = permutation_y_z so that ObjectToRender = identity)."""
@@ -346,8 +346,14 @@ def cornell_box():
     add(_quad(P(552.8, 0, 0), P(549.6, 0, 559.2), P(556, 548.8, 559.2), P(556, 548.8, 0)), R)     # left (red)
     ly = 548.7
     add(_quad(P(343, ly, 227), P(343, ly, 332), P(213, ly, 332), P(213, ly, 227)), L)             # light
-    add(_box([(130, 165, 65), (82, 165, 225), (240, 165, 272), (290, 165, 114)], 165), W)
-    add(_box([(423, 330, 247), (265, 330, 296), (314, 330, 456), (472, 330, 406)], 330), W)
+    if blocks:
+        add(_box([(130, 165, 65), (82, 165, 225), (240, 165, 272), (290, 165, 114)], 165), W)
+        add(_box([(423, 330, 247), (265, 330, 296), (314, 330, 456), (472, 330, 406)], 330), W)
+    n_fixed = len(faces)
+    if extra is not None:  # (nt, 3, 3) world-space triangles, already outward-wound, white material
+        for tri in extra:
+            faces.append(tri)
+            mats.append(W)
     faces = np.array(faces)
     # make every wall face the interior / light face downward: orient normals toward the box centre
     centre = np.array([278.0, 274.4, 279.6])
@@ -358,7 +364,7 @@ def cornell_box():
     lflip = (np.array(mats) == L) & (nn[:, 1] > 0)
     faces[flip | lflip] = faces[flip | lflip][:, [0, 2, 1]]
     # blocks: outward
-    blk = np.arange(len(faces)) >= 12
+    blk = (np.arange(len(faces)) >= 12) & (np.arange(len(faces)) < n_fixed)
     bc = np.where(np.arange(len(faces))[:, None] < 24, faces[12:24].reshape(-1, 3).mean(0), faces[24:].reshape(-1, 3).mean(0))
     nn = np.cross(faces[:, 1] - faces[:, 0], faces[:, 2] - faces[:, 0])
     bflip = blk & (np.einsum("ij,ij->i", nn, cen - bc) < 0)
@@ -420,5 +426,22 @@ def cfg_cornell(res=(256, 256), spp_side=4, n_index=None, max_depth=5):
     cam = cornell_camera(res)
     n_index = spp_side * spp_side if n_index is None else n_index
     return Config(f"cornell_{res[0]}x{res[1]}_{spp_side * spp_side}spp", cornell_box(), cam,
+                  StratifiedSampler(spp_side, spp_side, True, 0), Film(res=res, filter=capi.RT_FILTER_BOX),
+                  Integrator(capi.RT_INTEGRATOR_PATH, max_depth=max_depth), 0, n_index)
+
+
+def cfg3_blob(res=(1920, 1080), spp_side=16, n_index=None, max_depth=5, frequency=70):
+    """BASELINE configs[2]: a seeded ~100k-triangle procedural 'bunny-like' mesh
+    (20*70^2 = 98,000 triangles) standing on the floor of the Cornell box, lit by its quad area light;
+    walls, light and mesh form ONE triangle model and one octree (TRIANGLE_CAPACITY 40)."""
+    pos, _, idx = procedural_blob(frequency=frequency, radius=1.0, seed=1)
+    tri = pos[idx].astype(np.float64)                      # unit-ish blob, object space
+    lo = tri.reshape(-1, 3).min(0)
+    s = 150.0
+    world = tri * s + np.array([278.0, -lo[1] * s + 0.5, 280.0])
+    model = cornell_box(blocks=False, extra=world)
+    cam = cornell_camera(res)
+    n_index = spp_side * spp_side if n_index is None else n_index
+    return Config(f"cfg3_blob{len(idx)}_{res[0]}x{res[1]}_{spp_side * spp_side}spp", model, cam,
                   StratifiedSampler(spp_side, spp_side, True, 0), Film(res=res, filter=capi.RT_FILTER_BOX),
                   Integrator(capi.RT_INTEGRATOR_PATH, max_depth=max_depth), 0, n_index)

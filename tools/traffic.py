@@ -41,6 +41,7 @@ def main():
     p.add_argument("--write", required=True)
     p.add_argument("--stats")
     p.add_argument("--out", default="profiles/traffic.json")
+    p.add_argument("--config", default="cornell", help="bench.py --config the PMC passes ran")
     a = p.parse_args()
     fetch = per_dispatch(a.fetch, "FETCH_SIZE")
     write = per_dispatch(a.write, "WRITE_SIZE")
@@ -48,7 +49,7 @@ def main():
     if a.stats:
         for r in csv.DictReader(open(a.stats)):
             avg_ns[kname(r["Name"])] = float(r["AverageNs"])
-    out = {"tag": a.tag, "units": "bytes per launch (mean over the run's dispatches)",
+    out = {"tag": a.tag, "config": a.config, "units": "bytes per launch (mean over the run's dispatches)",
            "correction": "FETCH_SIZE x2 (gfx950 half-count of 16 B/lane reads), KiB -> bytes x1024",
            "kernels": {}}
     for k in KERNELS:
