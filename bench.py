@@ -39,8 +39,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--spp-per-step", type=int, default=8)
     p.add_argument("--res", type=str, default="1920x1080")
-    p.add_argument("--config", choices=["cornell", "cfg3"], default="cornell",
-                   help="cornell = BASELINE configs[1] (the metric's workload); cfg3 = configs[2] (98k-tri mesh)")
+    p.add_argument("--config", choices=["cornell", "cfg3", "cfg4", "cfg5"], default="cornell",
+                   help="cornell = BASELINE configs[1] (the metric's workload); cfg3..cfg5 = configs[2..4]")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     return p.parse_args()
@@ -122,6 +122,14 @@ def main():
         cfg = scene.cfg_cornell(res=(W, H), spp_side=16, max_depth=5)
         workload = (f"BASELINE configs[1]: Cornell box {W}x{H} @ 256 spp (16x16 stratified jittered), "
                     f"diffuse + NEE, max depth 5, 1 quad light, 36 triangles")
+    elif a.config == "cfg4":
+        cfg = scene.cfg4_mixed(res=(W, H))
+        workload = (f"BASELINE configs[3]: mixed scene {W}x{H} @ 1024 spp: 98k-tri mesh + diffuse/mirror/BK7-glass "
+                    f"spheres, quad + disk + point + sun lights, NEE + MIS, max depth 5")
+    elif a.config == "cfg5":
+        W, H = (3840, 2160) if a.res == "1920x1080" else (W, H)
+        cfg = scene.cfg5_spectral(res=(W, H))
+        workload = (f"BASELINE configs[4]: spectral (8 hero wavelengths) mixed scene {W}x{H} @ 2048 spp, NEE + MIS")
     else:
         cfg = scene.cfg3_blob(res=(W, H), spp_side=16, max_depth=5)
         cfg.sampler = scene.StratifiedSampler(32, 16, True, 0)  # 512 spp

@@ -14,11 +14,14 @@ LIB_PATH = PKG_DIR / "lib" / "librtmi355x.so"
 RT_OK, RT_E_ARG, RT_E_HIP, RT_E_RCCL, RT_E_OOM, RT_E_STATE, RT_E_NODEVICE, RT_E_LIMIT = 0, -1, -2, -3, -4, -5, -6, -7
 STATUS_NAMES = {0: "RT_OK", -1: "RT_E_ARG", -2: "RT_E_HIP", -3: "RT_E_RCCL", -4: "RT_E_OOM", -5: "RT_E_STATE",
                 -6: "RT_E_NODEVICE", -7: "RT_E_LIMIT"}
-RT_MAT_DIFFUSE = 0
+RT_MAT_DIFFUSE, RT_MAT_MIRROR, RT_MAT_DIELECTRIC = 0, 1, 2
+RT_SHAPE_SPHERE, RT_SHAPE_DISK, RT_SHAPE_TRIANGLE = 0, 1, 2
+RT_LIGHT_QUAD, RT_LIGHT_DISK, RT_LIGHT_POINT, RT_LIGHT_DISTANT = 0, 1, 2, 3
 RT_CAMERA_PERSPECTIVE = 0
 RT_SAMPLER_INDEPENDENT, RT_SAMPLER_STRATIFIED = 0, 1
 RT_FILTER_BOX, RT_FILTER_TRIANGLE = 0, 1
-RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH = 0, 1
+RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
+ABI_VERSION = 2
 
 F16 = C.c_float * 16
 F9 = C.c_float * 9
@@ -36,11 +39,19 @@ class rt_pixel(C.Structure):
 
 
 class rt_material(C.Structure):
-    _fields_ = [("type", C.c_int), ("sigmoid", F3), ("emission_scale", C.c_float)]
+    _fields_ = [("type", C.c_int), ("sigmoid", F3), ("emission_scale", C.c_float), ("eta", C.c_float)]
 
 
-class rt_quad_light(C.Structure):
-    _fields_ = [("p", F3), ("e1", F3), ("e2", F3), ("n", F3), ("material", C.c_int)]
+class rt_shape(C.Structure):
+    _fields_ = [("type", C.c_int), ("object_to_render", F16), ("render_to_object", F16), ("normal_to_render", F9),
+                ("radius", C.c_float), ("zmin", C.c_float), ("zmax", C.c_float), ("phimax", C.c_float),
+                ("height", C.c_float), ("inner_radius", C.c_float), ("outer_radius", C.c_float),
+                ("p", F9), ("material", C.c_int)]
+
+
+class rt_light(C.Structure):
+    _fields_ = [("type", C.c_int), ("p", F3), ("e1", F3), ("e2", F3), ("n", F3), ("dir", F3), ("scale", C.c_float),
+                ("shape", C.c_int), ("material", C.c_int)]
 
 
 class rt_scene_desc(C.Structure):
@@ -51,7 +62,8 @@ class rt_scene_desc(C.Structure):
         ("cull_backfaces", C.c_int), ("cull_look", F3), ("octree_capacity", C.c_int),
         ("tri_material", C.POINTER(C.c_int32)),
         ("n_materials", C.c_int), ("materials", C.POINTER(rt_material)),
-        ("n_lights", C.c_int), ("lights", C.POINTER(rt_quad_light)),
+        ("n_lights", C.c_int), ("lights", C.POINTER(rt_light)),
+        ("n_shapes", C.c_int), ("shapes", C.POINTER(rt_shape)),
     ]
 
 
@@ -146,7 +158,7 @@ def load_library(path=None):
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
-    if lib.rt_abi_version() != 1:
+    if lib.rt_abi_version() != ABI_VERSION:
         raise RuntimeError("librtmi355x ABI version mismatch")
     if path is None:
         _lib = lib

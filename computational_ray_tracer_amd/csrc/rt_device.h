@@ -359,4 +359,125 @@ RT_DEV bool box_hit(float4 a, float4 b, V3 o, V3 inv, float tMax) {
     return !(mn > mx);
 }
 
+
+// ---------------------------------------------------------------------- analytic shapes (a21)
+// Restated from Shapes.h like oracle/rtcore.hpp (same op order): the ray goes to object space through
+// RenderToObject, hits come back through LocalSurfaceInfo::Transform (Shapes.h:147-160).  Full spheres and
+// disks only (φmax = 360°, checked at upload), so the atan2 φ clips are never evaluated.
+RT_DEV V3 m4_point(const float* M, V3 p) { float o[4]; mat4_mul(M, p.x, p.y, p.z, 1.f, o); return v3(o[0], o[1], o[2]); }
+RT_DEV V3 m4_dir(const float* M, V3 d) { float o[4]; mat4_mul(M, d.x, d.y, d.z, 0.f, o); return v3(o[0], o[1], o[2]); }
+RT_DEV V3 m3_mul(const float* M, V3 v) {  // glm mat3*vec3: (m0 x + m1 y) + m2 z
+    return v3((M[0] * v.x + M[3] * v.y) + M[6] * v.z, (M[1] * v.x + M[4] * v.y) + M[7] * v.z,
+              (M[2] * v.x + M[5] * v.y) + M[8] * v.z);
+}
+// Shapes.h:294-376 Sphere::BasicIntersect
+RT_DEV bool sphere_isect(const DevShape& s, V3 o, V3 d, float tMax, V3& ph, float& th) {
+    const float r = s.r;
+    float a = d.x * d.x + d.y * d.y + d.z * d.z;
+    float b = 2 * (d.x * o.x + d.y * o.y + d.z * o.z);
+    float c = o.x * o.x + o.y * o.y + o.z * o.z - r * r;
+    V3 v = vsub(o, vmul(d, b / (2 * a)));
+    float length = sqrtf(vdot(v, v));
+    float discrim = 4 * a * (r + length) * (r - length);
+    if (discrim < 0) return false;
+    float rootDiscrim = sqrtf(discrim);
+    float q = (b < 0) ? -.5f * (b - rootDiscrim) : -.5f * (b + rootDiscrim);
+    float t0 = q / a, t1 = c / q;
+    if (t0 > t1) { float x = t0; t0 = t1; t1 = x; }
+    if (t0 > tMax || t1 <= 0) return false;
+    float tsh = t0;
+    if (tsh <= 0) {
+        tsh = t1;
+        if (tsh > tMax) return false;
+    }
+    const float fixx = (float)(1e-5 * (double)r);
+    V3 hp = vadd(o, vmul(d, tsh));
+    hp = vmul(hp, r / sqrtf(vdot(hp, hp)));
+    if (hp.x == 0 && hp.y == 0) hp.x = fixx;
+    if (hp.z < s.zmin || hp.z > s.zmax) {
+        if (tsh == t1) return false;
+        if (t1 > tMax) return false;
+        tsh = t1;
+        hp = vadd(o, vmul(d, tsh));
+        hp = vmul(hp, r / sqrtf(vdot(hp, hp)));
+        if (hp.x == 0 && hp.y == 0) hp.x = fixx;
+        if (hp.z < s.zmin || hp.z > s.zmax) return false;
+    }
+    ph = hp; th = tsh;
+    return true;
+}
+// Shapes.h:684-716 Disk::BasicIntersect
+RT_DEV bool disk_isect(const DevShape& s, V3 o, V3 d, float tMax, V3& ph, float& th) {
+    float t0 = (s.h - o.z) / d.z;
+    if (t0 <= 0 || t0 >= tMax) return false;
+    if (d.z == 0) return false;
+    V3 p = vadd(o, vmul(d, t0));
+    float dist2 = p.x * p.x + p.y * p.y;
+    if (dist2 > s.ro * s.ro || dist2 < s.ri * s.ri) return false;
+    ph = p; th = t0;
+    return true;
+}
+// Shapes.h:842-880 TriangleSimple::BasicIntersect
+RT_DEV bool trisimple_isect(const DevShape& s, V3 orig, V3 dir, float tMax, V3& ph, float& th) {
+    float a = s.p1[0] - s.p2[0], b = s.p1[1] - s.p2[1], c = s.p1[2] - s.p2[2];
+    float d = s.p1[0] - s.p3[0], e = s.p1[1] - s.p3[1], f = s.p1[2] - s.p3[2];
+    float g = dir.x, h = dir.y, i = dir.z;
+    float j = s.p1[0] - orig.x, k = s.p1[1] - orig.y, l = s.p1[2] - orig.z;
+    float M = a * (e * i - h * f) + b * (g * f - d * i) + c * (d * h - e * g);
+    float t = -(f * (a * k - j * b) + e * (j * c - a * l) + d * (b * l - k * c)) / M;
+    if (t < 0 || t >= tMax) return false;
+    float Y = (i * (a * k - j * b) + h * (j * c - a * l) + g * (b * l - k * c)) / M;
+    if (Y < 0 || Y > 1) return false;
+    float B = (j * (e * i - h * f) + k * (g * f - d * i) + l * (d * h - e * g)) / M;
+    if (B < 0 || B > 1 - Y) return false;
+    ph = vadd(orig, vmul(dir, t)); th = t;
+    return true;
+}
+RT_DEV bool shape_isect(const DevShape& s, V3 o, V3 d, float tMax, V3& ph, float& th) {
+    V3 oo = m4_point(s.r2o, o), dd = m4_dir(s.r2o, d);
+    if (s.type == 0) return sphere_isect(s, oo, dd, tMax, ph, th);
+    if (s.type == 1) return disk_isect(s, oo, dd, tMax, ph, th);
+    return trisimple_isect(s, oo, dd, tMax, ph, th);
+}
+// object-space normal: sphere gradient (Shapes.h:417-422), disk +z (744-752), TriangleSimple (897-901)
+RT_DEV V3 shape_normal_obj(const DevShape& s, V3 p) {
+    if (s.type == 0) return vnorm(v3(2 * p.x, 2 * p.y, 2 * p.z));
+    if (s.type == 1) return v3(0, 0, 1);
+    return vnorm(vcross(vsub(v3(s.p3[0], s.p3[1], s.p3[2]), v3(s.p1[0], s.p1[1], s.p1[2])),
+                        vsub(v3(s.p2[0], s.p2[1], s.p2[2]), v3(s.p1[0], s.p1[1], s.p1[2]))));
+}
+
+// ------------------------------------------------------------------ scattering (pbrt-v4)
+RT_DEV float power_heuristic(float f, float g) {
+    float f2 = f * f, g2 = g * g;
+    if (__builtin_isinf(f2)) return 1;
+    return f2 / (f2 + g2);
+}
+RT_DEV float fr_dielectric(float cosi, float eta) {
+    cosi = gclamp(cosi, -1.0f, 1.0f);
+    if (cosi < 0) { eta = 1 / eta; cosi = -cosi; }
+    float sin2i = 1 - cosi * cosi;
+    float sin2t = sin2i / (eta * eta);
+    if (sin2t >= 1) return 1.f;
+    float x = 1 - sin2t;
+    float cost = sqrtf(x > 0.f ? x : 0.f);
+    float r_parl = (eta * cosi - cost) / (eta * cosi + cost);
+    float r_perp = (cosi - eta * cost) / (cosi + eta * cost);
+    return (r_parl * r_parl + r_perp * r_perp) / 2;
+}
+RT_DEV bool refract_dir(V3 wi, V3 n, float eta, float& etap, V3& wt) {
+    float cosi = vdot(n, wi);
+    if (cosi < 0) { eta = 1 / eta; cosi = -cosi; n = v3(-n.x, -n.y, -n.z); }
+    float x = 1 - cosi * cosi;
+    float sin2i = x > 0.f ? x : 0.f;   // std::max(0, .)
+    float sin2t = sin2i / (eta * eta);
+    if (sin2t >= 1) return false;
+    float y = 1 - sin2t;
+    float cost = sqrtf(y > 0.f ? y : 0.f);
+    wt = vadd(v3(-wi.x / eta, -wi.y / eta, -wi.z / eta), vmul(n, cosi / eta - cost));
+    etap = eta;
+    return true;
+}
+RT_DEV V3 reflect_dir(V3 I, V3 N) { return vsub(I, vmul(vmul(N, vdot(N, I)), 2.0f)); }  // glm::reflect
+
 }  // namespace rtmi

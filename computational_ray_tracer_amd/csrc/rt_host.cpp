@@ -25,6 +25,7 @@ using namespace rtmi;
 namespace {
 
 constexpr int kRingMax = 1 << 16;  // largest BFS group FIFO (HBM ring per resident thread, 4 B per entry)
+constexpr int kMaxLights = 64;
 
 // ------------------------------------------------------------------------------ host float math
 // glm operation order, float, -ffp-contract=off (same contract as the device code)
@@ -87,7 +88,7 @@ float inner_product(const A& f, const B& g) {  // spectrum.h:762-768
 }
 struct HostSpectra {
     DenseS X, Y, Z, D65d;
-    PLS D65, F1;
+    PLS D65, F1, BK7;
     PLS interleaved(const float* s, int n, bool normalize) const {  // spectrum.cpp:134-165 FromInterleaved
         PLS p;
         if (s[0] > 360) { p.l.push_back(359); p.v.push_back(s[1]); }
@@ -109,6 +110,7 @@ struct HostSpectra {
         X = cie(rtdata::cie_x); Y = cie(rtdata::cie_y); Z = cie(rtdata::cie_z);
         D65 = interleaved(rtdata::illum_d65, rtdata::illum_d65_n, true);
         F1 = interleaved(rtdata::illum_f1, rtdata::illum_f1_n, true);
+        BK7 = interleaved(rtdata::glass_bk7_eta, rtdata::glass_bk7_eta_n, false);  // spectrum.cpp:2674-2675
         D65d = to_dense(D65);
     }
 };
@@ -246,6 +248,7 @@ struct rt_ctx {
     std::vector<int32_t> h_child, h_leaf_first, h_leaf_count, h_refs;
     rt_octree_info info{};
     bool cull = false;
+    bool scene_full = false;   // the scene needs the general path-shade kernel
     DevScene dsc{};
     std::vector<void*> scene_allocs;
     // spectra + resolve matrices
@@ -264,6 +267,7 @@ struct rt_ctx {
     float4* hitB = nullptr;
     float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr;
     int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
+    float* prevPdf = nullptr;
     uint4* rng = nullptr;
     int* d_qcount = nullptr;   // queue q, bin b length at [(3q + b) * kQStride] (separate cache lines)
     unsigned long long* d_ctr = nullptr;
@@ -305,13 +309,14 @@ void free_scene(rt_ctx* c) {
 
 void free_workspace(rt_ctx* c) {
     void* ptrs[] = {c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->betaA, c->betaB,
-                    c->LA, c->LB, c->slot, c->hitPrim, c->dim, c->rng};
+                    c->LA, c->LB, c->slot, c->hitPrim, c->dim, c->rng, c->prevPdf};
     for (void* p : ptrs)
         if (p) hipFree(p);
     c->rayO = c->rayD = c->lamA = c->lamB = c->pdfA = c->pdfB = c->hitB = nullptr;
     c->betaA = c->betaB = c->LA = c->LB = nullptr;
     c->slot = c->hitPrim = c->dim = nullptr;
     c->rng = nullptr;
+    c->prevPdf = nullptr;
     c->cap = 0;
 }
 
@@ -327,7 +332,7 @@ int ensure_workspace(rt_ctx* c, size_t n, bool path) {
     if (path) {
         HIPCHK(c, dalloc(&c->betaA, n)); HIPCHK(c, dalloc(&c->betaB, n));
         HIPCHK(c, dalloc(&c->LA, n)); HIPCHK(c, dalloc(&c->LB, n));
-        HIPCHK(c, dalloc(&c->dim, n)); HIPCHK(c, dalloc(&c->rng, n));
+        HIPCHK(c, dalloc(&c->dim, n)); HIPCHK(c, dalloc(&c->rng, n)); HIPCHK(c, dalloc(&c->prevPdf, n));
     }
     c->cap = n;
     return RT_OK;
@@ -449,7 +454,9 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
         return fail(c, RT_E_ARG, "StratifiedSampler without jitter supports indices < SamplesPerPixel (samplers.h:83-87)");
     if ((rc = build_work(c))) return rc;
     if (ie == ib || c->n_work == 0) return RT_OK;
-    bool path = c->integ.kind == RT_INTEGRATOR_PATH;
+    bool path = c->integ.kind == RT_INTEGRATOR_PATH || c->integ.kind == RT_INTEGRATOR_PATH_MIS;
+    c->dsc.mis = c->integ.kind == RT_INTEGRATOR_PATH_MIS;
+    c->dsc.full = c->scene_full || c->dsc.mis;
     const size_t target = path ? (size_t)8 << 20 : (size_t)16 << 20;  // samples in flight per batch
     int B = (int)std::max<size_t>(1, target / (size_t)c->n_work);
     B = std::min(B, ie - ib);
@@ -462,7 +469,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
         int nS = nIdx * c->n_work;
         SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
         GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB,
-                  path ? c->rng : nullptr, c->dim, c->betaA, c->betaB, c->LA, c->LB};
+                  path ? c->rng : nullptr, c->dim, path && c->dsc.full ? c->prevPdf : nullptr, c->betaA, c->betaB, c->LA, c->LB};
         hipEvent_t e0 = ev_start(c, st);
         HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
         ev_mark(c, st, ST_GEN, e0);
@@ -484,7 +491,8 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
             HIPCHK(c, hipMemsetAsync(c->d_qcount, 0, 6 * kQStride * sizeof(int), st));
             HIPCHK(c, hipMemcpyAsync(c->d_qcount, &nS, sizeof(int), hipMemcpyHostToDevice, st));
             for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
-                if (depth == c->integ.max_depth && depth > 0) break;  // that step could only add counters
+                // the last trace can only add emitter hits, which count only after specular bounces or with MIS
+                if (depth == c->integ.max_depth && depth > 0 && !c->dsc.full) break;
                 int nxt = cur ^ 1;
                 const size_t qs = 3 * nmax;  // one queue = 3 bins of nmax
                 float4* cO = c->rayO + (size_t)cur * qs;
@@ -505,6 +513,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 pio.rng = c->rng; pio.dim = c->dim; pio.betaA = c->betaA; pio.betaB = c->betaB;
                 pio.LA = c->LA; pio.LB = c->LB;
                 pio.lamA = c->lamA; pio.lamB = c->lamB; pio.pdfA = c->pdfA; pio.pdfB = c->pdfB;
+                pio.prevPdf = c->prevPdf;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 e0 = ev_start(c, st);
                 HIPCHK(c, launch_path_shade(st, c->grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
@@ -558,6 +567,9 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     ds.f1_n = (int)c->hs.F1.l.size();
     std::memcpy(ds.f1_lambda, c->hs.F1.l.data(), 4 * ds.f1_n);
     std::memcpy(ds.f1_value, c->hs.F1.v.data(), 4 * ds.f1_n);
+    ds.bk7_n = (int)c->hs.BK7.l.size();
+    std::memcpy(ds.bk7_lambda, c->hs.BK7.l.data(), 4 * ds.bk7_n);
+    std::memcpy(ds.bk7_value, c->hs.BK7.v.data(), 4 * ds.bk7_n);
     hipMemcpy(c->d_spec, &ds, sizeof(ds), hipMemcpyHostToDevice);
     hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * C_NCOUNTERS);
     // a20 resolve matrices: XYZFromSensorRGB (WhiteBalance of identical whites, color.h:616-628) and the sRGB
@@ -643,9 +655,43 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         for (int t = 0; t < s->n_triangles; ++t)
             if (s->tri_material[t] < 0 || s->tri_material[t] >= std::max(1, s->n_materials))
                 return fail(c, RT_E_ARG, "material id out of range");
-    if (s->n_lights > 1) return fail(c, RT_E_ARG, "one quad light supported in this build (DESIGN.md §Path mode)");
-    if (s->n_lights == 1 && (s->lights[0].material < 0 || s->lights[0].material >= s->n_materials))
-        return fail(c, RT_E_ARG, "light material out of range");
+    auto mat_ok = [&](int m) { return m >= 0 && m < std::max(1, s->n_materials); };
+    for (int i = 0; i < s->n_materials; ++i) {
+        const rt_material& m = s->materials[i];
+        if (m.type < RT_MAT_DIFFUSE || m.type > RT_MAT_DIELECTRIC) return fail(c, RT_E_ARG, "unknown material type");
+        if (m.type == RT_MAT_DIELECTRIC && m.eta < 0) return fail(c, RT_E_ARG, "dielectric eta must be >= 0");
+    }
+    if (s->n_shapes < 0 || (s->n_shapes > 0 && !s->shapes)) return fail(c, RT_E_ARG, "shapes");
+    for (int i = 0; i < s->n_shapes; ++i) {
+        const rt_shape& h = s->shapes[i];
+        if (!mat_ok(h.material)) return fail(c, RT_E_ARG, "shape material out of range");
+        if (h.type == RT_SHAPE_SPHERE) {
+            if (!(h.radius > 0) || h.zmin > -h.radius || h.zmax < h.radius || h.phimax < 360.f)
+                return fail(c, RT_E_ARG, "only full spheres are supported (zmin <= -r, zmax >= r, phimax >= 360)");
+        } else if (h.type == RT_SHAPE_DISK) {
+            if (h.phimax < 360.f || !(h.outer_radius > 0) || h.inner_radius < 0)
+                return fail(c, RT_E_ARG, "only full disks are supported (phimax >= 360)");
+        } else if (h.type != RT_SHAPE_TRIANGLE) {
+            return fail(c, RT_E_ARG, "unknown shape type");
+        }
+    }
+    if (s->n_lights < 0 || s->n_lights > kMaxLights || (s->n_lights > 0 && !s->lights))
+        return fail(c, RT_E_ARG, "lights: at most " + std::to_string(kMaxLights));
+    for (int i = 0; i < s->n_lights; ++i) {
+        const rt_light& L = s->lights[i];
+        if (L.type == RT_LIGHT_QUAD) {
+            if (!mat_ok(L.material) || !(s->materials && s->materials[L.material].emission_scale > 0))
+                return fail(c, RT_E_ARG, "quad light needs an emissive material");
+        } else if (L.type == RT_LIGHT_DISK) {
+            if (L.shape < 0 || L.shape >= s->n_shapes || s->shapes[L.shape].type != RT_SHAPE_DISK ||
+                s->shapes[L.shape].inner_radius != 0 || !(s->materials[s->shapes[L.shape].material].emission_scale > 0))
+                return fail(c, RT_E_ARG, "disk light needs an emissive full DISK shape with inner radius 0");
+        } else if (L.type == RT_LIGHT_DISTANT) {
+            if (L.dir[0] == 0 && L.dir[1] == 0 && L.dir[2] == 0) return fail(c, RT_E_ARG, "distant light direction");
+        } else if (L.type != RT_LIGHT_POINT) {
+            return fail(c, RT_E_ARG, "unknown light type");
+        }
+    }
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     free_scene(c);
@@ -806,11 +852,54 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         }
     std::vector<int> tm(nt, 0);
     if (s->tri_material) tm.assign(s->tri_material, s->tri_material + nt);
-    std::vector<float4> mats;
-    for (int i = 0; i < s->n_materials; ++i)
-        mats.push_back(make_float4(s->materials[i].sigmoid[0], s->materials[i].sigmoid[1], s->materials[i].sigmoid[2],
-                                   s->materials[i].emission_scale));
-    if (mats.empty()) mats.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+    std::vector<DevMaterial> mats;
+    for (int i = 0; i < s->n_materials; ++i) {
+        const rt_material& m = s->materials[i];
+        mats.push_back(DevMaterial{m.sigmoid[0], m.sigmoid[1], m.sigmoid[2], m.emission_scale, m.type, m.eta, -1, 0});
+    }
+    if (mats.empty()) mats.push_back(DevMaterial{0.f, 0.f, 0.f, 0.f, RT_MAT_DIFFUSE, 0.f, -1, 0});
+    std::vector<DevShape> shapes(s->n_shapes);
+    for (int i = 0; i < s->n_shapes; ++i) {
+        const rt_shape& h = s->shapes[i];
+        DevShape& d = shapes[i];
+        d = DevShape{};
+        d.type = h.type; d.material = h.material; d.light = -1;
+        d.r = h.radius;
+        d.zmin = std::min(std::max(h.zmin, -h.radius), h.radius);  // glm::clamp(_zmin, -r, r) (Shapes.h:222-223)
+        d.zmax = std::min(std::max(h.zmax, -h.radius), h.radius);
+        d.h = h.height; d.ri = h.inner_radius; d.ro = h.outer_radius;
+        std::memcpy(d.o2r, h.object_to_render, 64); std::memcpy(d.r2o, h.render_to_object, 64);
+        std::memcpy(d.n2r, h.normal_to_render, 36);
+        std::memcpy(d.p1, h.p, 12); std::memcpy(d.p2, h.p + 3, 12); std::memcpy(d.p3, h.p + 6, 12);
+    }
+    std::vector<DevLight> lights(s->n_lights);
+    bool full = s->n_shapes > 0 || s->n_lights != 1;
+    for (const DevMaterial& m : mats) full = full || m.type != RT_MAT_DIFFUSE;
+    for (int i = 0; i < s->n_lights; ++i) {
+        const rt_light& q = s->lights[i];
+        DevLight& L = lights[i];
+        L = DevLight{};
+        L.type = q.type; L.shape = q.shape; L.material = q.material; L.scale = q.scale;
+        for (int k = 0; k < 3; ++k) { L.p[k] = q.p[k]; L.e1[k] = q.e1[k]; L.e2[k] = q.e2[k]; L.n[k] = q.n[k]; }
+        if (q.type == RT_LIGHT_QUAD) {
+            F3 cr = f3cross({q.e1[0], q.e1[1], q.e1[2]}, {q.e2[0], q.e2[1], q.e2[2]});
+            L.area = std::sqrt(f3dot(cr, cr));
+            if (mats[q.material].light < 0) mats[q.material].light = i;
+        } else if (q.type == RT_LIGHT_DISK) {
+            const DevShape& ds = shapes[q.shape];
+            const float phimax = 360.0f * 0.01745329251994329576923690768489f;  // glm::radians(360.f)
+            L.area = phimax * .5f * (ds.ro * ds.ro - ds.ri * ds.ri);           // Disk::Area (Shapes.h:641-644)
+            F3 n = f3norm(m3v(ds.n2r, F3{0.f, 0.f, 1.f}));
+            L.n[0] = n.x; L.n[1] = n.y; L.n[2] = n.z;
+            L.material = ds.material; L.ro = ds.ro; L.h = ds.h;
+            std::memcpy(L.o2r, ds.o2r, 64);
+            shapes[q.shape].light = i;
+        } else if (q.type == RT_LIGHT_DISTANT) {
+            F3 d = f3norm(F3{q.dir[0], q.dir[1], q.dir[2]});
+            L.dir[0] = d.x; L.dir[1] = d.y; L.dir[2] = d.z;
+        }
+        if (q.type != RT_LIGHT_QUAD) full = true;
+    }
     // upload
     auto up = [&](const void* src, size_t bytes, void** dst) -> int {
         void* p = nullptr;
@@ -820,21 +909,27 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         *dst = p;
         return RT_OK;
     };
-    void *pA, *pB, *pl0, *pl1, *pt0, *pt1 = nullptr, *ptw, *ptn, *ptm, *pm;
+    void *pA, *pB, *pl0, *pl1, *pt0, *pt1 = nullptr, *ptw, *ptn, *ptm, *pm, *psh, *plt;
     int rc;
     if ((rc = up(nA.data(), nA.size() * 16, &pA)) || (rc = up(nB.data(), nB.size() * 16, &pB)) ||
         (rc = up(lr0.data(), lr0.size() * 8, &pl0)) || (rc = up(lr1.data(), lr1.size() * 8, &pl1)) ||
         (rc = up(tiles0.data(), tiles0.size() * 16, &pt0)) || (rc = up(tiles1.data(), tiles1.size() * 16, &pt1)) ||
         (rc = up(tw.data(), tw.size() * 16, &ptw)) || (rc = up(tn.data(), tn.size() * 16, &ptn)) ||
-        (rc = up(tm.data(), tm.size() * 4, &ptm)) || (rc = up(mats.data(), mats.size() * 16, &pm)))
+        (rc = up(tm.data(), tm.size() * 4, &ptm)) || (rc = up(mats.data(), mats.size() * sizeof(DevMaterial), &pm)) ||
+        (rc = up(shapes.data(), shapes.size() * sizeof(DevShape), &psh)) ||
+        (rc = up(lights.data(), lights.size() * sizeof(DevLight), &plt)))
         return rc;
     DevScene& d = c->dsc;
     d.nodeA = (const float4*)pA; d.nodeB = (const float4*)pB;
     d.leafRange[0] = (const int2*)pl0; d.leafRange[1] = (const int2*)pl1;
     d.tiles[0] = (const float4*)pt0; d.tiles[1] = (const float4*)pt1;
     d.triWorld = (const float4*)ptw; d.triNormal = (const float4*)ptn;
-    d.triMaterial = (const int*)ptm; d.materials = (const float4*)pm;
+    d.triMaterial = (const int*)ptm; d.materials = (const DevMaterial*)pm;
+    d.shapes = (const DevShape*)psh; d.lights = (const DevLight*)plt;
     d.n_nodes = nn;
+    d.n_tris = nt;
+    d.n_shapes = s->n_shapes;
+    c->scene_full = full;
     d.qcap = qcap;
     if (qcap == 0) {
         int rs = 1;
@@ -848,15 +943,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         d.ring = (int*)pr;
     }
     d.n_lights = s->n_lights;
-    if (s->n_lights == 1) {
-        const rt_quad_light& q = s->lights[0];
-        for (int k = 0; k < 3; ++k) {
-            d.light0.p[k] = q.p[k]; d.light0.e1[k] = q.e1[k]; d.light0.e2[k] = q.e2[k]; d.light0.n[k] = q.n[k];
-        }
-        F3 cr = f3cross({q.e1[0], q.e1[1], q.e1[2]}, {q.e2[0], q.e2[1], q.e2[2]});
-        d.light0.area = std::sqrt(f3dot(cr, cr));
-        d.light0.material = q.material;
-    }
+    if (s->n_lights >= 1) d.light0 = lights[0];
     c->have_scene = true;
     return RT_OK;
 }
@@ -892,7 +979,8 @@ int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
 
 int rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
     if (!c || !d) return RT_E_ARG;
-    if (d->kind != RT_INTEGRATOR_REFERENCE && d->kind != RT_INTEGRATOR_PATH) return fail(c, RT_E_ARG, "unknown integrator");
+    if (d->kind != RT_INTEGRATOR_REFERENCE && d->kind != RT_INTEGRATOR_PATH && d->kind != RT_INTEGRATOR_PATH_MIS)
+        return fail(c, RT_E_ARG, "unknown integrator");
     if (d->max_depth < 0 || d->max_depth > 64) return fail(c, RT_E_ARG, "max_depth out of range");
     if (d->kind == RT_INTEGRATOR_REFERENCE &&
         !(d->albedo_rgb[0] == d->albedo_rgb[1] && d->albedo_rgb[1] == d->albedo_rgb[2] && d->albedo_rgb[0] > 0 &&
@@ -1062,7 +1150,7 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
         hipMemcpy(dp, pixel_ids, 4 * (size_t)n, hipMemcpyHostToDevice);
         hipMemcpy(di, indices, 4 * (size_t)n, hipMemcpyHostToDevice);
         SampleIds ids{nullptr, 1, 0, dp, di};
-        GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB, nullptr, nullptr,
+        GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB, nullptr, nullptr, nullptr,
                   nullptr, nullptr, nullptr, nullptr};
         DevFilm fd = dev_film(c->film);
         TraceIO tio{c->rayO, c->rayD, nullptr, n, 0, c->cull ? 1 : 0, c->hitB, c->hitPrim};

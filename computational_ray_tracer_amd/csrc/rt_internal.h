@@ -22,6 +22,8 @@ struct DevSpectra {                 // Spectra::Init products (spectrum.cpp:2612
     float X[kSpecN], Y[kSpecN], Z[kSpecN], D65[kSpecN];
     float f1_lambda[kF1Max], f1_value[kF1Max];
     int f1_n;
+    float bk7_lambda[kF1Max], bk7_value[kF1Max];   // glass-BK7 eta, FromInterleaved(.., false) (spectrum.cpp:2674)
+    int bk7_n;
 };
 
 struct DevCamera {
@@ -38,10 +40,30 @@ struct DevFilm {
     float rx, ry, imaging_ratio;
 };
 
-struct DevLight {
+struct DevLight {                   // rt_light (build-defined)
     float p[3], e1[3], e2[3], n[3];
     float area;
     int material;
+    int type, shape;
+    float dir[3];
+    float scale;
+    float ro, h;                    // disk: outer radius and height of shapes[shape]
+    float o2r[16];                  // disk: ObjectToRender of shapes[shape]
+};
+
+struct DevMaterial {                // rt_material + the area light it feeds (MIS)
+    float c0, c1, c2, emit;
+    int type;
+    float eta;
+    int light;
+    int pad;
+};
+
+struct DevShape {                   // rt_shape (Shapes.h:209-907)
+    int type, material, light, pad;
+    float r, zmin, zmax, h, ri, ro;
+    float o2r[16], r2o[16], n2r[9];
+    float p1[3], p2[3], p3[3];
 };
 
 struct DevScene {
@@ -52,9 +74,15 @@ struct DevScene {
     const float4* triWorld;
     const float4* triNormal;
     const int* triMaterial;
-    const float4* materials;        // (c0, c1, c2, emission_scale)
+    const DevMaterial* materials;
+    const DevShape* shapes;         // analytic shapes, intersected after the octree (prim id = n_tris + index)
+    const DevLight* lights;
     int n_nodes;
+    int n_tris;
+    int n_shapes;
     int n_lights;
+    int mis;                        // RT_INTEGRATOR_PATH_MIS
+    int full;                       // path shading needs the general kernel (shapes, specular, >1 / non-quad lights, MIS)
     DevLight light0;
     int qcap;                       // BFS group FIFO size (compiled variants); 0 = global-memory ring below
     int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
@@ -84,6 +112,7 @@ struct GenOut {
     float4* rayO; float4* rayD; int* slot;
     float4* lamA; float4* lamB; float4* pdfA; float4* pdfB;
     uint4* rng; int* dim;                                 // path-mode sampler state (nullptr in reference mode)
+    float* prevPdf;                                       // path mode, general kernel: set to 0 (camera ray)
     float4* betaA; float4* betaB; float4* LA; float4* LB;
 };
 
@@ -116,7 +145,8 @@ struct PathIO {
     float4* nO; float4* nD; int* nSlot; int* nCount;                            // next binned queue
     size_t bstride;
     uint4* rng; int* dim; float4* betaA; float4* betaB; float4* LA; float4* LB;
-    const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
+    const float4* lamA; const float4* lamB; float4* pdfA; float4* pdfB;  // pdf: TerminateSecondary writes it
+    float* prevPdf;                                                       // pdf of the last diffuse bounce
     int depth, max_depth;
 };
 

@@ -183,6 +183,7 @@ __global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevC
             out.betaB[s] = make_float4(1.f, 1.f, 1.f, 1.f);
             out.LA[s] = make_float4(0.f, 0.f, 0.f, 0.f);
             out.LB[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (out.prevPdf) out.prevPdf[s] = 0.f;
         }
     }
 }
@@ -197,6 +198,17 @@ __device__ __forceinline__ float4 ldc4(const float4* p, int i) {
 __device__ __forceinline__ int2 ldc2i(const int2* p, int i) {
     i2v v = ((const __attribute__((address_space(4))) i2v*)p)[i];
     return make_int2(v.x, v.y);
+}
+// a whole record (shape, light) at a wave-uniform index through the scalar cache
+template <class T>
+__device__ __forceinline__ T ldconst(const T* p, int i) {
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    T r;
+    const __attribute__((address_space(4))) int* src = (const __attribute__((address_space(4))) int*)(p + i);
+    int* dst = (int*)&r;
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k) dst[k] = src[k];
+    return r;
 }
 
 // ===================================================================================== K2 traverse
@@ -320,6 +332,17 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
         int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
                                              b0, b1, b2, t, nn, nt);
+        if (sc.n_shapes) {  // analytic shapes after the octree, running tMax; hitB = object-space point
+            float tm = prim >= 0 ? t : 3.402823466e+38f;
+            for (int si = 0; si < sc.n_shapes; ++si) {
+                DevShape sh = ldconst(sc.shapes, si);
+                V3 ph;
+                float th;
+                if (shape_isect(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
+                    prim = sc.n_tris + si; b0 = ph.x; b1 = ph.y; b2 = ph.z; t = th; tm = th;
+                }
+            }
+        }
         io.hitB[k] = make_float4(b0, b1, b2, t);
         io.hitPrim[k] = prim;
         nh += prim >= 0;
@@ -443,7 +466,8 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                 V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
                 float4 d4 = io.rayD[q];
                 V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
-                float4 mt = sc.materials[sc.triMaterial[prim]];
+                DevMaterial dm = sc.materials[sc.triMaterial[prim]];
+                float4 mt = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
                 if (mt.w > 0) {
                     if (io.depth == 0 && vdot(ng, rayd) < 0) {
                         float L[8];
@@ -485,7 +509,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                         float cs = vdot(nrm, wi);
                         float cl = -vdot(v3(Lq.n[0], Lq.n[1], Lq.n[2]), wi);
                         if (cs > 0 && cl > 0) {
-                            float le = sc.materials[Lq.material].w;
+                            float le = sc.materials[Lq.material].emit;
                             float G = (cs * cl) / dist2;
                             float wgt = G * Lq.area;
 #pragma unroll
@@ -535,6 +559,270 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
 #pragma unroll
                 for (int i = 0; i < 8; ++i) L[i] += Ld[i];
                 store8(io.LA, io.LB, slot, L);
+            }
+        }
+        long pn = block_append_bin(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
+        if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
+    }
+    count_add(ctr, C_SNODES, snn);
+    count_add(ctr, C_STRIS, snt);
+    count_add(ctr, C_SHADOW, nsh);
+}
+
+// ------------------------------------------------------------------- path mode, general scenes (§8 a21/a22)
+// Same bounce as k_path_shade for scenes that need more than one quad light and Lambert triangles: analytic
+// shapes, mirror and BK7/constant-eta glass (TerminateSecondary rewrites the sample's pdf), point / distant /
+// disk / quad lights (one sample each, shadow rays traced inline in light order), and MIS (power heuristic).
+// Semantics and sample-dimension order: oracle/rtcore.hpp LiPath, DESIGN.md §5.
+__device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevFilm& film, const PathIO& io, int slot,
+                                                Smp& sm, uint4& rs) {
+    int pixel, index, x, y;
+    sample_of(ids, slot, pixel, index);
+    pixel_xy(film, pixel, x, y);
+    rs = io.rng[slot];
+    sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
+    sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
+    sm.px = x; sm.py = y; sm.index = index; sm.dim = io.dim[slot];
+}
+__device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm, uint4 rs) {
+    io.rng[slot] = make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), rs.z, rs.w);
+    io.dim[slot] = sm.dim;
+}
+template <int QCAP>
+__device__ __forceinline__ bool scene_occluded(const DevScene& sc, V3 o, V3 d, float tmax, unsigned long long& nn,
+                                               unsigned long long& nt) {
+    float b0, b1, b2, t;
+    if (traverse_any<QCAP, true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0) return true;
+    for (int si = 0; si < sc.n_shapes; ++si) {
+        DevShape sh = ldconst(sc.shapes, si);
+        V3 ph;
+        float th;
+        if (shape_isect(sh, o, d, tmax, ph, th)) return true;
+    }
+    return false;
+}
+
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const DevSpectra* sp, DevSampler smp,
+                                                            DevFilm film, SampleIds ids, PathIO io,
+                                                            unsigned long long* ctr) {
+    const float InvPi = 0.31830988618379067154f;
+    __shared__ int lds[4 * (kBlock / 64) + 3];
+    int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
+    int n = c0 + c1 + c2;
+    unsigned long long snn = 0, snt = 0, nsh = 0;
+    for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        int k = base + threadIdx.x;
+        bool wantNext = false;
+        float4 nO = make_float4(0, 0, 0, 0), nD = nO;
+        int nbin = -1, slot = -1;
+        if (k < n) {
+            size_t q = queue_pos(k, c0, c1, io.bstride);
+            slot = io.slot[q];
+            int prim = io.hitPrim[k];
+            if (prim >= 0) {
+                float lam[8], beta[8], L[8];
+                load8(io.lamA, io.lamB, slot, lam);
+                load8(io.betaA, io.betaB, slot, beta);
+                load8(io.LA, io.LB, slot, L);
+                float4 o4 = io.rayO[q], d4 = io.rayD[q];
+                V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
+                V3 rayd = vnorm(rdw);
+                float4 hb = io.hitB[k];
+                // ---- surface (oracle SurfaceAt)
+                V3 p, nrm, nout;
+                bool front;
+                int mid, lidx;
+                if (prim < sc.n_tris) {
+                    float4 P0 = sc.triWorld[3 * prim], P1 = sc.triWorld[3 * prim + 1], P2 = sc.triWorld[3 * prim + 2];
+                    V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
+                    V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));
+                    p = vadd(vadd(vmul(p0, hb.x), vmul(p1, hb.y)), vmul(p2, hb.z));
+                    nout = ng;
+                    front = vdot(ng, rayd) < 0;
+                    nrm = ng;
+                    if (vdot(nrm, rayd) > 0) nrm = v3(-ng.x, -ng.y, -ng.z);
+                    mid = sc.triMaterial[prim];
+                    lidx = sc.materials[mid].light;
+                } else {
+                    const DevShape& s = sc.shapes[prim - sc.n_tris];
+                    V3 rdo = vnorm(m4_dir(s.r2o, rdw));
+                    V3 ph = v3(hb.x, hb.y, hb.z);
+                    V3 no = shape_normal_obj(s, ph);
+                    bool flip = vdot(no, rdo) > 0;
+                    if (flip) no = v3(-no.x, -no.y, -no.z);
+                    V3 nw = vnorm(m3_mul(s.n2r, no));
+                    p = m4_point(s.o2r, ph);
+                    nrm = nw;
+                    front = !flip;
+                    nout = flip ? v3(-nw.x, -nw.y, -nw.z) : nw;
+                    mid = s.material;
+                    lidx = s.light;
+                }
+                const DevMaterial mt = sc.materials[mid];
+                float prevPdf = io.prevPdf[slot];
+                if (mt.emit > 0) {  // one-sided pure emitter, ends the path
+                    if (front) {
+                        if (prevPdf == 0) {
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.emit * dense_query(sp->D65, lam[i]));
+                        } else if (sc.mis && lidx >= 0) {
+                            const DevLight& Lt = sc.lights[lidx];
+                            V3 dv = vsub(p, ro);
+                            float dist2 = vdot(dv, dv);
+                            float cl = -vdot(v3(Lt.n[0], Lt.n[1], Lt.n[2]), rayd);
+                            if (cl > 0) {
+                                float wb = power_heuristic(prevPdf, dist2 / (cl * Lt.area));
+#pragma unroll
+                                for (int i = 0; i < 8; ++i)
+                                    L[i] += (beta[i] * (mt.emit * dense_query(sp->D65, lam[i]))) * wb;
+                            }
+                        }
+                        store8(io.LA, io.LB, slot, L);
+                    }
+                } else if (io.depth < io.max_depth) {
+                    float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
+                    float R[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.c0, mt.c1, mt.c2, lam[i]);
+                    if (mt.type == 1) {  // perfect mirror: no sampler draws
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) beta[i] *= R[i];
+                        store8(io.betaA, io.betaB, slot, beta);
+                        V3 po = vadd(p, vmul(nrm, off)), wi = reflect_dir(rayd, nrm);
+                        wantNext = true;
+                        nO = make_float4(po.x, po.y, po.z, 0.f);
+                        nD = make_float4(wi.x, wi.y, wi.z, 0.f);
+                        nbin = RT_KZ_BINS ? dominant_axis(wi) : 0;
+                        io.prevPdf[slot] = 0.f;
+                    } else {
+                        Smp sm;
+                        uint4 rs;
+                        restore_sampler(ids, film, io, slot, sm, rs);
+                        if (mt.type == 2) {  // smooth dielectric
+                            if (mt.eta == 0) {  // dispersive BK7: TerminateSecondary (spectrum.h:302-310)
+                                float pdf[8];
+                                load8(io.pdfA, io.pdfB, slot, pdf);
+                                bool term = true;
+#pragma unroll
+                                for (int i = 1; i < 8; ++i) term = term && pdf[i] == 0;
+                                if (!term) {
+#pragma unroll
+                                    for (int i = 1; i < 8; ++i) pdf[i] = 0;
+                                    pdf[0] /= 8;
+                                    store8(io.pdfA, io.pdfB, slot, pdf);
+                                }
+                            }
+                            float eta = mt.eta != 0 ? mt.eta : piecewise_query(sp->bk7_lambda, sp->bk7_value, sp->bk7_n, lam[0]);
+                            float u = sm.get1d(smp);
+                            V3 wo = v3(-rayd.x, -rayd.y, -rayd.z);
+                            float Fr = fr_dielectric(vdot(nout, wo), eta);
+                            V3 wt, po, wi;
+                            float etap;
+                            if (u < Fr || !refract_dir(wo, nout, eta, etap, wt)) {
+                                po = vadd(p, vmul(nrm, off));
+                                wi = reflect_dir(rayd, nrm);
+                            } else {
+#pragma unroll
+                                for (int i = 0; i < 8; ++i) beta[i] /= (etap * etap);
+                                store8(io.betaA, io.betaB, slot, beta);
+                                po = vsub(p, vmul(nrm, off));
+                                wi = wt;
+                            }
+                            wantNext = true;
+                            nO = make_float4(po.x, po.y, po.z, 0.f);
+                            nD = make_float4(wi.x, wi.y, wi.z, 0.f);
+                            nbin = RT_KZ_BINS ? dominant_axis(wi) : 0;
+                            io.prevPdf[slot] = 0.f;
+                        } else {  // Lambert: NEE per light, then a cosine-hemisphere bounce
+                            V3 po = vadd(p, vmul(nrm, off));
+                            for (int li = 0; li < sc.n_lights; ++li) {
+                                const DevLight Lt = ldconst(sc.lights, li);
+                                float u0, u1;
+                                sm.get2d(smp, u0, u1);
+                                V3 wi;
+                                float tmax, wgt, sc_le;
+                                bool ok;
+                                int lmat = Lt.material;
+                                if (Lt.type <= 1) {
+                                    V3 pl;
+                                    if (Lt.type == 0) {
+                                        pl = vadd(vadd(v3(Lt.p[0], Lt.p[1], Lt.p[2]), vmul(v3(Lt.e1[0], Lt.e1[1], Lt.e1[2]), u0)),
+                                                  vmul(v3(Lt.e2[0], Lt.e2[1], Lt.e2[2]), u1));
+                                    } else {
+                                        float dx, dy;
+                                        disk_concentric(u0, u1, dx, dy);
+                                        pl = m4_point(Lt.o2r, v3(Lt.ro * dx, Lt.ro * dy, Lt.h));
+                                    }
+                                    V3 wv = vsub(pl, po);
+                                    float dist2 = vdot(wv, wv);
+                                    float dist = sqrtf(dist2);
+                                    wi = vmul(wv, 1.0f / dist);
+                                    float cs = vdot(nrm, wi);
+                                    float cl = -vdot(v3(Lt.n[0], Lt.n[1], Lt.n[2]), wi);
+                                    ok = cs > 0 && cl > 0;
+                                    tmax = dist * 0.999f;
+                                    float G = (cs * cl) / dist2;
+                                    wgt = G * Lt.area;
+                                    if (sc.mis) wgt = wgt * power_heuristic(dist2 / (cl * Lt.area), cs * InvPi);
+                                    sc_le = sc.materials[lmat].emit;
+                                } else {
+                                    float fall;
+                                    if (Lt.type == 2) {
+                                        V3 wv = vsub(v3(Lt.p[0], Lt.p[1], Lt.p[2]), po);
+                                        float dist2 = vdot(wv, wv);
+                                        float dist = sqrtf(dist2);
+                                        wi = vmul(wv, 1.0f / dist);
+                                        tmax = dist * 0.999f;
+                                        fall = 1.0f / dist2;
+                                    } else {
+                                        wi = v3(Lt.dir[0], Lt.dir[1], Lt.dir[2]);
+                                        tmax = 3.402823466e+38f;
+                                        fall = 1.0f;
+                                    }
+                                    float cs = vdot(nrm, wi);
+                                    ok = cs > 0;
+                                    wgt = cs * fall;
+                                    sc_le = Lt.scale;
+                                }
+                                if (ok) {
+                                    ++nsh;
+                                    if (!scene_occluded<QCAP>(sc, po, wi, tmax, snn, snt)) {
+#pragma unroll
+                                        for (int i = 0; i < 8; ++i) {
+                                            float Le = sc_le * dense_query(sp->D65, lam[i]);
+                                            L[i] += ((beta[i] * (R[i] * InvPi)) * Le) * wgt;
+                                        }
+                                    }
+                                }
+                            }
+                            store8(io.LA, io.LB, slot, L);
+                            // cosine-hemisphere bounce (Sampling.h:449-454), pbrt CoordinateSystem frame
+                            float u0, u1, dx, dy;
+                            sm.get2d(smp, u0, u1);
+                            disk_concentric(u0, u1, dx, dy);
+                            float z = 1 - dx * dx - dy * dy;
+                            z = sqrtf(z > 0.f ? z : 0.f);
+                            if (z != 0) {
+                                float sign = copysignf(1.0f, nrm.z);
+                                float a = -1 / (sign + nrm.z);
+                                float b = nrm.x * nrm.y * a;
+                                V3 ss = v3(1 + sign * (nrm.x * nrm.x) * a, sign * b, -sign * nrm.x);
+                                V3 tt = v3(b, sign + (nrm.y * nrm.y) * a, -nrm.y);
+                                V3 wi = vadd(vadd(vmul(ss, dx), vmul(tt, dy)), vmul(nrm, z));
+#pragma unroll
+                                for (int i = 0; i < 8; ++i) beta[i] *= R[i];
+                                store8(io.betaA, io.betaB, slot, beta);
+                                wantNext = true;
+                                nO = make_float4(po.x, po.y, po.z, 0.f);
+                                nD = make_float4(wi.x, wi.y, wi.z, 0.f);
+                                nbin = RT_KZ_BINS ? dominant_axis(wi) : 0;
+                                io.prevPdf[slot] = z * InvPi;
+                            }
+                        }
+                        save_sampler(io, slot, sm, rs);
+                    }
+                }
             }
         }
         long pn = block_append_bin(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
@@ -638,15 +926,21 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
     int gb = grid > 0 ? grid : 1;
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 g(gb), b(kBlock);
+#define RT_SHADE_CASE(Q)                                                                                         \
+    case Q:                                                                                                      \
+        if (sc.full) hipLaunchKernelGGL(k_path_shade_full<Q>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr);    \
+        else hipLaunchKernelGGL(k_path_shade<Q>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr);                 \
+        break;
     switch (qcap) {
-        case 0: hipLaunchKernelGGL(k_path_shade<0>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
-        case 1: hipLaunchKernelGGL(k_path_shade<1>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
-        case 16: hipLaunchKernelGGL(k_path_shade<16>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
-        case 64: hipLaunchKernelGGL(k_path_shade<64>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
-        case 256: hipLaunchKernelGGL(k_path_shade<256>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
-        case 1024: hipLaunchKernelGGL(k_path_shade<1024>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr); break;
+        RT_SHADE_CASE(0)
+        RT_SHADE_CASE(1)
+        RT_SHADE_CASE(16)
+        RT_SHADE_CASE(64)
+        RT_SHADE_CASE(256)
+        RT_SHADE_CASE(1024)
         default: return hipErrorInvalidValue;
     }
+#undef RT_SHADE_CASE
     return hipGetLastError();
 }
 

@@ -172,6 +172,60 @@ class Integrator:
         return d
 
 
+# ------------------------------------------------------------------------------- analytic shapes
+
+
+@dataclass
+class Shape:
+    """Shape(name, rigidtransform) base (Shapes.h:172-207): ObjectToRender = rigid * permutation_y_z,
+    RenderToObject = inverse (float64, rounded once), normal matrix = mat3(transpose(inverse(O2R)))."""
+    rigid: np.ndarray
+    material: int
+
+    def _fill(self, d):
+        o2r = np.asarray(self.rigid, float) @ PERM_YZ
+        r2o = np.linalg.inv(o2r)
+        d.object_to_render[:] = colmajor(o2r).tolist()
+        d.render_to_object[:] = colmajor(r2o).tolist()
+        d.normal_to_render[:] = np.asarray(r2o.T[:3, :3], float).T.astype(np.float32).reshape(-1).tolist()
+        d.material = self.material
+
+
+@dataclass
+class Sphere(Shape):
+    """Sphere(r, zmin=-r, zmax=r, phimax=360) (Shapes.h:209-432)."""
+    radius: float = 1.0
+
+    def desc(self, d):
+        self._fill(d)
+        d.type = capi.RT_SHAPE_SPHERE
+        d.radius, d.zmin, d.zmax, d.phimax = self.radius, -self.radius, self.radius, 360.0
+
+
+@dataclass
+class Disk(Shape):
+    """Disk(height, in_radius, out_radius, phimax=360) (Shapes.h:622-758); emits along object +z."""
+    height: float = 0.0
+    inner_radius: float = 0.0
+    outer_radius: float = 1.0
+
+    def desc(self, d):
+        self._fill(d)
+        d.type = capi.RT_SHAPE_DISK
+        d.height, d.inner_radius, d.outer_radius, d.phimax = self.height, self.inner_radius, self.outer_radius, 360.0
+
+
+@dataclass
+class TriangleSimple(Shape):
+    """TriangleSimple(p1, p2, p3) (Shapes.h:760-907), object space."""
+    p: tuple = ((0, 0, 0), (1, 0, 0), (0, 1, 0))
+
+    def desc(self, d):
+        self._fill(d)
+        d.type = capi.RT_SHAPE_TRIANGLE
+        d.p[:] = [float(np.float32(x)) for v in self.p for x in v]
+
+
 # ------------------------------------------------------------------------------------ meshes
 
 
@@ -188,8 +242,10 @@ class TriModel:
     cull_look: tuple = (0.0, 0.0, 1.0)
     octree_capacity: int = 40
     tri_material: np.ndarray = None
-    materials: list = field(default_factory=list)   # list of (sigmoid c0,c1,c2, emission_scale)
-    lights: list = field(default_factory=list)      # list of dict(p, e1, e2, n, material)
+    materials: list = field(default_factory=list)   # (sigmoid c0,c1,c2, emission_scale[, type, eta])
+    lights: list = field(default_factory=list)      # dict(type=QUAD: p, e1, e2, n, material | DISK: shape,
+                                                    #      material | POINT: p, scale | DISTANT: dir, scale)
+    shapes: list = field(default_factory=list)      # Sphere / Disk / TriangleSimple, after the octree
 
     def object_to_render(self):
         return np.asarray(self.rigid, float) @ PERM_YZ
@@ -217,20 +273,32 @@ class TriModel:
             d.tri_material = self._mat.ctypes.data_as(C.POINTER(C.c_int32))
         mats = self.materials or [((0.0, 0.0, 0.0), 0.0)]
         self._mats = (capi.rt_material * len(mats))()
-        for i, (c, e) in enumerate(mats):
-            self._mats[i].type = capi.RT_MAT_DIFFUSE
+        for i, m in enumerate(mats):
+            c, e = m[0], m[1]
+            self._mats[i].type = m[2] if len(m) > 2 else capi.RT_MAT_DIFFUSE
             self._mats[i].sigmoid[:] = [float(np.float32(x)) for x in c]
             self._mats[i].emission_scale = e
+            self._mats[i].eta = m[3] if len(m) > 3 else 0.0
         d.n_materials = len(mats)
         d.materials = C.cast(self._mats, C.POINTER(capi.rt_material))
         if self.lights:
-            self._lights = (capi.rt_quad_light * len(self.lights))()
+            self._lights = (capi.rt_light * len(self.lights))()
             for i, L in enumerate(self.lights):
-                for k in ("p", "e1", "e2", "n"):
-                    getattr(self._lights[i], k)[:] = [float(np.float32(x)) for x in L[k]]
-                self._lights[i].material = L["material"]
+                self._lights[i].type = L.get("type", capi.RT_LIGHT_QUAD)
+                for k in ("p", "e1", "e2", "n", "dir"):
+                    if k in L:
+                        getattr(self._lights[i], k)[:] = [float(np.float32(x)) for x in L[k]]
+                self._lights[i].scale = L.get("scale", 0.0)
+                self._lights[i].shape = L.get("shape", -1)
+                self._lights[i].material = L.get("material", -1)
             d.n_lights = len(self.lights)
-            d.lights = C.cast(self._lights, C.POINTER(capi.rt_quad_light))
+            d.lights = C.cast(self._lights, C.POINTER(capi.rt_light))
+        if self.shapes:
+            self._shapes = (capi.rt_shape * len(self.shapes))()
+            for i, s in enumerate(self.shapes):
+                s.desc(self._shapes[i])
+            d.n_shapes = len(self.shapes)
+            d.shapes = C.cast(self._shapes, C.POINTER(capi.rt_shape))
         self._desc = d
         return d
 
@@ -445,3 +513,51 @@ def cfg3_blob(res=(1920, 1080), spp_side=16, n_index=None, max_depth=5, frequenc
     return Config(f"cfg3_blob{len(idx)}_{res[0]}x{res[1]}_{spp_side * spp_side}spp", model, cam,
                   StratifiedSampler(spp_side, spp_side, True, 0), Film(res=res, filter=capi.RT_FILTER_BOX),
                   Integrator(capi.RT_INTEGRATOR_PATH, max_depth=max_depth), 0, n_index)
+
+
+def mixed_scene(frequency=70):
+    """SURVEY §8(d) CFG4 scene: the CFG3 procedural mesh (smaller, back right) in the Cornell box, three
+    spheres — diffuse, perfect mirror, BK7 glass — and four lights: the ceiling quad, a disk under the ceiling,
+    a point light and a sun shining in through the open front (build-defined placement constants)."""
+    pos, _, idx = procedural_blob(frequency=frequency, radius=1.0, seed=1)
+    tri = pos[idx].astype(np.float64)
+    lo = tri.reshape(-1, 3).min(0)
+    s = 105.0
+    world = tri * s + np.array([370.0, -lo[1] * s + 0.5, 380.0])
+    model = cornell_box(blocks=False, extra=world)
+    W, R, G, L = 0, 1, 2, 3
+    mats = list(model.materials)
+    mats[L] = ((0.0, 0.0, 0.0), 12.0)                                            # ceiling quad: dimmer
+    DIFF, MIRR, GLASS, DISKL = len(mats), len(mats) + 1, len(mats) + 2, len(mats) + 3
+    mats += [(CORNELL_GREEN, 0.0, capi.RT_MAT_DIFFUSE, 0.0),
+             (grey_sigmoid(0.9), 0.0, capi.RT_MAT_MIRROR, 0.0),
+             ((0.0, 0.0, 0.0), 0.0, capi.RT_MAT_DIELECTRIC, 0.0),                # eta 0 = glass-BK7
+             ((0.0, 0.0, 0.0), 30.0)]
+    model.materials = mats
+    down = translate((150.0, 540.0, 430.0)) @ rotate(180.0, (1, 0, 0))             # disk normal -> -y
+    model.shapes = [Sphere(translate((120.0, 60.0, 330.0)), DIFF, radius=60.0),
+                    Sphere(translate((430.0, 70.0, 120.0)), MIRR, radius=70.0),
+                    Sphere(translate((215.0, 65.0, 140.0)), GLASS, radius=65.0),
+                    Disk(down, DISKL, height=0.0, inner_radius=0.0, outer_radius=40.0)]
+    quad = dict(model.lights[0])
+    quad["type"] = capi.RT_LIGHT_QUAD
+    model.lights = [quad,
+                    dict(type=capi.RT_LIGHT_DISK, shape=3),
+                    dict(type=capi.RT_LIGHT_POINT, p=(450.0, 420.0, 250.0), scale=4.0e4),
+                    dict(type=capi.RT_LIGHT_DISTANT, dir=(0.25, 0.6, -1.0), scale=1.5)]
+    return model
+
+
+def cfg4_mixed(res=(1920, 1080), spp=(32, 32), max_depth=5, frequency=70):
+    """BASELINE configs[3]: mixed scene, NEE + MIS (power heuristic), 1024 spp."""
+    cam = cornell_camera(res)
+    return Config(f"cfg4_mixed_{res[0]}x{res[1]}_{spp[0] * spp[1]}spp", mixed_scene(frequency), cam,
+                  StratifiedSampler(spp[0], spp[1], True, 0), Film(res=res, filter=capi.RT_FILTER_BOX),
+                  Integrator(capi.RT_INTEGRATOR_PATH_MIS, max_depth=max_depth), 0, spp[0] * spp[1])
+
+
+def cfg5_spectral(res=(3840, 2160), spp=(64, 32), max_depth=5, frequency=70):
+    """BASELINE configs[4]: the CFG4 scene, 8 hero wavelengths per path, 4K, 2048 spp."""
+    c = cfg4_mixed(res=res, spp=spp, max_depth=max_depth, frequency=frequency)
+    c.name = f"cfg5_spectral_{res[0]}x{res[1]}_{spp[0] * spp[1]}spp"
+    return c

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 typedef enum {
     RT_OK = 0,
@@ -45,21 +45,50 @@ typedef struct {
 /* Film pixel, layout-identical to `pixel {glm::vec3 rgbsum; float weightsum;}` (Film.h:6-9). */
 typedef struct { float r, g, b, w; } rt_pixel;
 
-enum { RT_MAT_DIFFUSE = 0 };
+enum { RT_MAT_DIFFUSE = 0, RT_MAT_MIRROR = 1, RT_MAT_DIELECTRIC = 2 };
 /* Build-defined material (the reference has none: Shading.h:1-21 is a comment stub).
- * Reflectance is an RGBSigmoidPolynomial (color.h:363-403): R(λ) = s(c0 λ² + c1 λ + c2).
- * emission_scale > 0 makes the triangle a pure one-sided emitter with Le = scale · stdillum-D65. */
+ * DIFFUSE: Lambert R/π; MIRROR: perfect specular reflection scaled by R; R(λ) is an RGBSigmoidPolynomial
+ *   (color.h:363-403): R(λ) = s(c0 λ² + c1 λ + c2).
+ * DIELECTRIC: smooth Fresnel glass; eta > 0 is a constant IOR, eta == 0 selects the dispersive
+ *   "glass-BK7" table (spectrum.cpp:2674-2691) with SampledWavelengths::TerminateSecondary (spectrum.h:302-310).
+ * emission_scale > 0 makes the surface a pure one-sided emitter with Le = scale · stdillum-D65. */
 typedef struct {
     int type;
     float sigmoid[3];
     float emission_scale;
+    float eta;
 } rt_material;
 
-/* Build-defined quad area light (Lights.h:1-10 is a comment stub): x = p + u·e1 + v·e2, normal n. */
+enum { RT_SHAPE_SPHERE = 0, RT_SHAPE_DISK = 1, RT_SHAPE_TRIANGLE = 2 };
+/* Analytic shapes besides the triangle octree (Shapes.h:172-907), intersected in object space.
+ * SPHERE: Sphere(r, zmin, zmax, phimax) (Shapes.h:209-432) — full spheres only (zmin <= -r, zmax >= r,
+ *   phimax >= 360), so the atan2 φ clip can never fire;  DISK: Disk(height, inner, outer, phimax)
+ *   (Shapes.h:622-758), phimax >= 360;  TRIANGLE: TriangleSimple(p1, p2, p3) (Shapes.h:760-907). */
 typedef struct {
-    float p[3], e1[3], e2[3], n[3];
+    int type;
+    float object_to_render[16];      /* column-major rigidtransform * permutation_y_z (Shapes.h:175-181) */
+    float render_to_object[16];      /* column-major glm::inverse(ObjectToRender)                        */
+    float normal_to_render[9];       /* column-major mat3(transpose(inverse(ObjectToRender))) (:150)     */
+    float radius, zmin, zmax, phimax;
+    float height, inner_radius, outer_radius;
+    float p[9];                      /* TriangleSimple p1, p2, p3 (object space) */
     int material;
-} rt_quad_light;
+} rt_shape;
+
+enum { RT_LIGHT_QUAD = 0, RT_LIGHT_DISK = 1, RT_LIGHT_POINT = 2, RT_LIGHT_DISTANT = 3 };
+/* Build-defined lights (Lights.h:1-10 is a comment stub naming area, point and sun lights).
+ * QUAD: x = p + u·e1 + v·e2, emitting normal n, Le from `material` (the quad is also geometry: two
+ *   emissive triangles of the mesh);  DISK: uniform area sampling of shapes[shape] (an emissive DISK
+ *   shape with inner_radius 0), Le from its material;  POINT: at p, intensity scale · D65;
+ *   DISTANT: unit direction `dir` towards the light, irradiance scale · D65. */
+typedef struct {
+    int type;
+    float p[3], e1[3], e2[3], n[3];
+    float dir[3];
+    float scale;
+    int shape;
+    int material;
+} rt_light;
 
 /* TriModel + Octtree_Model inputs (Shapes.h:1272-1491, Octtree_Model.h:33-63). */
 typedef struct {
@@ -77,7 +106,9 @@ typedef struct {
     int n_materials;
     const rt_material* materials;
     int n_lights;
-    const rt_quad_light* lights;
+    const rt_light* lights;
+    int n_shapes;                    /* analytic shapes, intersected after the octree in list order     */
+    const rt_shape* shapes;
 } rt_scene_desc;
 
 enum { RT_CAMERA_PERSPECTIVE = 0 };
@@ -110,11 +141,12 @@ typedef struct {
     float imaging_ratio;             /* 1/CIE_Y_integral in the reference app (RayTracerTestApp.h:149) */
 } rt_film_desc;
 
-enum { RT_INTEGRATOR_REFERENCE = 0, RT_INTEGRATOR_PATH = 1 };
+enum { RT_INTEGRATOR_REFERENCE = 0, RT_INTEGRATOR_PATH = 1, RT_INTEGRATOR_PATH_MIS = 2 };
 /* RT_INTEGRATOR_REFERENCE: the Li lambda of RayTracerTestApp.h:218-284 (ambient 0.3·F1 +
  *   clamp(n·(0,0,-1))·D65·albedo), octree back-face culling honoured.
- * RT_INTEGRATOR_PATH: build-defined diffuse path tracer with next-event estimation on quad lights
- *   (Integrator.h:1-14 is a stub; semantics in DESIGN.md §Path mode). */
+ * RT_INTEGRATOR_PATH: build-defined path tracer (Integrator.h:1-14 is a stub): one light
+ *   sample per light at every diffuse vertex (NEE), emitters seen by camera rays or specular bounces.
+ * RT_INTEGRATOR_PATH_MIS: the same plus BSDF-sampled emitter hits, both weighted by the power heuristic. */
 typedef struct {
     int kind;
     int max_depth;

@@ -49,6 +49,10 @@ def lib():
             "orc_spectra_query": ([C.c_int, C.c_int, P(C.c_float), P(C.c_float)], None),
             "orc_inner_product_y_d65": ([], C.c_float),
             "orc_sigmoid_eval": ([C.c_float] * 4, C.c_float),
+            "orc_fr_dielectric": ([C.c_float, C.c_float], C.c_float),
+            "orc_refract": ([P(C.c_float), P(C.c_float), C.c_float, P(C.c_float)], C.c_int),
+            "orc_bk7_eta": ([C.c_float], C.c_float),
+            "orc_power_heuristic": ([C.c_float, C.c_float], C.c_float),
             "orc_triangle_intersect": ([P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, P(C.c_float)], C.c_int),
             "orc_tribox_overlap": ([P(C.c_float)] * 3, C.c_int),
             "orc_bounds_intersect": ([P(C.c_float), P(C.c_float), P(C.c_float), C.c_float], C.c_int),

@@ -814,12 +814,118 @@ struct Filter {
     }
 };
 
+// ======================================================================= analytic shapes (a21)
+// Shape (Shapes.h:172-207): rays go to object space through RenderToObject; hits come back through
+// LocalSurfaceInfo::Transform(ObjectToRender) (Shapes.h:147-160).  Full spheres / disks only (φmax = 360°),
+// so the atan2 φ clips (Shapes.h:343-349, 710-713) can never reject and are not evaluated.
+struct AShape {
+    int type = 0;          // 0 sphere, 1 disk, 2 TriangleSimple
+    mat4 o2r, r2o;
+    mat3 n2r;
+    float r = 1, zmin = -1, zmax = 1;
+    float h = 0, ri = 0, ro = 1;
+    vec3 p1{}, p2{}, p3{};
+    int material = 0;
+};
+struct ShapeHit { vec3 phit; float t; };   // object-space hit point
+
+static inline void ObjRay(const AShape& s, const Ray& ray, vec3* o, vec3* d) {
+    vec4 o4 = mul(s.r2o, vec4{ray.o.x, ray.o.y, ray.o.z, 1});
+    vec4 d4 = mul(s.r2o, vec4{ray.d.x, ray.d.y, ray.d.z, 0});
+    *o = {o4.x, o4.y, o4.z};
+    *d = {d4.x, d4.y, d4.z};
+}
+// Shapes.h:294-376 Sphere::BasicIntersect
+static inline bool SphereIntersect(const AShape& s, vec3 o, vec3 d, float tMax, ShapeHit* out) {
+    const float r = s.r;
+    float a = d.x * d.x + d.y * d.y + d.z * d.z;
+    float b = 2 * (d.x * o.x + d.y * o.y + d.z * o.z);
+    float c = o.x * o.x + o.y * o.y + o.z * o.z - r * r;
+    vec3 v = sub(o, mul(d, b / (2 * a)));
+    float length = std::sqrt(dot(v, v));
+    float discrim = 4 * a * (r + length) * (r - length);
+    if (discrim < 0) return false;
+    float rootDiscrim = std::sqrt(discrim);
+    float q = (b < 0) ? -.5f * (b - rootDiscrim) : -.5f * (b + rootDiscrim);
+    float t0 = q / a, t1 = c / q;
+    if (t0 > t1) std::swap(t0, t1);
+    if (t0 > tMax || t1 <= 0) return false;
+    float tShapeHit = t0;
+    if (tShapeHit <= 0) {
+        tShapeHit = t1;
+        if (tShapeHit > tMax) return false;
+    }
+    auto refine = [&](float th) {
+        vec3 hp = add(o, mul(d, th));
+        hp = mul(hp, r / std::sqrt(dot(hp, hp)));  // hitp *= r / distance(hitp, 0)
+        if (hp.x == 0 && hp.y == 0) hp.x = (float)(1e-5 * (double)r);
+        return hp;
+    };
+    vec3 hitp = refine(tShapeHit);
+    if (hitp.z < s.zmin || hitp.z > s.zmax) {
+        if (tShapeHit == t1) return false;
+        if (t1 > tMax) return false;
+        tShapeHit = t1;
+        hitp = refine(tShapeHit);
+        if (hitp.z < s.zmin || hitp.z > s.zmax) return false;
+    }
+    *out = {hitp, tShapeHit};
+    return true;
+}
+// Shapes.h:684-716 Disk::BasicIntersect
+static inline bool DiskIntersect(const AShape& s, vec3 o, vec3 d, float tMax, ShapeHit* out) {
+    float t0 = (s.h - o.z) / d.z;
+    if (t0 <= 0 || t0 >= tMax) return false;
+    if (d.z == 0) return false;
+    vec3 phit = add(o, mul(d, t0));
+    float dist2 = phit.x * phit.x + phit.y * phit.y;
+    if (dist2 > s.ro * s.ro || dist2 < s.ri * s.ri) return false;
+    *out = {phit, t0};
+    return true;
+}
+// Shapes.h:842-880 TriangleSimple::BasicIntersect (Cramer's rule in object space)
+static inline bool TriSimpleIntersect(const AShape& s, vec3 orig, vec3 dir, float tMax, ShapeHit* out) {
+    float a = s.p1.x - s.p2.x, b = s.p1.y - s.p2.y, c = s.p1.z - s.p2.z;
+    float d = s.p1.x - s.p3.x, e = s.p1.y - s.p3.y, f = s.p1.z - s.p3.z;
+    float g = dir.x, h = dir.y, i = dir.z;
+    float j = s.p1.x - orig.x, k = s.p1.y - orig.y, l = s.p1.z - orig.z;
+    float M = a * (e * i - h * f) + b * (g * f - d * i) + c * (d * h - e * g);
+    float t = -(f * (a * k - j * b) + e * (j * c - a * l) + d * (b * l - k * c)) / M;
+    if (t < 0 || t >= tMax) return false;
+    float Y = (i * (a * k - j * b) + h * (j * c - a * l) + g * (b * l - k * c)) / M;
+    if (Y < 0 || Y > 1) return false;
+    float B = (j * (e * i - h * f) + k * (g * f - d * i) + l * (d * h - e * g)) / M;
+    if (B < 0 || B > 1 - Y) return false;
+    *out = {add(orig, mul(dir, t)), t};
+    return true;
+}
+static inline bool ShapeIntersect(const AShape& s, const Ray& ray, float tMax, ShapeHit* out) {
+    vec3 o, d;
+    ObjRay(s, ray, &o, &d);
+    if (s.type == 0) return SphereIntersect(s, o, d, tMax, out);
+    if (s.type == 1) return DiskIntersect(s, o, d, tMax, out);
+    return TriSimpleIntersect(s, o, d, tMax, out);
+}
+// object-space normal (Shapes.h:417-422 sphere gradient, 744-752 disk +z, 897-901 TriangleSimple)
+static inline vec3 ShapeNormalObj(const AShape& s, vec3 p) {
+    if (s.type == 0) return normalize({2 * p.x, 2 * p.y, 2 * p.z});
+    if (s.type == 1) return {0, 0, 1};
+    return normalize(cross(sub(s.p3, s.p1), sub(s.p2, s.p1)));
+}
+
 // ========================================================================= the integrators
-struct Material { float c[3] = {0, 0, 0}; float emit = 0; };   // sigmoid coeffs + Le = emit * D65
-struct QuadLight { vec3 p, e1, e2, n; float area; int material; };
+// Build-defined materials and lights (Shading.h:1-21, Lights.h:1-10 are stubs) — DESIGN.md §5.
+struct Material { int type = 0; float c[3] = {0, 0, 0}; float emit = 0; float eta = 0; };  // Le = emit * D65
+struct Light {
+    int type = 0;          // 0 quad, 1 disk, 2 point, 3 distant
+    vec3 p{}, e1{}, e2{}, n{}, dir{};
+    float scale = 0, area = 0;
+    int material = -1, shape = -1;
+};
 
 struct Scene {
     Spectra spectra;
+    Piecewise bk7;       // FromInterleaved(GlassBK7_eta, false) (spectrum.cpp:2674-2675)
     TriModel model;
     Octree octree;
     Camera camera;
@@ -832,7 +938,10 @@ struct Scene {
     // path mode (build-defined)
     std::vector<int> tri_material;
     std::vector<Material> materials;
-    std::vector<QuadLight> lights;
+    std::vector<Light> lights;
+    std::vector<AShape> shapes;
+    std::vector<int> light_of_material, light_of_shape;   // area light index of an emitter, or -1
+    bool mis = false;
     int max_depth = 5;
 };
 
@@ -880,57 +989,232 @@ static inline SS LiReference(const Scene& S, const Ray& ray, const SW& w, Sample
     return r;
 }
 
-// Build-defined path integrator (pbrt-v4 SimplePathIntegrator semantics with NEE on quad lights,
-// Lambert R/pi, geometric normals = Shapes.h:1073 fallback, no MIS, no RR).  See DESIGN.md §Path mode.
-static inline SS LiPath(const Scene& S, Ray ray, const SW& w, Sampler& smp, long* counters) {
+// ---- scene queries (build-defined combination): the octree's closest hit first, then every
+// analytic shape in list order with the running tMax and that shape's own acceptance rule.
+struct SceneHit { int kind = 0; int id = -1; TriIsect tri{}; ShapeHit sh{}; };  // kind 0 miss, 1 triangle, 2 shape
+static inline SceneHit Closest(const Scene& S, const Ray& ray, bool use_cull, long* counters) {
+    SceneHit h;
+    Octree::Hit oh = S.octree.Traverse(ray, use_cull);
+    if (counters) { counters[0] += oh.nodes_tested; counters[1] += oh.tris_tested; }
+    float tMax = std::numeric_limits<float>::max();
+    if (oh.tri >= 0) { h.kind = 1; h.id = oh.tri; h.tri = oh.isect; tMax = oh.isect.t; }
+    for (size_t i = 0; i < S.shapes.size(); ++i) {
+        ShapeHit sh;
+        if (ShapeIntersect(S.shapes[i], ray, tMax, &sh)) { h.kind = 2; h.id = (int)i; h.sh = sh; tMax = sh.t; }
+    }
+    if (counters) { counters[2] += (h.kind != 0); counters[3] += 1; }
+    return h;
+}
+static inline bool SceneOccluded(const Scene& S, const Ray& ray, float tMax) {
+    if (S.octree.Occluded(ray, tMax)) return true;
+    for (const AShape& sh : S.shapes) {
+        ShapeHit x;
+        if (ShapeIntersect(sh, ray, tMax, &x)) return true;
+    }
+    return false;
+}
+// Surface at a hit: world point p, world normal n turned against the ray (Shapes.h:1074, 262-263), the
+// front-side normal nout (triangle winding Shapes.h:1073 / shape outward normal) and whether the ray arrives
+// on the front side.
+struct Surf { vec3 p, n, nout; bool front; int material; };
+static inline Surf SurfaceAt(const Scene& S, const SceneHit& h, const Ray& ray) {
+    Surf sf;
+    vec3 rayd = normalize(ray.d);
+    if (h.kind == 1) {
+        const TriModel& m = S.model;
+        vec3 p0 = m.P(h.id, 0), p1 = m.P(h.id, 1), p2 = m.P(h.id, 2);
+        vec3 ng = normalize(cross(sub(p0, p2), sub(p1, p2)));
+        sf.p = add(add(mul(p0, h.tri.b0), mul(p1, h.tri.b1)), mul(p2, h.tri.b2));
+        sf.nout = ng;
+        sf.front = dot(ng, rayd) < 0;
+        sf.n = ng;
+        if (dot(sf.n, rayd) > 0) sf.n = {-ng.x, -ng.y, -ng.z};
+        sf.material = S.tri_material[h.id];
+    } else {
+        const AShape& s = S.shapes[h.id];
+        vec3 o, d;
+        ObjRay(s, ray, &o, &d);
+        vec3 rd = normalize(d);                               // ray_d = glm::normalize(d) (Shapes.h:375)
+        vec3 n = ShapeNormalObj(s, h.sh.phit);
+        bool flip = dot(n, rd) > 0;
+        if (flip) n = {-n.x, -n.y, -n.z};
+        vec3 nw = normalize(mul(s.n2r, n));                   // LocalSurfaceInfo::Transform (Shapes.h:150-151)
+        vec4 pw = mul(s.o2r, vec4{h.sh.phit.x, h.sh.phit.y, h.sh.phit.z, 1});
+        sf.p = {pw.x, pw.y, pw.z};
+        sf.n = nw;
+        sf.front = !flip;
+        sf.nout = flip ? vec3{-nw.x, -nw.y, -nw.z} : nw;
+        sf.material = s.material;
+    }
+    return sf;
+}
+// pbrt-v4 PowerHeuristic(1, f, 1, g)
+static inline float PowerHeuristic(float f, float g) {
+    float f2 = f * f, g2 = g * g;
+    if (std::isinf(f2)) return 1;
+    return f2 / (f2 + g2);
+}
+// pbrt-v4 FrDielectric (smooth dielectric Fresnel reflectance)
+static inline float FrDielectric(float cosTheta_i, float eta) {
+    cosTheta_i = gclamp(cosTheta_i, -1.0f, 1.0f);
+    if (cosTheta_i < 0) { eta = 1 / eta; cosTheta_i = -cosTheta_i; }
+    float sin2Theta_i = 1 - cosTheta_i * cosTheta_i;
+    float sin2Theta_t = sin2Theta_i / (eta * eta);
+    if (sin2Theta_t >= 1) return 1.f;
+    float cosTheta_t = std::sqrt(std::max(0.f, 1 - sin2Theta_t));
+    float r_parl = (eta * cosTheta_i - cosTheta_t) / (eta * cosTheta_i + cosTheta_t);
+    float r_perp = (cosTheta_i - eta * cosTheta_t) / (cosTheta_i + eta * cosTheta_t);
+    return (r_parl * r_parl + r_perp * r_perp) / 2;
+}
+// pbrt-v4 Refract(wi, n, eta, &etap, &wt)
+static inline bool Refract(vec3 wi, vec3 n, float eta, float* etap, vec3* wt) {
+    float cosTheta_i = dot(n, wi);
+    if (cosTheta_i < 0) { eta = 1 / eta; cosTheta_i = -cosTheta_i; n = {-n.x, -n.y, -n.z}; }
+    float sin2Theta_i = std::max(0.f, 1 - cosTheta_i * cosTheta_i);
+    float sin2Theta_t = sin2Theta_i / (eta * eta);
+    if (sin2Theta_t >= 1) return false;
+    float cosTheta_t = std::sqrt(std::max(0.f, 1 - sin2Theta_t));
+    vec3 a = {-wi.x / eta, -wi.y / eta, -wi.z / eta};
+    *wt = add(a, mul(n, cosTheta_i / eta - cosTheta_t));
+    *etap = eta;
+    return true;
+}
+// glm::reflect(I, N) = I - N * dot(N, I) * 2
+static inline vec3 Reflect(vec3 I, vec3 N) { return sub(I, mul(mul(N, dot(N, I)), 2.0f)); }
+// spectrum.h:302-310 SampledWavelengths::TerminateSecondary
+static inline void TerminateSecondary(SW& w) {
+    bool terminated = true;
+    for (int i = 1; i < NSpectrumSamples; ++i) if (w.pdf[i] != 0) terminated = false;
+    if (terminated) return;
+    for (int i = 1; i < NSpectrumSamples; ++i) w.pdf[i] = 0;
+    w.pdf[0] /= NSpectrumSamples;
+}
+
+// Build-defined path integrator (pbrt-v4 PathIntegrator semantics): Lambert R/π, perfect mirror,
+// smooth dielectric (BK7 dispersion → TerminateSecondary); one light sample per light at every diffuse vertex;
+// emitters are one-sided and end the path.  Sample dimensions per vertex: diffuse = one Get2D per light, then
+// Get2D for the cosine direction; mirror = none; dielectric = Get1D.  With `mis` (RT_INTEGRATOR_PATH_MIS) light
+// samples of area lights and BSDF-sampled emitter hits are weighted by the power heuristic; without it emitters
+// count only on camera rays and after specular bounces.
+static inline SS LiPath(const Scene& S, Ray ray, SW& w, Sampler& smp, long* counters) {
     SS L{}, beta;
     for (int i = 0; i < 8; ++i) beta.v[i] = 1.0f;
-    const TriModel& m = S.model;
+    float prevPdf = 0;  // solid-angle pdf of the last diffuse bounce; 0 = camera ray or specular bounce
     for (int depth = 0;; ++depth) {
-        Octree::Hit h = S.octree.Traverse(ray, false);
-        if (counters) { counters[0] += h.nodes_tested; counters[1] += h.tris_tested; counters[2] += (h.tri >= 0); counters[3] += 1; }
-        if (h.tri < 0) break;
-        vec3 p0 = m.P(h.tri, 0), p1 = m.P(h.tri, 1), p2 = m.P(h.tri, 2);
-        vec3 dp02 = sub(p0, p2), dp12 = sub(p1, p2);
-        vec3 ng = normalize(cross(dp02, dp12));
-        vec3 rayd = normalize(ray.d);
-        const Material& mat = S.materials[S.tri_material[h.tri]];
-        if (mat.emit > 0) {  // pure emitter: Le on camera rays only (NEE covers later bounces), one-sided
-            if (depth == 0 && dot(ng, rayd) < 0)
-                for (int i = 0; i < 8; ++i) L.v[i] += beta.v[i] * (mat.emit * S.spectra.D65dense.Query(w.lambda[i]));
+        SceneHit h = Closest(S, ray, false, counters);
+        if (h.kind == 0) break;
+        Surf sf = SurfaceAt(S, h, ray);
+        const Material& mat = S.materials[sf.material];
+        if (mat.emit > 0) {  // pure emitter: one-sided, terminates the path
+            if (sf.front) {
+                if (prevPdf == 0) {
+                    for (int i = 0; i < 8; ++i) L.v[i] += beta.v[i] * (mat.emit * S.spectra.D65dense.Query(w.lambda[i]));
+                } else if (S.mis) {
+                    int li = h.kind == 1 ? S.light_of_material[sf.material] : S.light_of_shape[h.id];
+                    if (li >= 0) {
+                        const Light& Lt = S.lights[li];
+                        vec3 dv = sub(sf.p, ray.o);
+                        float dist2 = dot(dv, dv);
+                        float cl = -dot(Lt.n, normalize(ray.d));
+                        if (cl > 0) {
+                            float wb = PowerHeuristic(prevPdf, dist2 / (cl * Lt.area));
+                            for (int i = 0; i < 8; ++i)
+                                L.v[i] += (beta.v[i] * (mat.emit * S.spectra.D65dense.Query(w.lambda[i]))) * wb;
+                        }
+                    }
+                }
+            }
             break;
         }
         if (depth == S.max_depth) break;
-        vec3 n = ng;
-        if (dot(n, rayd) > 0) n = {-n.x, -n.y, -n.z};
-        vec3 p = add(add(mul(p0, h.isect.b0), mul(p1, h.isect.b1)), mul(p2, h.isect.b2));
+        vec3 n = sf.n, p = sf.p;
+        vec3 rayd = normalize(ray.d);
         float ap = MaxComponentValue({std::fabs(p.x), std::fabs(p.y), std::fabs(p.z)});
         float off = 1e-4f * (1.0f + ap);
-        vec3 po = add(p, mul(n, off));
         float R[8];
         Sigmoid sg{mat.c[0], mat.c[1], mat.c[2]};
         for (int i = 0; i < 8; ++i) R[i] = sg(w.lambda[i]);
-        // --- NEE: one quad light (the first), uniform area sampling
-        vec2 ul = smp.Get2D();
-        if (!S.lights.empty()) {
-            const QuadLight& Lq = S.lights[0];
-            vec3 pl = add(add(Lq.p, mul(Lq.e1, ul.x)), mul(Lq.e2, ul.y));
-            vec3 wv = sub(pl, po);
-            float dist2 = dot(wv, wv);
-            float dist = std::sqrt(dist2);
-            vec3 wi = mul(wv, 1.0f / dist);
-            float cs = dot(n, wi);
-            float cl = -dot(Lq.n, wi);
-            if (counters) counters[4] += 1;
-            if (cs > 0 && cl > 0) {
-                Ray sr{po, wi};
-                if (!S.octree.Occluded(sr, dist * 0.999f)) {
-                    const Material& lm = S.materials[Lq.material];
-                    float G = (cs * cl) / dist2;
-                    float wgt = G * Lq.area;
-                    for (int i = 0; i < 8; ++i) {
-                        float Le = lm.emit * S.spectra.D65dense.Query(w.lambda[i]);
-                        L.v[i] += ((beta.v[i] * (R[i] * InvPi)) * Le) * wgt;
+        if (mat.type == 1) {  // perfect mirror
+            for (int i = 0; i < 8; ++i) beta.v[i] *= R[i];
+            ray = Ray{add(p, mul(n, off)), Reflect(rayd, n)};
+            prevPdf = 0;
+            continue;
+        }
+        if (mat.type == 2) {  // smooth dielectric
+            if (mat.eta == 0) TerminateSecondary(w);
+            float eta = mat.eta != 0 ? mat.eta : S.bk7.Query(w.lambda[0]);
+            float u = smp.Get1D();
+            vec3 wo = {-rayd.x, -rayd.y, -rayd.z};
+            float Fr = FrDielectric(dot(sf.nout, wo), eta);
+            vec3 wt;
+            float etap;
+            if (u < Fr || !Refract(wo, sf.nout, eta, &etap, &wt)) {
+                ray = Ray{add(p, mul(n, off)), Reflect(rayd, n)};
+            } else {
+                for (int i = 0; i < 8; ++i) beta.v[i] /= (etap * etap);
+                ray = Ray{sub(p, mul(n, off)), wt};
+            }
+            prevPdf = 0;
+            continue;
+        }
+        vec3 po = add(p, mul(n, off));
+        // --- NEE: one sample per light, in list order
+        for (size_t li = 0; li < S.lights.size(); ++li) {
+            const Light& Lt = S.lights[li];
+            vec2 ul = smp.Get2D();
+            if (Lt.type <= 1) {  // quad / disk area light, uniform area sampling
+                vec3 pl;
+                if (Lt.type == 0) {
+                    pl = add(add(Lt.p, mul(Lt.e1, ul.x)), mul(Lt.e2, ul.y));
+                } else {  // Sampling.h:383-403 on the object-space disk z = h, then ObjectToRender
+                    const AShape& ds = S.shapes[Lt.shape];
+                    vec2 dk = SampleUniformDiskConcentric(ul);
+                    vec4 pw = mul(ds.o2r, vec4{ds.ro * dk.x, ds.ro * dk.y, ds.h, 1});
+                    pl = {pw.x, pw.y, pw.z};
+                }
+                vec3 wv = sub(pl, po);
+                float dist2 = dot(wv, wv);
+                float dist = std::sqrt(dist2);
+                vec3 wi = mul(wv, 1.0f / dist);
+                float cs = dot(n, wi);
+                float cl = -dot(Lt.n, wi);
+                if (cs > 0 && cl > 0) {
+                    if (counters) counters[4] += 1;
+                    if (!SceneOccluded(S, Ray{po, wi}, dist * 0.999f)) {
+                        const Material& lm = S.materials[Lt.material];
+                        float G = (cs * cl) / dist2;
+                        float wgt = G * Lt.area;
+                        if (S.mis) wgt = wgt * PowerHeuristic(dist2 / (cl * Lt.area), cs * InvPi);
+                        for (int i = 0; i < 8; ++i) {
+                            float Le = lm.emit * S.spectra.D65dense.Query(w.lambda[i]);
+                            L.v[i] += ((beta.v[i] * (R[i] * InvPi)) * Le) * wgt;
+                        }
+                    }
+                }
+            } else {  // point (intensity) / distant (irradiance) light
+                vec3 wi;
+                float tmax, fall;
+                if (Lt.type == 2) {
+                    vec3 wv = sub(Lt.p, po);
+                    float dist2 = dot(wv, wv);
+                    float dist = std::sqrt(dist2);
+                    wi = mul(wv, 1.0f / dist);
+                    tmax = dist * 0.999f;
+                    fall = 1.0f / dist2;
+                } else {
+                    wi = Lt.dir;
+                    tmax = std::numeric_limits<float>::max();
+                    fall = 1.0f;
+                }
+                float cs = dot(n, wi);
+                if (cs > 0) {
+                    if (counters) counters[4] += 1;
+                    if (!SceneOccluded(S, Ray{po, wi}, tmax)) {
+                        float wgt = cs * fall;
+                        for (int i = 0; i < 8; ++i) {
+                            float I = Lt.scale * S.spectra.D65dense.Query(w.lambda[i]);
+                            L.v[i] += ((beta.v[i] * (R[i] * InvPi)) * I) * wgt;
+                        }
                     }
                 }
             }
@@ -946,6 +1230,7 @@ static inline SS LiPath(const Scene& S, Ray ray, const SW& w, Sampler& smp, long
         vec3 t = {b, sign + (n.y * n.y) * a, -n.y};
         vec3 wi = add(add(mul(s, wl.x), mul(t, wl.y)), mul(n, wl.z));
         for (int i = 0; i < 8; ++i) beta.v[i] *= R[i];
+        prevPdf = wl.z * InvPi;  // CosineHemispherePDF
         ray = Ray{po, wi};
     }
     return L;

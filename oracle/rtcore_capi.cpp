@@ -136,6 +136,20 @@ float orc_inner_product_y_d65(void) {
     return InnerProduct(sp.D65, sp.Y);
 }
 float orc_sigmoid_eval(float c0, float c1, float c2, float lambda) { return Sigmoid{c0, c1, c2}(lambda); }
+float orc_fr_dielectric(float cosi, float eta) { return FrDielectric(cosi, eta); }
+int orc_refract(const float* wi, const float* n, float eta, float* wt) {
+    float etap;
+    vec3 o;
+    if (!Refract({wi[0], wi[1], wi[2]}, {n[0], n[1], n[2]}, eta, &etap, &o)) return 0;
+    wt[0] = o.x; wt[1] = o.y; wt[2] = o.z;
+    return 1;
+}
+float orc_bk7_eta(float lambda) {
+    Spectra sp;
+    sp.Init();
+    return sp.FromInterleaved(rtdata::glass_bk7_eta, rtdata::glass_bk7_eta_n, false).Query(lambda);
+}
+float orc_power_heuristic(float f, float g) { return PowerHeuristic(f, g); }
 
 int orc_triangle_intersect(const float* p, const float* ro, const float* rd, float tMax, float* out4) {
     Ray r{{ro[0], ro[1], ro[2]}, {rd[0], rd[1], rd[2]}};
@@ -181,19 +195,47 @@ void* orc_scene_create(const rt_scene_desc* sc, const rt_camera_desc* cam, const
     if (sc->tri_material) S.tri_material.assign(sc->tri_material, sc->tri_material + sc->n_triangles);
     for (int i = 0; i < sc->n_materials; ++i) {
         Material mt;
+        mt.type = sc->materials[i].type;
         for (int k = 0; k < 3; ++k) mt.c[k] = sc->materials[i].sigmoid[k];
         mt.emit = sc->materials[i].emission_scale;
+        mt.eta = sc->materials[i].eta;
         S.materials.push_back(mt);
     }
     if (S.materials.empty()) S.materials.push_back(Material{});
+    S.bk7 = S.spectra.FromInterleaved(rtdata::glass_bk7_eta, rtdata::glass_bk7_eta_n, false);
+    for (int i = 0; i < sc->n_shapes; ++i) {
+        const rt_shape& d = sc->shapes[i];
+        AShape s;
+        s.type = d.type;
+        s.o2r = M4(d.object_to_render); s.r2o = M4(d.render_to_object); s.n2r = M3(d.normal_to_render);
+        s.r = d.radius; s.zmin = gclamp(d.zmin, -d.radius, d.radius); s.zmax = gclamp(d.zmax, -d.radius, d.radius);
+        s.h = d.height; s.ri = d.inner_radius; s.ro = d.outer_radius;
+        s.p1 = {d.p[0], d.p[1], d.p[2]}; s.p2 = {d.p[3], d.p[4], d.p[5]}; s.p3 = {d.p[6], d.p[7], d.p[8]};
+        s.material = d.material;
+        S.shapes.push_back(s);
+    }
+    S.light_of_material.assign(S.materials.size(), -1);
+    S.light_of_shape.assign(S.shapes.size(), -1);
     for (int i = 0; i < sc->n_lights; ++i) {
-        const rt_quad_light& q = sc->lights[i];
-        QuadLight L;
+        const rt_light& q = sc->lights[i];
+        Light L;
+        L.type = q.type;
         L.p = {q.p[0], q.p[1], q.p[2]}; L.e1 = {q.e1[0], q.e1[1], q.e1[2]}; L.e2 = {q.e2[0], q.e2[1], q.e2[2]};
         L.n = {q.n[0], q.n[1], q.n[2]};
-        vec3 cr = cross(L.e1, L.e2);
-        L.area = std::sqrt(dot(cr, cr));
-        L.material = q.material;
+        if (q.type == RT_LIGHT_DISTANT) L.dir = normalize({q.dir[0], q.dir[1], q.dir[2]});
+        L.scale = q.scale; L.material = q.material; L.shape = q.shape;
+        if (q.type == RT_LIGHT_QUAD) {
+            vec3 cr = cross(L.e1, L.e2);
+            L.area = std::sqrt(dot(cr, cr));
+            if (L.material >= 0 && S.light_of_material[L.material] < 0) S.light_of_material[L.material] = i;
+        } else if (q.type == RT_LIGHT_DISK) {
+            const AShape& ds = S.shapes[q.shape];
+            const float phimax = 360.0f * 0.01745329251994329576923690768489f;  // glm::radians(360.f)
+            L.area = phimax * .5f * (ds.ro * ds.ro - ds.ri * ds.ri);           // Disk::Area (Shapes.h:641-644)
+            L.n = normalize(mul(ds.n2r, vec3{0, 0, 1}));
+            L.material = ds.material;
+            S.light_of_shape[q.shape] = i;
+        }
         S.lights.push_back(L);
     }
     S.camera = Camera{M4(cam->raster_to_camera), M4(cam->camera_to_world), cam->lens_radius, cam->focal_distance};
@@ -202,7 +244,8 @@ void* orc_scene_create(const rt_scene_desc* sc, const rt_camera_desc* cam, const
     S.resX = film->res_x; S.resY = film->res_y;
     S.filter.kind = film->filter; S.filter.rx = film->filter_radius[0]; S.filter.ry = film->filter_radius[1];
     S.imagingRatio = film->imaging_ratio;
-    o->path = integ->kind == RT_INTEGRATOR_PATH;
+    o->path = integ->kind == RT_INTEGRATOR_PATH || integ->kind == RT_INTEGRATOR_PATH_MIS;
+    S.mis = integ->kind == RT_INTEGRATOR_PATH_MIS;
     S.max_depth = integ->max_depth;
     for (int k = 0; k < 3; ++k) S.albedo_rgb[k] = integ->albedo_rgb[k];
     o->InitResolve();
@@ -256,11 +299,18 @@ int orc_trace(void* h, int n, const float* ro, const float* rd, int use_cull, in
     auto& S = static_cast<OracleScene*>(h)->S;
     for (int i = 0; i < n; ++i) {
         Ray r{{ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]}, {rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]}};
-        Octree::Hit hh = S.octree.Traverse(r, use_cull != 0);
-        prim[i] = hh.tri;
-        bt[4 * i] = hh.isect.b0; bt[4 * i + 1] = hh.isect.b1; bt[4 * i + 2] = hh.isect.b2; bt[4 * i + 3] = hh.isect.t;
-        if (hh.tri < 0) { bt[4 * i] = bt[4 * i + 1] = bt[4 * i + 2] = bt[4 * i + 3] = 0; }
-        if (counters) { counters[0] += hh.nodes_tested; counters[1] += hh.tris_tested; }
+        long ctr[5] = {0, 0, 0, 0, 0};
+        SceneHit hh = Closest(S, r, use_cull != 0, ctr);   // octree, then analytic shapes (prim = ntri + index)
+        bt[4 * i] = bt[4 * i + 1] = bt[4 * i + 2] = bt[4 * i + 3] = 0;
+        prim[i] = -1;
+        if (hh.kind == 1) {
+            prim[i] = hh.id;
+            bt[4 * i] = hh.tri.b0; bt[4 * i + 1] = hh.tri.b1; bt[4 * i + 2] = hh.tri.b2; bt[4 * i + 3] = hh.tri.t;
+        } else if (hh.kind == 2) {
+            prim[i] = (int)S.model.ntri() + hh.id;
+            bt[4 * i] = hh.sh.phit.x; bt[4 * i + 1] = hh.sh.phit.y; bt[4 * i + 2] = hh.sh.phit.z; bt[4 * i + 3] = hh.sh.t;
+        }
+        if (counters) { counters[0] += ctr[0]; counters[1] += ctr[1]; }
     }
     return 0;
 }

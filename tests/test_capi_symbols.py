@@ -24,13 +24,33 @@ def test_library_exports_every_symbol():
     lib = capi.load_library()
     for s in header_symbols():
         assert hasattr(lib, s), s
-    assert lib.rt_abi_version() == 1
+    assert lib.rt_abi_version() == capi.ABI_VERSION
 
 
-def test_struct_sizes_match_header_layout():
-    assert C.sizeof(capi.rt_pixel) == 16
-    assert C.sizeof(capi.rt_sample_record) == 39 * 4
-    assert C.sizeof(capi.rt_camera_desc) == 4 + 64 + 64 + 8
+STRUCTS = ["rt_options", "rt_pixel", "rt_material", "rt_shape", "rt_light", "rt_scene_desc", "rt_camera_desc",
+           "rt_sampler_desc", "rt_film_desc", "rt_integrator_desc", "rt_stats", "rt_sample_record", "rt_octree_info"]
+
+
+def test_struct_sizes_match_header_layout(tmp_path):
+    """Compile the header with gcc and compare every struct's size and field offsets with the ctypes mirror."""
+    import subprocess
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "rtmi355x.h"', "int main(void) {"]
+    for s in STRUCTS:
+        lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
+        for f, _ in getattr(capi, s)._fields_:
+            cf = "lambda" if f == "lambda_" else f
+            lines.append(f'printf("{s}.{f} %zu\\n", offsetof({s}, {cf}));')
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n") if l)
+    for s in STRUCTS:
+        st = getattr(capi, s)
+        assert int(got[s]) == C.sizeof(st), s
+        for f, _ in st._fields_:
+            assert int(got[f"{s}.{f}"]) == getattr(st, f).offset, f"{s}.{f}"
 
 
 def test_no_device_fails_loudly():
