@@ -480,4 +480,23 @@ RT_DEV bool refract_dir(V3 wi, V3 n, float eta, float& etap, V3& wt) {
 }
 RT_DEV V3 reflect_dir(V3 I, V3 N) { return vsub(I, vmul(vmul(N, vdot(N, I)), 2.0f)); }  // glm::reflect
 
+// Bounds3::IntersectP (Shapes.h:100-124) split at tMax: with F the ternary chain-min of the inflated far planes
+// (NaN axes skipped, as in box_hit) and mn the chain-max of the near planes, the test passes for a given tMax iff
+// mn <= min(tMax, F), i.e. iff box_entry(..) <= tMax (+inf when mn > F: never passes).
+RT_DEV float box_entry(float4 a, float4 b, V3 o, V3 inv) {
+    const float g = 1 + 2 * gamma_n(3);
+    float mn = 0, F = __builtin_inff();
+    float tn, tf, s;
+    tn = (a.x - o.x) * inv.x; tf = (b.x - o.x) * inv.x;
+    if (tn > tf) { s = tn; tn = tf; tf = s; }
+    tf *= g; mn = tn > mn ? tn : mn; F = tf < F ? tf : F;
+    tn = (a.y - o.y) * inv.y; tf = (b.y - o.y) * inv.y;
+    if (tn > tf) { s = tn; tn = tf; tf = s; }
+    tf *= g; mn = tn > mn ? tn : mn; F = tf < F ? tf : F;
+    tn = (a.z - o.z) * inv.z; tf = (b.z - o.z) * inv.z;
+    if (tn > tf) { s = tn; tn = tf; tf = s; }
+    tf *= g; mn = tn > mn ? tn : mn; F = tf < F ? tf : F;
+    return mn > F ? __builtin_inff() : mn;
+}
+
 }  // namespace rtmi

@@ -827,13 +827,19 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
     }
     int qcap = 1;
     if (ob.nodes[0].first_child >= 0) {
-        const int caps[] = {16, 64, 256, 1024};
+        const int caps[] = {16};  // register FIFO; larger bounds use the LDS + HBM-spill FIFO (qcap 0)
         qcap = 0;
         for (int cp : caps)
             if (cp >= bound) { qcap = cp; break; }
         if (!qcap && bound > kRingMax)
             return fail(c, RT_E_LIMIT, "octree BFS frontier bound " + std::to_string(bound) + " exceeds " +
                                            std::to_string(kRingMax) + " groups");
+        // the LDS FIFO stores 16-bit group ids: children are created 8 at a time after the root (node 1 + 8 g)
+        for (int i = 0; i < nn && !qcap; ++i) {
+            int fc = ob.nodes[i].first_child;
+            if (fc >= 0 && ((fc - 1) % 8 != 0 || (fc - 1) / 8 > 65535))
+                return fail(c, RT_E_LIMIT, "octree too large for 16-bit BFS group ids");
+        }
     }
     c->info.n_nodes = nn;
     c->info.n_leaf_refs = (int)c->h_refs.size();

@@ -18,6 +18,12 @@
 namespace rtmi {
 
 static constexpr int kBlock = kBlockThreads;
+#ifndef RT_LEAF_CHUNK
+#define RT_LEAF_CHUNK 16
+#endif
+static constexpr int kLeafChunk = RT_LEAF_CHUNK;  // triangles per leaf phase of the while-while traversal
+static constexpr int kLdsQ = 32;  // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
+__shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by every traversal call site
 
 #ifndef RT_TRI_UNROLL
 #define RT_TRI_UNROLL 4      // triangles per scalar-cache batch in single-leaf traversal
@@ -261,46 +267,109 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         }
         return best;
     }
-    // group FIFO: a private array (registers / scratch) or, for QCAP == 0, a per-thread ring in HBM whose
-    // size is the host's exact worst-case bound (scenes beyond 1024 groups, e.g. the 98k-triangle CFG3)
+    // Group FIFO.  QCAP > 1: a private array (registers) holding the host's exact worst-case bound.
+    // QCAP == 0: the first kLdsQ entries of each lane's FIFO live in LDS as 16-bit group ids (first child =
+    // 8 g + 1); once a push finds them full the lane spills every later push to its HBM ring (sized by the
+    // bound) until the FIFO drains, so pops read LDS for positions below `spill` and HBM from there on.
     constexpr bool GQ = QCAP == 0;
     int q[GQ ? 1 : QCAP];
+    unsigned short* lq = g_lq;
     int* gq = GQ ? sc.ring + (blockIdx.x * blockDim.x + threadIdx.x) : nullptr;
     const int qmask = GQ ? sc.ring_mask : QCAP - 1;
+    int spill = 0x7fffffff;
     int head = 0, tail = 0;
-    int n = 0;       // current node
-    int left = 1;    // nodes left in the current group (root: a group of one)
-    while (true) {
+    bool done = false;
+    int lf = 0, lc = 0;  // pending leaf: first tile, triangle count
+    // The 8 children of a popped group are fetched together (16 independent float4 loads) and reduced to
+    // entry distances E[i] (box_entry: the box test passes for tMax iff E[i] <= tMax); the visit mask is
+    // re-evaluated whenever a leaf has shrunk tMax, so every child is still tested against the tMax the
+    // reference's node-by-node BFS would use at that point.
+    // "while-while" (Aila & Laine 2009): each lane walks its BFS until it reaches a non-empty leaf (or drains),
+    // then the wave tests the pending leaves together.  A lane's own sequence of box and triangle tests — and
+    // the tMax each sees — is unchanged, so results are the reference's bit for bit.
+    int gfirst = 0;          // node index of child 0 of the current group
+    unsigned pm;             // children still to visit whose box passes
+    float E[8];
+    int Ch[8];
+    {
+        float4 a = sc.nodeA[0], b = sc.nodeB[0];  // the root: a group of one
         ++nn;
-        float4 a = sc.nodeA[n];
-        float4 b = sc.nodeB[n];
-        if (box_hit(a, b, o, inv, tMax)) {
-            int child = __float_as_int(a.w);
+        E[0] = box_entry(a, b, o, inv);
+        Ch[0] = __float_as_int(a.w);
+#pragma unroll
+        for (int i = 1; i < 8; ++i) { E[i] = __builtin_inff(); Ch[i] = -1; }
+        pm = E[0] <= tMax ? 1u : 0u;
+    }
+    while (true) {
+        while (!done && lc == 0) {
+            if (pm == 0) {
+                if (head == tail) { done = true; break; }
+                if constexpr (GQ) {
+                    if (head < spill) gfirst = 8 * (int)lq[(head & (kLdsQ - 1)) * kBlock + threadIdx.x] + 1;
+                    else gfirst = gq[(size_t)(head & qmask) * sc.ring_threads];
+                } else {
+                    gfirst = q[head & qmask];
+                }
+                ++head;
+                if (GQ && head == tail) spill = 0x7fffffff;  // drained: LDS again
+                float4 A8[8], B8[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) { A8[i] = sc.nodeA[gfirst + i]; B8[i] = sc.nodeB[gfirst + i]; }
+                nn += 8;
+                pm = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    E[i] = box_entry(A8[i], B8[i], o, inv);
+                    Ch[i] = __float_as_int(A8[i].w);
+                    pm |= (E[i] <= tMax ? 1u : 0u) << i;
+                }
+                continue;
+            }
+            int i = __builtin_ctz(pm);
+            pm &= pm - 1;
+            int child = Ch[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) child = i == k ? Ch[k] : child;
             if (child >= 0) {
-                if constexpr (GQ) gq[(size_t)(tail & qmask) * sc.ring_threads] = child;
-                else q[tail & qmask] = child;
+                if constexpr (GQ) {
+                    if (spill == 0x7fffffff && tail - head < kLdsQ) {
+                        lq[(tail & (kLdsQ - 1)) * kBlock + threadIdx.x] = (unsigned short)((child - 1) >> 3);
+                    } else {
+                        if (spill == 0x7fffffff) spill = tail;
+                        gq[(size_t)(tail & qmask) * sc.ring_threads] = child;
+                    }
+                } else {
+                    q[tail & qmask] = child;
+                }
                 ++tail;
             } else {
-                int2 r = lr[n];
-                for (int k = 0; k < r.y; ++k) {
-                    const float4* tp = tiles + 3 * (r.x + k);
-                    float4 A = tp[0], B = tp[1], Cc = tp[2];
-                    ++nt;
-                    float b0, b1, b2, t;
-                    if (tri_intersect<KZ>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
-                        best = __float_as_int(Cc.y);
-                        if (ANYHIT) return best;
-                        tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
-                    }
-                }
+                int2 r = lr[gfirst + i];
+                lf = r.x;
+                lc = r.y;
             }
         }
-        if (--left > 0) { ++n; continue; }
-        if (head == tail) break;
-        if constexpr (GQ) n = gq[(size_t)(head & qmask) * sc.ring_threads];
-        else n = q[head & qmask];
-        ++head;
-        left = 8;
+        if (lc == 0) break;
+        // at most kLeafChunk triangles per phase: a lane in a big leaf (the CFG3 octree has leaves of up to 583
+        // triangles) keeps the rest pending while the other lanes walk on to their next leaf
+        int m = lc < kLeafChunk ? lc : kLeafChunk;
+        for (int k = 0; k < m; ++k) {
+            const float4* tp = tiles + 3 * (lf + k);
+            float4 A = tp[0], B = tp[1], Cc = tp[2];
+            ++nt;
+            float b0, b1, b2, t;
+            if (tri_intersect<KZ>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                best = __float_as_int(Cc.y);
+                if (ANYHIT) return best;
+                tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+            }
+        }
+        lf += m;
+        lc -= m;
+        if (lc > 0) continue;
+        unsigned keep = 0;  // tMax may have shrunk: the remaining children are tested against the new value
+#pragma unroll
+        for (int k = 0; k < 8; ++k) keep |= (E[k] <= tMax ? 1u : 0u) << k;
+        pm &= keep;
     }
     return best;
 }
@@ -900,9 +969,6 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
         case 0: hipLaunchKernelGGL(k_trace_closest<0>, g, b, 0, st, sc, io, ctr); break;
         case 1: hipLaunchKernelGGL(k_trace_closest<1>, g, b, 0, st, sc, io, ctr); break;
         case 16: hipLaunchKernelGGL(k_trace_closest<16>, g, b, 0, st, sc, io, ctr); break;
-        case 64: hipLaunchKernelGGL(k_trace_closest<64>, g, b, 0, st, sc, io, ctr); break;
-        case 256: hipLaunchKernelGGL(k_trace_closest<256>, g, b, 0, st, sc, io, ctr); break;
-        case 1024: hipLaunchKernelGGL(k_trace_closest<1024>, g, b, 0, st, sc, io, ctr); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -935,9 +1001,6 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
         RT_SHADE_CASE(0)
         RT_SHADE_CASE(1)
         RT_SHADE_CASE(16)
-        RT_SHADE_CASE(64)
-        RT_SHADE_CASE(256)
-        RT_SHADE_CASE(1024)
         default: return hipErrorInvalidValue;
     }
 #undef RT_SHADE_CASE

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 for round in 1 2; do
   for so in computational_ray_tracer_amd/lib/variants/*.so; do
     n=$(basename $so .so)
-    RTMI_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab_$n.log 2>&1
+    RTMI_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_$n.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { echo "$n rc=$rc"; exit $rc; }
     python3 -c "
 import json
