@@ -341,6 +341,39 @@ RT_DEV bool tri_intersect(const TriRay& R, float tMax, float4 A, float4 B, float
     return true;
 }
 
+// The tMax-independent rejections of tri_intersect (same operations, same order): false means the reference
+// test rejects this triangle for every tMax, so a caller may skip it without changing any result.
+template <int KZ>
+RT_DEV bool tri_candidate(const TriRay& R, float4 A, float4 B, float4 Cc) {
+    constexpr int KX = KZ == 0 ? 1 : (KZ == 1 ? 2 : 0), KY = KZ == 0 ? 2 : (KZ == 1 ? 0 : 1);
+    const int kx = KZ >= 0 ? KX : R.kx, ky = KZ >= 0 ? KY : R.ky, kz = KZ >= 0 ? KZ : R.kz;
+    float p0x = sel3(kx, A.x, A.y, A.z) - R.ox, p0y = sel3(ky, A.x, A.y, A.z) - R.oy, p0z = sel3(kz, A.x, A.y, A.z) - R.oz;
+    float p1x = sel3(kx, A.w, B.x, B.y) - R.ox, p1y = sel3(ky, A.w, B.x, B.y) - R.oy, p1z = sel3(kz, A.w, B.x, B.y) - R.oz;
+    float p2x = sel3(kx, B.z, B.w, Cc.x) - R.ox, p2y = sel3(ky, B.z, B.w, Cc.x) - R.oy, p2z = sel3(kz, B.z, B.w, Cc.x) - R.oz;
+    p0x += R.Sx * p0z; p0y += R.Sy * p0z;
+    p1x += R.Sx * p1z; p1y += R.Sy * p1z;
+    p2x += R.Sx * p2z; p2y += R.Sy * p2z;
+    float e0 = dop(p1x, p2y, p1y, p2x);
+    float e1 = dop(p2x, p0y, p2y, p0x);
+    float e2 = dop(p0x, p1y, p0y, p1x);
+    bool zero = (e0 == 0.0f) | (e1 == 0.0f) | (e2 == 0.0f);
+    bool mixed = ((e0 < 0) | (e1 < 0) | (e2 < 0)) & ((e0 > 0) | (e1 > 0) | (e2 > 0));
+    if (!zero & mixed) return false;
+    if (zero) {
+        e0 = (float)((double)p2y * (double)p1x - (double)p2x * (double)p1y);
+        e1 = (float)((double)p0y * (double)p2x - (double)p0x * (double)p2y);
+        e2 = (float)((double)p1y * (double)p0x - (double)p1x * (double)p0y);
+        if (((e0 < 0) | (e1 < 0) | (e2 < 0)) & ((e0 > 0) | (e1 > 0) | (e2 > 0))) return false;
+    }
+    float det = e0 + e1 + e2;
+    if (det == 0) return false;
+    p0z *= R.Sz; p1z *= R.Sz; p2z *= R.Sz;
+    float tScaled = e0 * p0z + e1 * p1z + e2 * p2z;
+    if (det < 0 && tScaled >= 0) return false;
+    if (det > 0 && tScaled <= 0) return false;
+    return true;
+}
+
 // Shapes.h:100-124 Bounds3::IntersectP.  1/d is hoisted (same value as computed per node); the per-axis
 // early return is folded into one final compare (min_t only grows, max_t only shrinks, NaN axes are no-ops).
 RT_DEV bool box_hit(float4 a, float4 b, V3 o, V3 inv, float tMax) {

@@ -28,6 +28,9 @@ __shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by eve
 #ifndef RT_TRI_UNROLL
 #define RT_TRI_UNROLL 4      // triangles per scalar-cache batch in single-leaf traversal
 #endif
+#ifndef RT_TWO_PASS
+#define RT_TWO_PASS 1        // single-leaf scenes: cheap candidate pass over all triangles, full test on survivors
+#endif
 #ifndef RT_KZ_BINS
 #define RT_KZ_BINS 0         // 1: path-mode ray queues split into dominant-axis bins (Cornell A/B: trace -7%, shade +23%)
 #endif
@@ -249,8 +252,43 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 }
                 return false;
             };
-            int k = 0;
             constexpr int U = RT_TRI_UNROLL;
+#if RT_TWO_PASS
+            if (r.y <= 64) {
+                // pass 1: every triangle's tMax-independent rejections (scalar-cache batches); pass 2: the full
+                // test, in leaf order with the running tMax, on the survivors only — so the division and the
+                // error-bound tail run per candidate, not once per triangle for whichever lane reached it
+                uint64_t cand = 0;
+                int k = 0;
+                for (; k + U <= r.y; k += U) {
+                    int e = 3 * (r.x + k);
+                    float4 T[3 * U];
+#pragma unroll
+                    for (int j = 0; j < 3 * U; ++j) T[j] = ldc4(tiles, e + j);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (tri_candidate<KZ>(R, T[3 * u], T[3 * u + 1], T[3 * u + 2])) cand |= 1ull << (k + u);
+                }
+                for (; k < r.y; ++k) {
+                    int e = 3 * (r.x + k);
+                    if (tri_candidate<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2))) cand |= 1ull << k;
+                }
+                nt += r.y;
+                while (cand) {
+                    int j = __builtin_ctzll(cand);
+                    cand &= cand - 1;
+                    const float4* tp = tiles + 3 * (r.x + j);
+                    float b0, b1, b2, t;
+                    if (tri_intersect<KZ>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax) {
+                        best = __float_as_int(tp[2].y);
+                        if (ANYHIT) return best;
+                        tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+                    }
+                }
+                return best;
+            }
+#endif
+            int k = 0;
             for (; k + U <= r.y; k += U) {
                 int e = 3 * (r.x + k);
                 float4 T[3 * U];
@@ -620,7 +658,11 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
         // pending contribution Ld stays live across the traversal.  No shadow queue in HBM.
         if (wantShadow) {
             float b0, b1, b2, t;
+#ifdef RT_PROFILE_NO_SHADOW  // timing experiments only: every shadow ray counts as unoccluded
+            int hit = -1;
+#else
             int hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt);
+#endif
             ++nsh;
             if (hit < 0) {
                 float L[8];
