@@ -17,11 +17,11 @@ STATUS_NAMES = {0: "RT_OK", -1: "RT_E_ARG", -2: "RT_E_HIP", -3: "RT_E_RCCL", -4:
 RT_MAT_DIFFUSE, RT_MAT_MIRROR, RT_MAT_DIELECTRIC = 0, 1, 2
 RT_SHAPE_SPHERE, RT_SHAPE_DISK, RT_SHAPE_TRIANGLE = 0, 1, 2
 RT_LIGHT_QUAD, RT_LIGHT_DISK, RT_LIGHT_POINT, RT_LIGHT_DISTANT = 0, 1, 2, 3
-RT_CAMERA_PERSPECTIVE = 0
+RT_CAMERA_PERSPECTIVE, RT_CAMERA_ORTHOGRAPHIC, RT_CAMERA_PINHOLE, RT_CAMERA_THINLENS = 0, 1, 2, 3
 RT_SAMPLER_INDEPENDENT, RT_SAMPLER_STRATIFIED = 0, 1
-RT_FILTER_BOX, RT_FILTER_TRIANGLE = 0, 1
+RT_FILTER_BOX, RT_FILTER_TRIANGLE, RT_FILTER_GAUSSIAN, RT_FILTER_LANCZOS = 0, 1, 2, 3
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 F16 = C.c_float * 16
 F9 = C.c_float * 9
@@ -69,7 +69,9 @@ class rt_scene_desc(C.Structure):
 
 class rt_camera_desc(C.Structure):
     _fields_ = [("type", C.c_int), ("raster_to_camera", F16), ("camera_to_world", F16),
-                ("lens_radius", C.c_float), ("focal_distance", C.c_float)]
+                ("lens_radius", C.c_float), ("focal_distance", C.c_float), ("raster_to_screen", F16),
+                ("pinhole_depth", C.c_float), ("thin_focal", C.c_float), ("thin_aperture_diameter", C.c_float),
+                ("sensor_depth", C.c_float)]
 
 
 class rt_sampler_desc(C.Structure):
@@ -79,7 +81,7 @@ class rt_sampler_desc(C.Structure):
 
 class rt_film_desc(C.Structure):
     _fields_ = [("res_x", C.c_int), ("res_y", C.c_int), ("filter", C.c_int), ("filter_radius", F2),
-                ("imaging_ratio", C.c_float)]
+                ("imaging_ratio", C.c_float), ("filter_param", C.c_float)]
 
 
 class rt_integrator_desc(C.Structure):

@@ -393,6 +393,23 @@ RT_DEV bool box_hit(float4 a, float4 b, V3 o, V3 inv, float tMax) {
 }
 
 
+// Sampling.h:809-840 Continuous_Inversion_Sampler::Sample: binary search of U in the CDF table, then linear
+// interpolation inside the bin (table built on the host, rt_host.cpp inversion_table).
+RT_DEV float inversion_sample(const float* cdf, int N, float a, float b, float U) {
+    int index = -1, low = 0, high = N;
+    while (low <= high) {
+        int mid = (int)((float)low + (float)(high - low) / 2.0f);
+        if (cdf[mid] < U && U <= cdf[mid + 1]) { index = mid; break; }
+        if (cdf[mid] < U) low = mid + 1;
+        else high = mid - 1;
+    }
+    if (index == -1) return 0;
+    float q = (U - cdf[index]) / (cdf[index + 1] - cdf[index]);
+    float t = q < 0.0f ? 0.0f : (1.f < q ? 1.f : q);
+    float delta_x = (b - a) / (float)N;
+    return (a + delta_x * index) + t * (delta_x * (index + 1) - delta_x * index);
+}
+
 // ---------------------------------------------------------------------- analytic shapes (a21)
 // Restated from Shapes.h like oracle/rtcore.hpp (same op order): the ray goes to object space through
 // RenderToObject, hits come back through LocalSurfaceInfo::Transform (Shapes.h:147-160).  Full spheres and

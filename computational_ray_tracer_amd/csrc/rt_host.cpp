@@ -272,6 +272,8 @@ struct rt_ctx {
     int* d_qcount = nullptr;   // queue q, bin b length at [(3q + b) * kQStride] (separate cache lines)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
+    float* d_cdf = nullptr;    // Gaussian / Lanczos filter tables: x then y, cdf_n + 1 floats each
+    int cdf_n = 0;
     size_t film_cap = 0;
     int grid = 0;              // persistent grid size (blocks)
     // stats
@@ -406,12 +408,65 @@ int build_work(rt_ctx* c) {
     return RT_OK;
 }
 
+// Sampling.h:781-807 Continuous_Inversion_Sampler table (Riemann sum, renormalised, last entry 1) and the
+// filters' 1-D factors (filters.h:101-107 Gaussian with helpers.h:221-225, 228-231 Lanczos with 236-251);
+// powf(v, 2) is written v * v.
+template <class F>
+void inversion_table(F pdf, float a, float b, int N, std::vector<float>& cdf) {
+    cdf.assign(N + 1, 0.0f);
+    float delta_x = (b - a) / (float)N;
+    float sum = 0;
+    for (int n = 1; n < N + 1; n++) {
+        float x = a + delta_x * n;
+        float current_x = x < a ? a : (b < x ? b : x);
+        sum += delta_x * pdf(current_x);
+        cdf[n] = sum;
+    }
+    float scaling_term = 1.0f / cdf[N];
+    for (int n = 1; n < N; n++) cdf[n] *= scaling_term;
+    cdf[N] = 1.0f;
+}
+inline float gaussian_f(float x, float mu, float sigma) {
+    const float Pi = 3.14159265358979323846f;
+    float v = x - mu;
+    return 1.0f / std::sqrt(2 * Pi * sigma * sigma) * std::exp(-(v * v) / (2 * sigma * sigma));
+}
+inline float sinx_over_x(float x) {
+    if (1 - x * x == 1) return 1;
+    return std::sin(x) / x;
+}
+inline float windowed_sinc(float x, float radius, float tau) {
+    const float Pi = 3.14159265358979323846f;
+    if (std::fabs(x) > radius) return 0;
+    return sinx_over_x(Pi * x) * sinx_over_x(Pi * (x / tau));
+}
+int build_filter_tables(const rt_film_desc& d, std::vector<float>& tx, std::vector<float>& ty) {
+    float rx = d.filter_radius[0], ry = d.filter_radius[1];
+    if (d.filter == RT_FILTER_GAUSSIAN) {
+        float sigma = d.filter_param > 0 ? d.filter_param : 0.5f;
+        float ex = gaussian_f(rx, 0, sigma), ey = gaussian_f(ry, 0, sigma);
+        inversion_table([&](float x) { return std::max<float>(0, gaussian_f(x, 0, sigma) - ex); }, -rx, rx, 10000, tx);
+        inversion_table([&](float y) { return std::max<float>(0, gaussian_f(y, 0, sigma) - ey); }, -ry, ry, 10000, ty);
+        return 10000;
+    }
+    float tau = d.filter_param > 0 ? d.filter_param : 3.f;
+    inversion_table([&](float x) { return windowed_sinc(x, rx, tau); }, -rx, rx, 2000, tx);
+    inversion_table([&](float y) { return windowed_sinc(y, ry, tau); }, -ry, ry, 2000, ty);
+    return 2000;
+}
+
 DevCamera dev_camera(const rt_camera_desc& d) {
     DevCamera c;
     std::memcpy(c.r2c, d.raster_to_camera, 64);
     std::memcpy(c.c2w, d.camera_to_world, 64);
     c.lens_radius = d.lens_radius;
     c.focal_distance = d.focal_distance;
+    c.type = d.type;
+    std::memcpy(c.r2s, d.raster_to_screen, 64);
+    c.pinhole_depth = d.pinhole_depth;
+    c.thin_focal = d.thin_focal;
+    c.thin_aperture = d.thin_aperture_diameter;
+    c.sensor_depth = d.sensor_depth;
     return c;
 }
 DevSampler dev_sampler(const rt_sampler_desc& d) {
@@ -420,10 +475,14 @@ DevSampler dev_sampler(const rt_sampler_desc& d) {
     s.spp = d.kind == RT_SAMPLER_INDEPENDENT ? d.x_samples : d.x_samples * d.y_samples;
     return s;
 }
-DevFilm dev_film(const rt_film_desc& d) {
+DevFilm dev_film(const rt_ctx* c) {
+    const rt_film_desc& d = c->film;
     DevFilm f;
     f.res_x = d.res_x; f.res_y = d.res_y; f.filter = d.filter;
     f.rx = d.filter_radius[0]; f.ry = d.filter_radius[1]; f.imaging_ratio = d.imaging_ratio;
+    f.cdf_x = c->d_cdf;
+    f.cdf_y = c->d_cdf ? c->d_cdf + (c->cdf_n + 1) : nullptr;
+    f.cdf_n = c->cdf_n;
     return f;
 }
 
@@ -463,7 +522,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     size_t nmax = (size_t)B * c->n_work;
     if ((rc = ensure_workspace(c, nmax, path))) return rc;
     DevCamera cam = dev_camera(c->cam);
-    DevFilm fd = dev_film(c->film);
+    DevFilm fd = dev_film(c);
     for (int b0 = ib; b0 < ie; b0 += B) {
         int nIdx = std::min(B, ie - b0);
         int nS = nIdx * c->n_work;
@@ -635,7 +694,7 @@ void rt_destroy(rt_ctx* c) {
     for (hipEvent_t e : c->pool) hipEventDestroy(e);
     free_scene(c);
     free_workspace(c);
-    void* ptrs[] = {c->d_spec, c->d_qcount, c->d_ctr, c->d_resolve, c->d_work, c->d_film};
+    void* ptrs[] = {c->d_spec, c->d_qcount, c->d_ctr, c->d_resolve, c->d_work, c->d_film, c->d_cdf};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -956,7 +1015,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
 
 int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
     if (!c || !d) return RT_E_ARG;
-    if (d->type != RT_CAMERA_PERSPECTIVE) return fail(c, RT_E_ARG, "only the PerspectiveCamera is supported");
+    if (d->type < RT_CAMERA_PERSPECTIVE || d->type > RT_CAMERA_THINLENS) return fail(c, RT_E_ARG, "unknown camera type");
     c->cam = *d;
     c->have_cam = true;
     return RT_OK;
@@ -974,9 +1033,20 @@ int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
 
 int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
     if (!c || !d) return RT_E_ARG;
-    if (d->res_x <= 0 || d->res_y <= 0 || (d->filter != RT_FILTER_BOX && d->filter != RT_FILTER_TRIANGLE))
+    if (d->res_x <= 0 || d->res_y <= 0 || d->filter < RT_FILTER_BOX || d->filter > RT_FILTER_LANCZOS)
         return fail(c, RT_E_ARG, "invalid film");
     if ((size_t)d->res_x * d->res_y > ((size_t)1 << 27)) return fail(c, RT_E_LIMIT, "film too large");
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);  // queued passes may still read the old tables
+    if (c->d_cdf) { hipFree(c->d_cdf); c->d_cdf = nullptr; c->cdf_n = 0; }
+    if (d->filter == RT_FILTER_GAUSSIAN || d->filter == RT_FILTER_LANCZOS) {
+        std::vector<float> tx, ty;
+        int n = build_filter_tables(*d, tx, ty);
+        if (hipMalloc(&c->d_cdf, sizeof(float) * 2 * (n + 1)) != hipSuccess) return fail(c, RT_E_OOM, "filter tables");
+        hipMemcpy(c->d_cdf, tx.data(), sizeof(float) * (n + 1), hipMemcpyHostToDevice);
+        hipMemcpy(c->d_cdf + (n + 1), ty.data(), sizeof(float) * (n + 1), hipMemcpyHostToDevice);
+        c->cdf_n = n;
+    }
     c->film = *d;
     c->have_film = true;
     c->work_dirty = true;
@@ -1158,7 +1228,7 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
         SampleIds ids{nullptr, 1, 0, dp, di};
         GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB, nullptr, nullptr, nullptr,
                   nullptr, nullptr, nullptr, nullptr};
-        DevFilm fd = dev_film(c->film);
+        DevFilm fd = dev_film(c);
         TraceIO tio{c->rayO, c->rayD, nullptr, n, 0, c->cull ? 1 : 0, c->hitB, c->hitPrim};
         ShadeRefIO sio = shade_ref_io(c);
         sio.rayD = c->rayD; sio.lamA = c->lamA; sio.lamB = c->lamB; sio.pdfA = c->pdfA; sio.pdfB = c->pdfB;

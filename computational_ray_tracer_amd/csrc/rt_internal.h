@@ -29,6 +29,9 @@ struct DevSpectra {                 // Spectra::Init products (spectrum.cpp:2612
 struct DevCamera {
     float r2c[16], c2w[16];         // column-major
     float lens_radius, focal_distance;
+    int type;                       // RT_CAMERA_*
+    float r2s[16];                  // M_RastertoScreen (pinhole / thin lens)
+    float pinhole_depth, thin_focal, thin_aperture, sensor_depth;
 };
 
 struct DevSampler {
@@ -38,6 +41,9 @@ struct DevSampler {
 struct DevFilm {
     int res_x, res_y, filter;
     float rx, ry, imaging_ratio;
+    const float* cdf_x;             // Gaussian / Lanczos: Continuous_Inversion_Sampler tables (N + 1 floats each)
+    const float* cdf_y;
+    int cdf_n;
 };
 
 struct DevLight {                   // rt_light (build-defined)

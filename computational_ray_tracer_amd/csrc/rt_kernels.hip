@@ -159,21 +159,54 @@ __global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevC
         sm.get2d(smp, u0, u1);
         float fx, fy;
         if (film.filter == 0) { fx = lerpf_(u0, -film.rx, film.rx); fy = lerpf_(u1, -film.ry, film.ry); }
-        else { fx = sample_tent(u0, film.rx); fy = sample_tent(u1, film.ry); }
+        else if (film.filter == 1) { fx = sample_tent(u0, film.rx); fy = sample_tent(u1, film.ry); }
+        else {  // Gaussian / Lanczos: tabulated inversion (filters.h:128-134, 239-245), weight f/pdf = 1
+            fx = inversion_sample(film.cdf_x, film.cdf_n, -film.rx, film.rx, u0);
+            fy = inversion_sample(film.cdf_y, film.cdf_n, -film.ry, film.ry, u1);
+        }
         float posx = ((float)x + .5f) + fx, posy = ((float)y + .5f) + fy;
-        float np[4];
-        mat4_mul(cam.r2c, posx, posy, 0.f, 1.f, np);
-        V3 d = vnorm(v3(np[0] / np[3], np[1] / np[3], np[2] / np[3]));
-        V3 o = v3(0, 0, 0);
-        if (cam.lens_radius > 0) {
-            float a0, a1, dx, dy;
-            sm.get2d(smp, a0, a1);
-            disk_concentric(a0, a1, dx, dy);
-            float lx = cam.lens_radius * dx, ly = cam.lens_radius * dy;
-            float ft = cam.focal_distance / d.z;
-            V3 pf = vadd(o, vmul(d, ft));
-            o = v3(lx, ly, 0);
-            d = vnorm(vsub(pf, o));
+        V3 d, o;
+        if (cam.type == 0) {  // PerspectiveCamera (Cameras.h:273-297)
+            float np[4];
+            mat4_mul(cam.r2c, posx, posy, 0.f, 1.f, np);
+            d = vnorm(v3(np[0] / np[3], np[1] / np[3], np[2] / np[3]));
+            o = v3(0, 0, 0);
+            if (cam.lens_radius > 0) {
+                float a0, a1, dx, dy;
+                sm.get2d(smp, a0, a1);
+                disk_concentric(a0, a1, dx, dy);
+                float lx = cam.lens_radius * dx, ly = cam.lens_radius * dy;
+                float ft = cam.focal_distance / d.z;
+                V3 pf = vadd(o, vmul(d, ft));
+                o = v3(lx, ly, 0);
+                d = vnorm(vsub(pf, o));
+            }
+        } else if (cam.type == 1) {  // OrthographicCamera (Cameras.h:230-243)
+            float cp[4];
+            mat4_mul(cam.r2c, posx, posy, 0.f, 1.f, cp);
+            o = v3(cp[0], cp[1], cp[2]);
+            d = v3(0, 0, 1);
+        } else {
+            float s4[4];
+            mat4_mul(cam.r2s, posx, posy, 0.f, 1.f, s4);
+            V3 sp = v3(s4[0], s4[1], s4[2]);
+            if (cam.type == 2) {  // PinholeCamera (Cameras.h:328-339): through the hole's centre
+                o = sp;
+                d = vnorm(vsub(v3(0.0f, 0.0f, cam.pinhole_depth), sp));
+            } else {  // ThinlensCamera (Cameras.h:378-400), (lens_angle, len_percent_r) = (360 u0, u1)
+                float a0, a1;
+                sm.get2d(smp, a0, a1);
+                float ang = (a0 * 360.0f) * 0.01745329251994329576923690768489f;
+                float sn, cs;
+                sincos_det(ang, sn, cs);
+                float half = cam.thin_aperture / 2.0f;
+                o = v3(a1 * half * cs, a1 * half * sn, cam.sensor_depth);
+                V3 lc = v3(0, 0, cam.sensor_depth);
+                V3 tmp = vnorm(vsub(lc, sp));
+                float t = cam.thin_focal / tmp.z;
+                V3 fpos = vadd(lc, vmul(tmp, t));
+                d = vnorm(vsub(fpos, o));
+            }
         }
         float wo[4], wd[4];
         mat4_mul(cam.c2w, o.x, o.y, o.z, 1.f, wo);

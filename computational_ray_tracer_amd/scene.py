@@ -55,6 +55,93 @@ def colmajor(m):
 # ----------------------------------------------------------------------------------------- camera
 
 
+def _camera_base(sw, sh, res, position, look, worldup):
+    """CameraBase (Cameras.h:80-142): M_RastertoScreen and M_CameratoWorld, float64."""
+    rx, ry = res
+    screen_to_ndc = scale((1 / sw, 1 / sh, 1)) @ translate((sw / 2, sh / 2, 0))   # Cameras.h:88-89
+    ndc_to_raster = scale((rx, -ry, 1)) @ translate((0, -1, 0))                   # Cameras.h:90-91
+    raster_to_screen = np.linalg.inv(ndc_to_raster @ screen_to_ndc)                # Cameras.h:93-94
+    d = np.asarray(look, float)
+    d = d / np.linalg.norm(d)
+    r = np.cross(np.asarray(worldup, float), d)
+    r = r / np.linalg.norm(r)
+    u = np.cross(d, r)                                                             # Cameras.h:130-139
+    cam_to_world = np.eye(4)
+    cam_to_world[:3, 0], cam_to_world[:3, 1], cam_to_world[:3, 2] = r, u, d
+    cam_to_world[:3, 3] = position
+    return raster_to_screen, cam_to_world
+
+
+def _camera_desc(kind, r2c, c2w, r2s=None, **kw):
+    d = capi.rt_camera_desc()
+    d.type = kind
+    d.raster_to_camera[:] = colmajor(r2c).tolist()
+    d.camera_to_world[:] = colmajor(c2w).tolist()
+    d.raster_to_screen[:] = colmajor(r2s if r2s is not None else np.eye(4)).tolist()
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+@dataclass
+class OrthographicCamera:
+    """OrthographicCamera(near, far, sensor_w, sensor_h, pos, look, right, worldup, res) (Cameras.h:213-245)."""
+    near: float = 1e-2
+    far: float = 1000.0
+    sensor: tuple = (500.0, 500.0)
+    position: tuple = (0.0, 0.0, 0.0)
+    look: tuple = (0.0, 0.0, 1.0)
+    right: tuple = (1.0, 0.0, 0.0)
+    worldup: tuple = (0.0, 1.0, 0.0)
+    res: tuple = (500, 500)
+
+    def desc(self):
+        r2s, c2w = _camera_base(self.sensor[0], self.sensor[1], self.res, self.position, self.look, self.worldup)
+        c2s = scale((1, 1, 1.0 / (self.far - self.near))) @ translate((0, 0, -self.near))   # Cameras.h:222-223
+        return _camera_desc(capi.RT_CAMERA_ORTHOGRAPHIC, np.linalg.inv(c2s) @ r2s, c2w, r2s)
+
+
+@dataclass
+class PinholeCamera:
+    """PinholeCamera(radius, box_dimensions, pos, look, right, worldup, res) (Cameras.h:313-359); the sampler
+    overload of generateRay aims every ray at the hole's centre (0, 0, box_dimensions.z)."""
+    radius: float = 1.0
+    box: tuple = (36.0, 24.0, 50.0)
+    position: tuple = (0.0, 0.0, 0.0)
+    look: tuple = (0.0, 0.0, 1.0)
+    right: tuple = (1.0, 0.0, 0.0)
+    worldup: tuple = (0.0, 1.0, 0.0)
+    res: tuple = (500, 500)
+
+    def desc(self):
+        r2s, c2w = _camera_base(self.box[0], self.box[1], self.res, self.position, self.look, self.worldup)
+        return _camera_desc(capi.RT_CAMERA_PINHOLE, np.eye(4), c2w, r2s, pinhole_depth=float(self.box[2]))
+
+
+@dataclass
+class ThinlensCamera:
+    """ThinlensCamera(R_curvature, lens_d, apeture, sensor_depth, sensor_w, sensor_h, pos, look, right, worldup,
+    res) (Cameras.h:362-409): focal point F = R/2, aperture diameter lens_d - apeture."""
+    curvature_radius: float = 100.0
+    lens_diameter: float = 20.0
+    aperture: float = 5.0
+    sensor_depth: float = 60.0
+    sensor: tuple = (36.0, 24.0)
+    position: tuple = (0.0, 0.0, 0.0)
+    look: tuple = (0.0, 0.0, 1.0)
+    right: tuple = (1.0, 0.0, 0.0)
+    worldup: tuple = (0.0, 1.0, 0.0)
+    res: tuple = (500, 500)
+
+    def desc(self):
+        r2s, c2w = _camera_base(self.sensor[0], self.sensor[1], self.res, self.position, self.look, self.worldup)
+        f32 = np.float32
+        return _camera_desc(capi.RT_CAMERA_THINLENS, np.eye(4), c2w, r2s,
+                            thin_focal=float(f32(self.curvature_radius) / f32(2.0)),
+                            thin_aperture_diameter=float(f32(self.lens_diameter) - f32(self.aperture)),
+                            sensor_depth=float(self.sensor_depth))
+
+
 @dataclass
 class PerspectiveCamera:
     """PerspectiveCamera(near, far, sensor_w, sensor_h, fov, pos, look, right, worldup, res, lens, focal)
@@ -97,13 +184,8 @@ class PerspectiveCamera:
 
     def desc(self):
         r2c, c2w = self.matrices()
-        d = capi.rt_camera_desc()
-        d.type = capi.RT_CAMERA_PERSPECTIVE
-        d.raster_to_camera[:] = colmajor(r2c).tolist()
-        d.camera_to_world[:] = colmajor(c2w).tolist()
-        d.lens_radius = self.lens_radius
-        d.focal_distance = self.focal_distance
-        return d
+        return _camera_desc(capi.RT_CAMERA_PERSPECTIVE, r2c, c2w, lens_radius=self.lens_radius,
+                            focal_distance=self.focal_distance)
 
 
 # ------------------------------------------------------------------------------- sampler / film
@@ -145,6 +227,7 @@ class Film:
     filter: int = capi.RT_FILTER_BOX
     filter_radius: tuple = (0.5, 0.5)
     imaging_ratio: float = float(np.float32(1.0) / np.float32(106.856895))
+    filter_param: float = 0.0        # Gaussian sigma / Lanczos tau (0: the reference defaults 0.5 / 3)
 
     def desc(self):
         d = capi.rt_film_desc()
@@ -152,6 +235,7 @@ class Film:
         d.filter = self.filter
         d.filter_radius[:] = list(self.filter_radius)
         d.imaging_ratio = self.imaging_ratio
+        d.filter_param = self.filter_param
         return d
 
     def new_pixels(self):

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 typedef enum {
     RT_OK = 0,
@@ -111,14 +111,25 @@ typedef struct {
     const rt_shape* shapes;
 } rt_scene_desc;
 
-enum { RT_CAMERA_PERSPECTIVE = 0 };
-/* The values CameraBase already holds (Cameras.h:190-210); generateRay = Cameras.h:273-297. */
+enum { RT_CAMERA_PERSPECTIVE = 0, RT_CAMERA_ORTHOGRAPHIC = 1, RT_CAMERA_PINHOLE = 2, RT_CAMERA_THINLENS = 3 };
+/* The values CameraBase and its subclasses already hold (Cameras.h:190-210 and the members below).
+ * PERSPECTIVE: generateRay Cameras.h:273-297 (raster_to_camera, lens_radius, focal_distance);
+ * ORTHOGRAPHIC: Cameras.h:230-243 (raster_to_camera);
+ * PINHOLE: Cameras.h:328-339, the sampler overload (raster_to_screen, pinhole_depth = box_dimensions.z);
+ * THINLENS: Cameras.h:378-400 (raster_to_screen, thin_focal = R/2, thin_aperture_diameter = lens_d - apeture,
+ *   sensor_depth); the reference only offers a (lens_angle, len_percent_r) overload, so the build draws one
+ *   Get2D per sample: lens_angle = 360° · u0, len_percent_r = u1. */
 typedef struct {
     int type;
     float raster_to_camera[16];      /* column-major M_RastertoCamera */
     float camera_to_world[16];       /* column-major M_CameratoWorld  */
     float lens_radius;
     float focal_distance;
+    float raster_to_screen[16];      /* column-major M_RastertoScreen (Cameras.h:93-94) */
+    float pinhole_depth;
+    float thin_focal;
+    float thin_aperture_diameter;
+    float sensor_depth;
 } rt_camera_desc;
 
 enum { RT_SAMPLER_INDEPENDENT = 0, RT_SAMPLER_STRATIFIED = 1 };
@@ -131,14 +142,17 @@ typedef struct {
     int seed;
 } rt_sampler_desc;
 
-enum { RT_FILTER_BOX = 0, RT_FILTER_TRIANGLE = 1 };
-/* Film (Film.h:11-20) + its filter (filters.h:66-93 Box, 267-296 Triangle with a deterministic coin)
- * + XYZ PixelSensor (pixelsensor.h:70-87). */
+enum { RT_FILTER_BOX = 0, RT_FILTER_TRIANGLE = 1, RT_FILTER_GAUSSIAN = 2, RT_FILTER_LANCZOS = 3 };
+/* Film (Film.h:11-20) + its filter + XYZ PixelSensor (pixelsensor.h:70-87).  Filters: Box (filters.h:66-93),
+ * Triangle (267-296, deterministic coin), Gaussian (96-154, sigma = filter_param) and LanczosSinc (223-264,
+ * tau = filter_param), the last two sampled through the reference's tabulated Continuous_Inversion_Sampler
+ * (Sampling.h:781-877; 10000 / 2000 bins) driven by the sampler's GetPixel2D. */
 typedef struct {
     int res_x, res_y;
     int filter;
     float filter_radius[2];
     float imaging_ratio;             /* 1/CIE_Y_integral in the reference app (RayTracerTestApp.h:149) */
+    float filter_param;              /* Gaussian sigma (0 -> 0.5) / Lanczos tau (0 -> 3)               */
 } rt_film_desc;
 
 enum { RT_INTEGRATOR_REFERENCE = 0, RT_INTEGRATOR_PATH = 1, RT_INTEGRATOR_PATH_MIS = 2 };

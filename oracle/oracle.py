@@ -58,6 +58,7 @@ def lib():
             "orc_bounds_intersect": ([P(C.c_float), P(C.c_float), P(C.c_float), C.c_float], C.c_int),
             "orc_camera_ray": ([P(capi.rt_camera_desc), P(capi.rt_sampler_desc), C.c_int, C.c_int, C.c_int, C.c_float,
                                 C.c_float, P(C.c_float), P(C.c_float)], None),
+            "orc_filter_sample": ([P(capi.rt_film_desc), C.c_float, C.c_float, P(C.c_float)], None),
             "orc_scene_create": ([P(capi.rt_scene_desc), P(capi.rt_camera_desc), P(capi.rt_sampler_desc),
                                   P(capi.rt_film_desc), P(capi.rt_integrator_desc)], C.c_void_p),
             "orc_scene_destroy": ([C.c_void_p], None),

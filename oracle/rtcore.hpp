@@ -786,7 +786,35 @@ struct Octree {
 struct Camera {
     mat4 rasterToCamera, cameraToWorld;
     float lensRadius = 0, focalDistance = 0;
+    int type = 0;                       // 0 perspective, 1 orthographic, 2 pinhole, 3 thin lens
+    mat4 rasterToScreen{};
+    float pinholeDepth = 0, thinF = 0, thinAperture = 0, sensorDepth = 0;
     Ray generateRay(vec2 pixel, Sampler* sampler) const {
+        if (type == 1) {  // Cameras.h:230-243 OrthographicCamera::generateRay
+            vec4 cp = mul(rasterToCamera, vec4{pixel.x, pixel.y, 0, 1});
+            return TransformRay(Ray{{cp.x, cp.y, cp.z}, {0, 0, 1}}, cameraToWorld);
+        }
+        if (type == 2) {  // Cameras.h:328-339 PinholeCamera::generateRay(pixel, sampler): the hole's centre
+            vec4 s4 = mul(rasterToScreen, vec4{pixel.x, pixel.y, 0, 1});
+            vec3 sp = {s4.x, s4.y, s4.z};
+            vec3 pin = {0.0f, 0.0f, pinholeDepth};
+            return TransformRay(Ray{sp, normalize(sub(pin, sp))}, cameraToWorld);
+        }
+        if (type == 3) {  // Cameras.h:378-400 ThinlensCamera, (lens_angle, len_percent_r) = (360 u0, u1)
+            vec2 u = sampler ? sampler->Get2D() : vec2{0, 0};
+            float lens_angle = u.x * 360.0f;
+            float len_percent_r = u.y;
+            vec4 s4 = mul(rasterToScreen, vec4{pixel.x, pixel.y, 0, 1});
+            vec3 sp = {s4.x, s4.y, s4.z};
+            float ang = lens_angle * 0.01745329251994329576923690768489f;  // glm::radians
+            float half = thinAperture / 2.0f;
+            vec3 lens_pos = {len_percent_r * half * cos_f(ang), len_percent_r * half * sin_f(ang), sensorDepth};
+            vec3 lens_center = {0, 0, sensorDepth};
+            vec3 tmp = normalize(sub(lens_center, sp));
+            float t = thinF / tmp.z;
+            vec3 fpos = add(lens_center, mul(tmp, t));
+            return TransformRay(Ray{lens_pos, normalize(sub(fpos, lens_pos))}, cameraToWorld);
+        }
         vec4 np = mul(rasterToCamera, vec4{pixel.x, pixel.y, 0, 1});
         vec3 near_pos = {np.x / np.w, np.y / np.w, np.z / np.w};
         Ray ray{{0, 0, 0}, normalize(near_pos)};
@@ -804,13 +832,78 @@ struct Camera {
 
 // ----------------------------------------------------------------------------- filters
 // filters.h:66-93 BoxFilter::Sample ; filters.h:285-290 TriangleFilter::Sample (deterministic coin)
+// Sampling.h:781-877 Continuous_Inversion_Sampler: Riemann-sum CDF over N bins of [a, b], renormalised, then a
+// binary search + linear interpolation (the reference draws U itself; here U is the sample's GetPixel2D value).
+struct InversionTable {
+    int N = 0;
+    float a = 0, b = 0;
+    std::vector<float> cdf;
+    template <class F>
+    void Build(F pdf, float a_, float b_, int N_) {
+        a = a_; b = b_; N = N_;
+        cdf.assign(N + 1, 0.0f);
+        float delta_x = (b - a) / (float)N;
+        float sum = 0;
+        for (int n = 1; n < N + 1; n++) {
+            float x = a + delta_x * n;
+            float current_x = x < a ? a : (b < x ? b : x);  // std::clamp
+            sum += delta_x * pdf(current_x);
+            cdf[n] = sum;
+        }
+        float scaling_term = 1.0f / cdf[N];
+        for (int n = 1; n < N; n++) cdf[n] *= scaling_term;
+        cdf[N] = 1.0f;
+    }
+    float Sample(float U) const {
+        int index = -1, low = 0, high = N;
+        while (low <= high) {
+            int mid = (int)((float)low + (float)(high - low) / 2.0f);
+            if (cdf[mid] < U && U <= cdf[mid + 1]) { index = mid; break; }
+            if (cdf[mid] < U) low = mid + 1;
+            else high = mid - 1;
+        }
+        if (index == -1) return 0;
+        float q = (U - cdf[index]) / (cdf[index + 1] - cdf[index]);
+        float t = q < 0.0f ? 0.0f : (1.f < q ? 1.f : q);
+        float delta_x = (b - a) / (float)N;
+        return (a + delta_x * index) + t * (delta_x * (index + 1) - delta_x * index);
+    }
+};
+// helpers.h:221-251 Gaussian / SinXOverX / Sinc / WindowedSinc (powf(v, 2) written v * v)
+static inline float GaussianF(float x, float mu, float sigma) {
+    float v = x - mu;
+    return 1.0f / std::sqrt(2 * Pi * sigma * sigma) * std::exp(-(v * v) / (2 * sigma * sigma));
+}
+static inline float SinXOverX(float x) {
+    if (1 - x * x == 1) return 1;
+    return std::sin(x) / x;
+}
+static inline float WindowedSinc(float x, float radius, float tau) {
+    if (std::fabs(x) > radius) return 0;
+    return SinXOverX(Pi * x) * SinXOverX(Pi * (x / tau));
+}
 struct Filter {
-    int kind = 0;  // 0 box, 1 triangle
+    int kind = 0;  // 0 box, 1 triangle, 2 gaussian, 3 lanczos sinc
     float rx = 0.5f, ry = 0.5f;
+    InversionTable tx, ty;
+    void Init(float param) {  // filters.h:101-107 (Gaussian, N 10000) / 228-231 (Lanczos, N 2000)
+        if (kind == 2) {
+            float sigma = param > 0 ? param : 0.5f;
+            float expX = GaussianF(rx, 0, sigma), expY = GaussianF(ry, 0, sigma);
+            tx.Build([&](float x) { return std::max<float>(0, GaussianF(x, 0, sigma) - expX); }, -rx, rx, 10000);
+            ty.Build([&](float y) { return std::max<float>(0, GaussianF(y, 0, sigma) - expY); }, -ry, ry, 10000);
+        } else if (kind == 3) {
+            float tau = param > 0 ? param : 3.f;
+            tx.Build([&](float x) { return WindowedSinc(x, rx, tau); }, -rx, rx, 2000);
+            ty.Build([&](float y) { return WindowedSinc(y, ry, tau); }, -ry, ry, 2000);
+        }
+    }
+    // FilterSample weight f(p)/(pdf_x pdf_y) with pdf = the filter's own 1-D factors: 1
     vec2 Sample(vec2 u, float* weight) const {
         *weight = 1.0f;
         if (kind == 0) return {Lerp(u.x, -rx, rx), Lerp(u.y, -ry, ry)};
-        return {SampleTentDet(u.x, rx), SampleTentDet(u.y, ry)};
+        if (kind == 1) return {SampleTentDet(u.x, rx), SampleTentDet(u.y, ry)};
+        return {tx.Sample(u.x), ty.Sample(u.y)};
     }
 };
 

@@ -164,14 +164,33 @@ int orc_tribox_overlap(const float* c, const float* h, const float* p) {
 int orc_bounds_intersect(const float* b, const float* ro, const float* rd, float tMax) {
     return IntersectP(Bounds3{{b[0], b[1], b[2]}, {b[3], b[4], b[5]}}, Ray{{ro[0], ro[1], ro[2]}, {rd[0], rd[1], rd[2]}}, tMax) ? 1 : 0;
 }
+static Camera MakeCamera(const rt_camera_desc* c) {
+    Camera cam{M4(c->raster_to_camera), M4(c->camera_to_world), c->lens_radius, c->focal_distance};
+    cam.type = c->type;
+    cam.rasterToScreen = M4(c->raster_to_screen);
+    cam.pinholeDepth = c->pinhole_depth;
+    cam.thinF = c->thin_focal;
+    cam.thinAperture = c->thin_aperture_diameter;
+    cam.sensorDepth = c->sensor_depth;
+    return cam;
+}
 void orc_camera_ray(const rt_camera_desc* c, const rt_sampler_desc* sd, int px, int py, int index, float fx, float fy,
                     float* ro, float* rd) {
-    Camera cam{M4(c->raster_to_camera), M4(c->camera_to_world), c->lens_radius, c->focal_distance};
+    Camera cam = MakeCamera(c);
     Sampler s;
     s.kind = sd->kind; s.xPixelSamples = sd->x_samples; s.yPixelSamples = sd->y_samples; s.jitter = sd->jitter != 0; s.seed = sd->seed;
     s.StartPixelSample(px, py, index, 3);
     Ray r = cam.generateRay({fx, fy}, &s);
     ro[0] = r.o.x; ro[1] = r.o.y; ro[2] = r.o.z; rd[0] = r.d.x; rd[1] = r.d.y; rd[2] = r.d.z;
+}
+
+void orc_filter_sample(const rt_film_desc* fd, float u0, float u1, float* out) {
+    Filter f;
+    f.kind = fd->filter; f.rx = fd->filter_radius[0]; f.ry = fd->filter_radius[1];
+    f.Init(fd->filter_param);
+    float w;
+    vec2 p = f.Sample({u0, u1}, &w);
+    out[0] = p.x; out[1] = p.y; out[2] = w;
 }
 
 void* orc_scene_create(const rt_scene_desc* sc, const rt_camera_desc* cam, const rt_sampler_desc* smp,
@@ -238,11 +257,12 @@ void* orc_scene_create(const rt_scene_desc* sc, const rt_camera_desc* cam, const
         }
         S.lights.push_back(L);
     }
-    S.camera = Camera{M4(cam->raster_to_camera), M4(cam->camera_to_world), cam->lens_radius, cam->focal_distance};
+    S.camera = MakeCamera(cam);
     S.sampler.kind = smp->kind; S.sampler.xPixelSamples = smp->x_samples; S.sampler.yPixelSamples = smp->y_samples;
     S.sampler.jitter = smp->jitter != 0; S.sampler.seed = smp->seed;
     S.resX = film->res_x; S.resY = film->res_y;
     S.filter.kind = film->filter; S.filter.rx = film->filter_radius[0]; S.filter.ry = film->filter_radius[1];
+    S.filter.Init(film->filter_param);
     S.imagingRatio = film->imaging_ratio;
     o->path = integ->kind == RT_INTEGRATOR_PATH || integ->kind == RT_INTEGRATOR_PATH_MIS;
     S.mis = integ->kind == RT_INTEGRATOR_PATH_MIS;
