@@ -102,6 +102,11 @@ class rt_sample_record(C.Structure):
                 ("t", C.c_float), ("L", F8), ("rgb", F3), ("weight", C.c_float)]
 
 
+class rt_mesh(C.Structure):
+    _fields_ = [("n_vertices", C.c_int), ("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
+                ("texcoords", C.POINTER(C.c_float)), ("n_triangles", C.c_int), ("indices", C.POINTER(C.c_uint32))]
+
+
 class rt_octree_info(C.Structure):
     _fields_ = [("n_nodes", C.c_int), ("n_leaf_refs", C.c_int), ("max_queue_groups", C.c_int), ("depth", C.c_int)]
 
@@ -113,6 +118,7 @@ EXPORTS = [
     "rt_render_pass", "rt_render_pass_device", "rt_film_resolve",
     "rt_get_stats", "rt_reset_stats", "rt_octree_get_info", "rt_octree_export",
     "rt_debug_trace", "rt_debug_samples",
+    "rt_film_resolve_srgb", "rt_load_obj", "rt_mesh_free", "rt_image_write", "rt_rgb_to_sigmoid",
 ]
 
 _lib = None
@@ -155,6 +161,11 @@ def load_library(path=None):
         "rt_octree_export": ([C.c_void_p, P(C.c_float), P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32)], C.c_int),
         "rt_debug_trace": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), C.c_int, P(C.c_int32), P(C.c_float)], C.c_int),
         "rt_debug_samples": ([C.c_void_p, C.c_int, P(C.c_int32), P(C.c_int32), P(rt_sample_record)], C.c_int),
+        "rt_film_resolve_srgb": ([C.c_void_p, P(rt_pixel), P(C.c_uint8)], C.c_int),
+        "rt_load_obj": ([C.c_char_p, P(P(rt_mesh))], C.c_int),
+        "rt_mesh_free": ([P(rt_mesh)], None),
+        "rt_image_write": ([C.c_char_p, C.c_int, C.c_int, P(C.c_uint8), C.c_int], C.c_int),
+        "rt_rgb_to_sigmoid": ([P(C.c_float), P(C.c_float)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

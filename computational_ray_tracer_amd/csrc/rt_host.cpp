@@ -1104,7 +1104,8 @@ int rt_render_pass(rt_ctx* c, int ib, int ie, rt_pixel* film) {
     return RT_OK;
 }
 
-int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) {
+namespace {
+int film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out, int srgb) {
     if (!c || !film || !out) return RT_E_ARG;
     if (!c->have_film) return fail(c, RT_E_STATE, "film not set");
     hipSetDevice(c->device);
@@ -1115,7 +1116,7 @@ int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) {
     if (dalloc(&dout, 3 * n) != hipSuccess) { hipFree(df); return fail(c, RT_E_OOM, "resolve buffer"); }
     int rc = RT_OK;
     if (hipMemcpy(df, film, n * 16, hipMemcpyHostToDevice) != hipSuccess ||
-        launch_resolve(c->stream, (int)n, df, c->d_resolve, c->d_resolve + 9, dout) != hipSuccess ||
+        launch_resolve(c->stream, (int)n, df, c->d_resolve, c->d_resolve + 9, dout, srgb) != hipSuccess ||
         hipMemcpyAsync(out, dout, 3 * n, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         rc = fail(c, RT_E_HIP, "resolve failed");
@@ -1123,6 +1124,10 @@ int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) {
     hipFree(dout);
     return rc;
 }
+}  // namespace
+
+int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 0); }
+int rt_film_resolve_srgb(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 1); }
 
 int rt_get_stats(rt_ctx* c, rt_stats* out) {
     if (!c || !out) return RT_E_ARG;

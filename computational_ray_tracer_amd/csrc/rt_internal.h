@@ -183,6 +183,6 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr);
 hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* m_xyz_from_sensor,
-                          const float* m_rgb_from_xyz, unsigned char* out);
+                          const float* m_rgb_from_xyz, unsigned char* out, int srgb);
 
 }  // namespace rtmi

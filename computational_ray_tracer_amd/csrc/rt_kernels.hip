@@ -1004,8 +1004,29 @@ __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevF
 }
 
 // a20 resolve (RayTracerTestApp.h:437-451): rgbsum/weightsum → XYZFromSensorRGB → RGBFromXYZ → clamp → u8
+// pbrt ColorEncoding::sRGB LinearToSRGB8 (color.h:537-557): EvaluatePolynomial is a Horner chain of FMAs
+__device__ __forceinline__ unsigned char linear_to_srgb8(float v) {
+    if (v <= 0) return 0;
+    if (v >= 1) return 255;
+    float e;
+    if (v <= 0.0031308f) {
+        e = 12.92f * v;
+    } else {
+        float s = sqrtf(v);
+        float p = __builtin_fmaf(s, __builtin_fmaf(s, __builtin_fmaf(s, __builtin_fmaf(s, __builtin_fmaf(s,
+                  -0.016202083165206348f, 0.7551545191665577f), 2.0041169284241644f), 0.7642611304733891f),
+                  0.03453868659826638f), -0.0016829072605308378f);
+        float q = __builtin_fmaf(s, __builtin_fmaf(s, __builtin_fmaf(s, __builtin_fmaf(s, __builtin_fmaf(s, 1.f,
+                  1.8970238036421054f), 0.6085338522168684f), 0.03467195408529984f), -0.00004375359692957097f),
+                  4.178892964897981e-7f);
+        e = p / q * v;
+    }
+    float r = roundf(255.f * e);
+    return (unsigned char)(r < 0 ? 0 : (r > 255 ? 255 : r));
+}
+
 __global__ void k_resolve(int n, const float4* film, const float* __restrict__ A, const float* __restrict__ B,
-                          unsigned char* out) {
+                          unsigned char* out, int srgb) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float4 f = film[i];
@@ -1017,8 +1038,12 @@ __global__ void k_resolve(int n, const float4* film, const float* __restrict__ A
     for (int k = 0; k < 3; ++k) r[k] = (B[0 * 3 + k] * x[0] + B[1 * 3 + k] * x[1]) + B[2 * 3 + k] * x[2];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        float v = 255.0f * gclamp(r[k], 0.0f, 1.0f);
-        out[3 * i + k] = (v == v) ? (unsigned char)v : 0;
+        if (srgb) {
+            out[3 * i + k] = r[k] == r[k] ? linear_to_srgb8(gclamp(r[k], 0.0f, 1.0f)) : 0;
+        } else {
+            float v = 255.0f * gclamp(r[k], 0.0f, 1.0f);
+            out[3 * i + k] = (v == v) ? (unsigned char)v : 0;
+        }
     }
 }
 
@@ -1088,8 +1113,9 @@ hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, cons
     return hipGetLastError();
 }
 
-hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* a, const float* b, unsigned char* out) {
-    hipLaunchKernelGGL(k_resolve, dim3(grid_for(n, 0)), dim3(kBlock), 0, st, n, film, a, b, out);
+hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* a, const float* b, unsigned char* out,
+                          int srgb) {
+    hipLaunchKernelGGL(k_resolve, dim3(grid_for(n, 0)), dim3(kBlock), 0, st, n, film, a, b, out, srgb);
     return hipGetLastError();
 }
 

@@ -58,9 +58,11 @@ class Renderer:
         self._chk("rt_render_pass_device", self.lib.rt_render_pass_device(
             self.h, index_begin, index_end, C.c_void_p(film_ptr), C.c_void_p(stream_ptr or 0)))
 
-    def resolve(self, film):
+    def resolve(self, film, srgb=False):
+        """rt_film_resolve (the reference's linear 255·x) or rt_film_resolve_srgb (pbrt's sRGB encoding)."""
         out = np.zeros((self.res[0] * self.res[1], 3), np.uint8)
-        self._chk("rt_film_resolve", self.lib.rt_film_resolve(self.h, np.ascontiguousarray(film, np.float32).ctypes.data_as(
+        name = "rt_film_resolve_srgb" if srgb else "rt_film_resolve"
+        self._chk(name, getattr(self.lib, name)(self.h, np.ascontiguousarray(film, np.float32).ctypes.data_as(
             C.POINTER(capi.rt_pixel)), out.ctypes.data_as(C.POINTER(C.c_uint8))))
         return out
 

@@ -645,3 +645,46 @@ def cfg5_spectral(res=(3840, 2160), spp=(64, 32), max_depth=5, frequency=70):
     c = cfg4_mixed(res=res, spp=spp, max_depth=max_depth, frequency=frequency)
     c.name = f"cfg5_spectral_{res[0]}x{res[1]}_{spp[0] * spp[1]}spp"
     return c
+
+
+# ------------------------------------------------------------------ ingest / colour / image output
+
+
+def load_obj(path):
+    """rt_load_obj: Wavefront OBJ -> (positions, normals, indices) as the reference's assimp import leaves a
+    MeshCache::Mesh (AssetManager.cpp:67-190): triangulated, one vertex per corner, flat normals if absent."""
+    lib = capi.load_library()
+    m = C.POINTER(capi.rt_mesh)()
+    rc = lib.rt_load_obj(str(path).encode(), C.byref(m))
+    if rc != capi.RT_OK:
+        raise capi.RTError("rt_load_obj", rc, f"cannot load {path}")
+    try:
+        mm = m.contents
+        nv = mm.n_vertices
+        pos = np.ctypeslib.as_array(mm.positions, shape=(nv, 3)).copy()
+        nrm = np.ctypeslib.as_array(mm.normals, shape=(nv, 3)).copy()
+        idx = np.ctypeslib.as_array(mm.indices, shape=(mm.n_triangles, 3)).copy()
+    finally:
+        lib.rt_mesh_free(m)
+    return pos, nrm, idx
+
+
+def rgb_albedo(rgb):
+    """rt_rgb_to_sigmoid: RGBAlbedoSpectrum(sRGB, rgb) sigmoid coefficients (color.cpp:26-72 without its table)."""
+    lib = capi.load_library()
+    src = (C.c_float * 3)(*[float(x) for x in rgb])
+    out = (C.c_float * 3)()
+    rc = lib.rt_rgb_to_sigmoid(src, out)
+    if rc != capi.RT_OK:
+        raise capi.RTError("rt_rgb_to_sigmoid", rc, f"rgb {rgb} outside [0,1]")
+    return tuple(float(x) for x in out)
+
+
+def write_image(path, rgb8, res, flip_y=True):
+    """rt_image_write: the resolved (res_x*res_y, 3) uint8 film to PNG / PPM, bottom row first by default."""
+    lib = capi.load_library()
+    a = np.ascontiguousarray(rgb8, np.uint8)
+    rc = lib.rt_image_write(str(path).encode(), int(res[0]), int(res[1]), a.ctypes.data_as(C.POINTER(C.c_uint8)),
+                            int(flip_y))
+    if rc != capi.RT_OK:
+        raise capi.RTError("rt_image_write", rc, f"cannot write {path}")

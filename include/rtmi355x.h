@@ -229,6 +229,31 @@ int rt_render_pass_device(rt_ctx* ctx, int index_begin, int index_end, void* d_f
 /* a20 resolve (RayTracerTestApp.h:424-452): rgbsum/weightsum -> XYZFromSensorRGB -> sRGB -> clamp -> u8. */
 int rt_film_resolve(rt_ctx* ctx, const rt_pixel* film, uint8_t* rgb_out);
 
+/* a20 + pbrt ColorEncoding::sRGB (color.h:537-557, commented out in the reference): the same resolve, quantised with
+ * LinearToSRGB8 (enoki minimax polynomial, round-to-nearest) instead of the reference's linear 255·x truncation. */
+int rt_film_resolve_srgb(rt_ctx* ctx, const rt_pixel* film, uint8_t* rgb_out);
+
+/* ---- scene ingest / image output / colour (host only: no device needed) ------------------------------- */
+/* MeshCache::Mesh as the reference's assimp import leaves it (AssetManager.cpp:67-190): triangulated, one
+ * vertex per face corner, file normals or flat face normals (aiProcess_GenNormals), texcoords or 0. */
+typedef struct {
+    int n_vertices;
+    float* positions;                /* 3 per vertex */
+    float* normals;                  /* 3 per vertex */
+    float* texcoords;                /* 2 per vertex */
+    int n_triangles;
+    uint32_t* indices;               /* 3 per triangle */
+} rt_mesh;
+/* Wavefront OBJ (v / vt / vn / f, polygons fan-triangulated, negative indices) -> *out (free with rt_mesh_free). */
+int rt_load_obj(const char* path, rt_mesh** out);
+void rt_mesh_free(rt_mesh* mesh);
+/* Write w x h 8-bit RGB to `path`: PNG when it ends in .png, binary PPM otherwise; flip_y writes rows bottom-up
+ * (the film's row 0 is the image bottom: the reference uploads it as a GL texture, RayTracerTestApp.h:453-455). */
+int rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_y);
+/* RGBAlbedoSpectrum coefficients for an sRGB reflectance in [0,1]^3 (replaces the missing RGBToSpectrumTable file,
+ * color.cpp:26-72, 114): grey = the closed form of color.cpp:35-37, otherwise a Gauss-Newton fit in CIELAB. */
+int rt_rgb_to_sigmoid(const float* rgb, float* coeffs);
+
 /* ---- instrumentation ---------------------------------------------------------------------------- */
 int rt_get_stats(rt_ctx* ctx, rt_stats* out);
 int rt_reset_stats(rt_ctx* ctx);

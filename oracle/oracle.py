@@ -69,6 +69,7 @@ def lib():
             "orc_samples": ([C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(capi.rt_sample_record)], C.c_int),
             "orc_render": ([C.c_void_p, C.c_int, C.c_int, P(C.c_float), C.c_int, P(C.c_int64), P(C.c_int), C.c_int], C.c_int),
             "orc_resolve": ([C.c_void_p, P(C.c_float), P(C.c_uint8)], None),
+            "orc_resolve_srgb": ([C.c_void_p, P(C.c_float), P(C.c_uint8)], None),
             "orc_resolve_matrices": ([C.c_void_p, P(C.c_float), P(C.c_float)], None),
         }
         for name, (a, r) in sig.items():
@@ -160,7 +161,8 @@ class OracleScene:
         self.counters = cnt
         return film
 
-    def resolve(self, film):
+    def resolve(self, film, srgb=False):
         out = np.zeros((self.res[0] * self.res[1], 3), np.uint8)
-        lib().orc_resolve(self.h, fptr(np.ascontiguousarray(film, np.float32)), out.ctypes.data_as(C.POINTER(C.c_uint8)))
+        f = lib().orc_resolve_srgb if srgb else lib().orc_resolve
+        f(self.h, fptr(np.ascontiguousarray(film, np.float32)), out.ctypes.data_as(C.POINTER(C.c_uint8)))
         return out

@@ -1038,6 +1038,26 @@ struct Scene {
     int max_depth = 5;
 };
 
+// color.h:537-557 LinearToSRGB / LinearToSRGB8 (pbrt ColorEncoding::sRGB; EvaluatePolynomial = FMA Horner chain)
+static inline float EvalPoly6(float t, float c0, float c1, float c2, float c3, float c4, float c5) {
+    return std::fmaf(t, std::fmaf(t, std::fmaf(t, std::fmaf(t, std::fmaf(t, c5, c4), c3), c2), c1), c0);
+}
+static inline float LinearToSRGB(float value) {
+    if (value <= 0.0031308f) return 12.92f * value;
+    float sqrtValue = std::sqrt(std::max(0.f, value));
+    float p = EvalPoly6(sqrtValue, -0.0016829072605308378f, 0.03453868659826638f, 0.7642611304733891f,
+                        2.0041169284241644f, 0.7551545191665577f, -0.016202083165206348f);
+    float q = EvalPoly6(sqrtValue, 4.178892964897981e-7f, -0.00004375359692957097f, 0.03467195408529984f,
+                        0.6085338522168684f, 1.8970238036421054f, 1.f);
+    return p / q * value;
+}
+static inline uint8_t LinearToSRGB8(float value) {
+    if (value <= 0) return 0;
+    if (value >= 1) return 255;
+    float r = std::round(255.f * LinearToSRGB(value));
+    return (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+}
+
 // Per-sample debug record (for golden fixtures / kernel-level parity)
 struct SampleRecord {
     float lambda[8], pdf[8];

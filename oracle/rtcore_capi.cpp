@@ -400,6 +400,18 @@ void orc_resolve(void* h, const float* film, uint8_t* out) {
         }
     }
 }
+void orc_resolve_srgb(void* h, const float* film, uint8_t* out) {
+    auto* o = static_cast<OracleScene*>(h);
+    int n = o->S.resX * o->S.resY;
+    for (int i = 0; i < n; ++i) {
+        float w = film[4 * i + 3];
+        vec3 s = {film[4 * i] / w, film[4 * i + 1] / w, film[4 * i + 2] / w};
+        vec3 xyz = mul(o->xyzFromSensor, s);
+        vec3 rgb = mul(o->rgbFromXyz, xyz);
+        float v[3] = {rgb.x, rgb.y, rgb.z};
+        for (int c = 0; c < 3; ++c) out[3 * i + c] = v[c] == v[c] ? LinearToSRGB8(gclamp(v[c], 0.0f, 1.0f)) : 0;
+    }
+}
 void orc_resolve_matrices(void* h, float* xyz_from_sensor9, float* rgb_from_xyz9) {
     auto* o = static_cast<OracleScene*>(h);
     std::memcpy(xyz_from_sensor9, o->xyzFromSensor.m, 36);

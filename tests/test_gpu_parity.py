@@ -113,6 +113,7 @@ def test_resolve_matches_oracle(pair_small):
     g, o = pair_small
     f = o.render(0, 3)
     assert np.array_equal(g.resolve(f), o.resolve(f))
+    assert np.array_equal(g.resolve(f, srgb=True), o.resolve(f, srgb=True))   # pbrt sRGB encoding (color.h:537-557)
 
 
 def test_cornell_path_film_bitexact(oracle_lib):
