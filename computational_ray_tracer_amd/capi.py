@@ -18,10 +18,11 @@ RT_MAT_DIFFUSE, RT_MAT_MIRROR, RT_MAT_DIELECTRIC = 0, 1, 2
 RT_SHAPE_SPHERE, RT_SHAPE_DISK, RT_SHAPE_TRIANGLE = 0, 1, 2
 RT_LIGHT_QUAD, RT_LIGHT_DISK, RT_LIGHT_POINT, RT_LIGHT_DISTANT = 0, 1, 2, 3
 RT_CAMERA_PERSPECTIVE, RT_CAMERA_ORTHOGRAPHIC, RT_CAMERA_PINHOLE, RT_CAMERA_THINLENS = 0, 1, 2, 3
-RT_SAMPLER_INDEPENDENT, RT_SAMPLER_STRATIFIED = 0, 1
+RT_SAMPLER_INDEPENDENT, RT_SAMPLER_STRATIFIED, RT_SAMPLER_SOBOL = 0, 1, 2
+RT_SOBOL_NONE, RT_SOBOL_PERMUTE_DIGITS, RT_SOBOL_FAST_OWEN, RT_SOBOL_OWEN = 0, 1, 2, 3
 RT_FILTER_BOX, RT_FILTER_TRIANGLE, RT_FILTER_GAUSSIAN, RT_FILTER_LANCZOS = 0, 1, 2, 3
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 F16 = C.c_float * 16
 F9 = C.c_float * 9
@@ -76,7 +77,7 @@ class rt_camera_desc(C.Structure):
 
 class rt_sampler_desc(C.Structure):
     _fields_ = [("kind", C.c_int), ("x_samples", C.c_int), ("y_samples", C.c_int), ("jitter", C.c_int),
-                ("seed", C.c_int)]
+                ("seed", C.c_int), ("randomize", C.c_int)]
 
 
 class rt_film_desc(C.Structure):

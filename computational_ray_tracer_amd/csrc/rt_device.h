@@ -156,18 +156,88 @@ struct Pcg {  // rng.h:24-144
     }
 };
 
-// samplers.h:38-136 — Independent / Stratified sampler state of one camera sample
+// ------------------------------------------------------------------------------------- Sobol
+// hash.h:96-104 Hash(int, int): an 8-byte key, one block, no tail
+RT_DEV uint64_t hash_int2(int a, int b) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = 0ull ^ (8ull * m);
+    h = murmur_mix_block(h, (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32));
+    return murmur_final(h);
+}
+// samplers.h:198-209 SobolSample + the scramblers of samplers.h:147-190 (ReverseBits32 = bit reversal)
+RT_DEV float sobol_sample(const DevSampler& S, uint64_t a, int dimension, int randomize, uint32_t seed) {
+    uint32_t v = 0;
+    const uint32_t* C = S.sobol_mats + dimension * kSobolMatrixSize;
+    for (int i = 0; a != 0; a >>= 1, i++)
+        if (a & 1) v ^= C[i];
+    if (randomize == 1) {
+        v ^= seed;
+    } else if (randomize == 2) {
+        v = __builtin_bitreverse32(v);
+        v ^= v * 0x3d20adeau;
+        v += seed;
+        v *= (seed >> 16) | 1u;
+        v ^= v * 0x05526c56u;
+        v ^= v * 0x53a22864u;
+        v = __builtin_bitreverse32(v);
+    } else if (randomize == 3) {
+        if (seed & 1) v ^= 1u << 31;
+        for (int b = 1; b < 32; ++b) {
+            uint32_t mask = (~0u) << (32 - b);
+            if ((uint32_t)mix_bits((uint64_t)((v & mask) ^ seed)) & (1u << b)) v ^= 1u << (31 - b);
+        }
+    }
+    float f = (float)v * 0x1p-32f;
+    const float ome = 0x1.fffffep-1f;  // FloatOneMinusEpsilon (samplers.h:141)
+    return ome < f ? ome : f;          // std::min(f, ome)
+}
+// samplers.h:211-227 SobolIntervalToIndex
+RT_DEV uint64_t sobol_interval_to_index(const DevSampler& S, uint64_t frame, int px, int py) {
+    const uint32_t m = (uint32_t)S.sobol_m;
+    if (m == 0) return frame;
+    uint64_t index = frame << (2 * m);
+    uint64_t delta = 0;
+    for (int c = 0; frame; frame >>= 1, ++c)
+        if (frame & 1) delta ^= S.sobol_fwd[c];
+    uint64_t b = (((uint64_t)(uint32_t)px << m) | (uint32_t)py) ^ delta;
+    for (int c = 0; b; b >>= 1, ++c)
+        if (b & 1) index ^= S.sobol_inv[c];
+    return index;
+}
+
+// samplers.h:38-136, 229-327 — Independent / Stratified / Sobol sampler state of one camera sample (Sobol keeps its
+// sobolIndex in rng.state)
 struct Smp {
     Pcg rng;
     int px, py, index, dim;
     // samplers.h:80-93 / 47-51 (caller guarantees the stratified jitter==false index < spp precondition)
     RT_DEV void start(const DevSampler& S, int x, int y, int idx, int d) {
         px = x; py = y; index = idx; dim = d;
+        if (S.kind == 2) {  // samplers.h:258-263
+            dim = d > 2 ? d : 2;
+            rng.state = sobol_interval_to_index(S, (uint64_t)idx, x, y);
+            rng.inc = 0;
+            return;
+        }
         rng.set_sequence(hash_pixel(x, y, S.seed));
         rng.advance((uint64_t)idx * 65536ull + (uint64_t)d);
     }
+    RT_DEV float sobol_dim(const DevSampler& S, int d) const {  // samplers.h:305-318
+        uint32_t h = S.randomize ? (uint32_t)hash_int2(d, S.seed) : 0u;
+        return sobol_sample(S, rng.state, d, S.randomize, h);
+    }
+    RT_DEV void get_pixel2d(const DevSampler& S, float& u0, float& u1) {  // samplers.h:283-297
+        if (S.kind != 2) { get2d(S, u0, u1); return; }
+        float a = sobol_sample(S, rng.state, 0, 0, 0u), b = sobol_sample(S, rng.state, 1, 0, 0u);
+        u0 = gclamp(a * (float)S.scale - (float)px, 0.0f, 1.0f);  // OneMinusEpsilon == 1.0f (pch.h:39)
+        u1 = gclamp(b * (float)S.scale - (float)py, 0.0f, 1.0f);
+    }
     RT_DEV float get1d(const DevSampler& S) {  // samplers.h:95-104
         if (S.kind == 0) return rng.uniform();
+        if (S.kind == 2) {
+            if (dim >= kSobolDims) dim = 2;
+            return sobol_dim(S, dim++);
+        }
         uint64_t h = hash_pixel_dim(px, py, dim, S.seed);
         int stratum = permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
         ++dim;
@@ -176,6 +246,13 @@ struct Smp {
     }
     RT_DEV void get2d(const DevSampler& S, float& u0, float& u1) {  // samplers.h:107-123
         if (S.kind == 0) { u0 = rng.uniform(); u1 = rng.uniform(); return; }
+        if (S.kind == 2) {
+            if (dim + 1 >= kSobolDims) dim = 2;
+            u0 = sobol_dim(S, dim);
+            u1 = sobol_dim(S, dim + 1);
+            dim += 2;
+            return;
+        }
         if (index >= S.spp) { u0 = 0; u1 = 0; return; }
         uint64_t h = hash_pixel_dim(px, py, dim, S.seed);
         int stratum = permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);

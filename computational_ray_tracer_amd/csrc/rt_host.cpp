@@ -274,6 +274,9 @@ struct rt_ctx {
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     float* d_cdf = nullptr;    // Gaussian / Lanczos filter tables: x then y, cdf_n + 1 floats each
     int cdf_n = 0;
+    uint32_t* d_sobol_mats = nullptr;  // Sobol generator columns; d_sobol_fwd: fwd then inv tables for sobol_m
+    uint64_t* d_sobol_fwd = nullptr;
+    int sobol_m = 0;
     size_t film_cap = 0;
     int grid = 0;              // persistent grid size (blocks)
     // stats
@@ -469,11 +472,94 @@ DevCamera dev_camera(const rt_camera_desc& d) {
     c.sensor_depth = d.sensor_depth;
     return c;
 }
-DevSampler dev_sampler(const rt_sampler_desc& d) {
-    DevSampler s;
+// Sobol generator matrices (32 dimensions, Joe-Kuo new-joe-kuo-6.21201 direction numbers; dimension 0 = van der
+// Corput) and SobolIntervalToIndex's tables for a resolution exponent m (the reference's VdCSobolMatrices /
+// VdCSobolMatricesInv, HelperFunctions.h:212-470, derived here by inverting the 2m x 2m GF(2) pixel map).
+void sobol_tables(int m, std::vector<uint32_t>& mats, std::vector<uint64_t>& fwd, std::vector<uint64_t>& inv) {
+    static const int dirs[31][9] = {
+        {1, 0, 1}, {2, 1, 1, 3}, {3, 1, 1, 3, 1}, {3, 2, 1, 1, 1}, {4, 1, 1, 1, 3, 3}, {4, 4, 1, 3, 5, 13},
+        {5, 2, 1, 1, 5, 5, 17}, {5, 4, 1, 1, 5, 5, 5}, {5, 7, 1, 1, 7, 11, 19}, {5, 11, 1, 1, 5, 1, 1},
+        {5, 13, 1, 1, 1, 3, 11}, {5, 14, 1, 3, 5, 5, 31}, {6, 1, 1, 3, 3, 9, 7, 49}, {6, 13, 1, 1, 1, 15, 21, 21},
+        {6, 16, 1, 3, 1, 13, 27, 49}, {6, 19, 1, 1, 1, 15, 7, 5}, {6, 22, 1, 3, 1, 15, 13, 25},
+        {6, 25, 1, 1, 5, 5, 19, 61}, {7, 1, 1, 3, 7, 11, 23, 15, 103}, {7, 4, 1, 3, 7, 13, 13, 15, 69},
+        {7, 7, 1, 1, 3, 13, 7, 35, 63}, {7, 8, 1, 3, 5, 9, 1, 25, 53}, {7, 14, 1, 3, 1, 13, 9, 35, 107},
+        {7, 19, 1, 3, 1, 5, 27, 61, 31}, {7, 21, 1, 1, 5, 11, 19, 41, 61}, {7, 28, 1, 3, 5, 3, 3, 13, 69},
+        {7, 31, 1, 1, 7, 13, 1, 19, 1}, {7, 32, 1, 3, 7, 5, 13, 19, 59}, {7, 37, 1, 1, 3, 9, 25, 29, 41},
+        {7, 41, 1, 3, 5, 13, 23, 1, 55}, {7, 42, 1, 3, 7, 3, 13, 59, 17}};
+    const int S = kSobolMatrixSize;
+    mats.assign((size_t)kSobolDims * S, 0u);
+    for (int j = 0; j < 32; ++j) mats[j] = 1u << (31 - j);
+    for (int d = 1; d < kSobolDims; ++d) {
+        int s = dirs[d - 1][0], a = dirs[d - 1][1];
+        uint64_t dn[kSobolMatrixSize];
+        for (int i = 0; i < s; ++i) dn[i] = (uint64_t)dirs[d - 1][2 + i];
+        for (int i = s; i < S; ++i) {  // m_i = 2^s m_{i-s} ^ m_{i-s} ^ sum_k a_k 2^k m_{i-k}
+            uint64_t v = dn[i - s] ^ (dn[i - s] << s);
+            for (int k = 1; k < s; ++k)
+                if ((a >> (s - 1 - k)) & 1) v ^= dn[i - k] << k;
+            dn[i] = v;
+        }
+        for (int j = 0; j < S; ++j) mats[(size_t)d * S + j] = (uint32_t)((dn[j] << (63 - j)) >> 32);
+    }
+    fwd.assign(S, 0);
+    inv.assign(S, 0);
+    if (m == 0) return;
+    const int n = 2 * m;
+    auto col = [&](int j) { return ((uint64_t)(mats[j] >> (32 - m)) << m) | (uint64_t)(mats[S + j] >> (32 - m)); };
+    for (int c = 0; c + n < S; ++c) fwd[c] = col(n + c);
+    uint64_t rows[32], id[32];
+    for (int r = 0; r < n; ++r) {
+        rows[r] = 0;
+        for (int j = 0; j < n; ++j) rows[r] |= ((col(j) >> r) & 1ull) << j;
+        id[r] = 1ull << r;
+    }
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        while (!((rows[p] >> c) & 1)) ++p;
+        std::swap(rows[p], rows[c]);
+        std::swap(id[p], id[c]);
+        for (int r = 0; r < n; ++r)
+            if (r != c && ((rows[r] >> c) & 1)) { rows[r] ^= rows[c]; id[r] ^= id[c]; }
+    }
+    for (int c = 0; c < n; ++c)  // column c of M^-1: index bits set by pixel bit c
+        for (int r = 0; r < n; ++r) inv[c] |= ((id[r] >> c) & 1ull) << r;
+}
+
+DevSampler dev_sampler(const rt_ctx* c) {
+    const rt_sampler_desc& d = c->smp;
+    DevSampler s{};
     s.kind = d.kind; s.xs = d.x_samples; s.ys = d.y_samples; s.jitter = d.jitter; s.seed = d.seed;
-    s.spp = d.kind == RT_SAMPLER_INDEPENDENT ? d.x_samples : d.x_samples * d.y_samples;
+    s.spp = d.kind == RT_SAMPLER_STRATIFIED ? d.x_samples * d.y_samples : d.x_samples;
+    s.randomize = d.randomize;
+    s.sobol_m = c->sobol_m;
+    s.scale = 1 << c->sobol_m;
+    s.sobol_mats = c->d_sobol_mats;
+    s.sobol_fwd = c->d_sobol_fwd;
+    s.sobol_inv = c->d_sobol_fwd ? c->d_sobol_fwd + kSobolMatrixSize : nullptr;
     return s;
+}
+
+// Sobol tables on the device for the current film (scale = RoundUpPow2(max(res)), samplers.h:243)
+int ensure_sobol(rt_ctx* c) {
+    if (c->smp.kind != RT_SAMPLER_SOBOL) return RT_OK;
+    int v = std::max(c->film.res_x, c->film.res_y) - 1;
+    v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
+    int m = (int)std::log2((float)(v + 1));
+    if (m > 16) return fail(c, RT_E_LIMIT, "Sobol sampler supports film resolutions up to 65536");
+    if (c->d_sobol_mats && c->sobol_m == m) return RT_OK;
+    std::vector<uint32_t> mats;
+    std::vector<uint64_t> fwd, inv;
+    sobol_tables(m, mats, fwd, inv);
+    if (!c->d_sobol_mats) {
+        HIPCHK(c, hipMalloc(&c->d_sobol_mats, mats.size() * 4));
+        HIPCHK(c, hipMalloc(&c->d_sobol_fwd, 2 * kSobolMatrixSize * 8));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(c->d_sobol_mats, mats.data(), mats.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_sobol_fwd, fwd.data(), kSobolMatrixSize * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_sobol_fwd + kSobolMatrixSize, inv.data(), kSobolMatrixSize * 8, hipMemcpyHostToDevice));
+    c->sobol_m = m;
+    return RT_OK;
 }
 DevFilm dev_film(const rt_ctx* c) {
     const rt_film_desc& d = c->film;
@@ -508,7 +594,8 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     int rc = check_ready(c);
     if (rc) return rc;
     if (ib < 0 || ie < ib) return fail(c, RT_E_ARG, "invalid index range");
-    DevSampler smp = dev_sampler(c->smp);
+    if ((rc = ensure_sobol(c))) return rc;
+    DevSampler smp = dev_sampler(c);
     if (c->smp.kind == RT_SAMPLER_STRATIFIED && !c->smp.jitter && ie > smp.spp)
         return fail(c, RT_E_ARG, "StratifiedSampler without jitter supports indices < SamplesPerPixel (samplers.h:83-87)");
     if ((rc = build_work(c))) return rc;
@@ -694,7 +781,8 @@ void rt_destroy(rt_ctx* c) {
     for (hipEvent_t e : c->pool) hipEventDestroy(e);
     free_scene(c);
     free_workspace(c);
-    void* ptrs[] = {c->d_spec, c->d_qcount, c->d_ctr, c->d_resolve, c->d_work, c->d_film, c->d_cdf};
+    void* ptrs[] = {c->d_spec, c->d_qcount, c->d_ctr, c->d_resolve, c->d_work, c->d_film, c->d_cdf, c->d_sobol_mats,
+                    c->d_sobol_fwd};
     for (void* p : ptrs)
         if (p) hipFree(p);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -1023,7 +1111,9 @@ int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
 
 int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
     if (!c || !d) return RT_E_ARG;
-    if (d->kind != RT_SAMPLER_INDEPENDENT && d->kind != RT_SAMPLER_STRATIFIED) return fail(c, RT_E_ARG, "unknown sampler");
+    if (d->kind < RT_SAMPLER_INDEPENDENT || d->kind > RT_SAMPLER_SOBOL) return fail(c, RT_E_ARG, "unknown sampler");
+    if (d->kind == RT_SAMPLER_SOBOL && (d->randomize < RT_SOBOL_NONE || d->randomize > RT_SOBOL_OWEN))
+        return fail(c, RT_E_ARG, "unknown Sobol randomization");
     if (d->x_samples <= 0 || (d->kind == RT_SAMPLER_STRATIFIED && d->y_samples <= 0))
         return fail(c, RT_E_ARG, "samples per pixel must be positive");
     c->smp = *d;
@@ -1215,7 +1305,8 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
     if (c->integ.kind != RT_INTEGRATOR_REFERENCE) return fail(c, RT_E_ARG, "records are for the reference integrator");
     if (n == 0) return RT_OK;
     int npx = c->film.res_x * c->film.res_y;
-    DevSampler smp = dev_sampler(c->smp);
+    if ((rc = ensure_sobol(c))) return rc;
+    DevSampler smp = dev_sampler(c);
     for (int i = 0; i < n; ++i) {
         if (pixel_ids[i] < 0 || pixel_ids[i] >= npx || indices[i] < 0) return fail(c, RT_E_ARG, "sample out of range");
         if (c->smp.kind == RT_SAMPLER_STRATIFIED && !c->smp.jitter && indices[i] >= smp.spp)

@@ -36,7 +36,12 @@ struct DevCamera {
 
 struct DevSampler {
     int kind, xs, ys, jitter, seed, spp;
+    int randomize, sobol_m, scale;  // SobolSampler (samplers.h:229-327)
+    const uint32_t* sobol_mats;     // kSobolDims x kSobolMatrixSize generator columns
+    const uint64_t* sobol_fwd;      // SobolIntervalToIndex tables for sobol_m (kSobolMatrixSize each)
+    const uint64_t* sobol_inv;
 };
+static const int kSobolDims = 32, kSobolMatrixSize = 52;
 
 struct DevFilm {
     int res_x, res_y, filter;

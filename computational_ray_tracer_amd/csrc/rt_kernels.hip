@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevC
             pdf[i] = visible_pdf(lam[i]);
         }
         float u0, u1;
-        sm.get2d(smp, u0, u1);
+        sm.get_pixel2d(smp, u0, u1);  // Sampler::GetPixel2D (RayTracerTestApp.h:316)
         float fx, fy;
         if (film.filter == 0) { fx = lerpf_(u0, -film.rx, film.rx); fy = lerpf_(u1, -film.ry, film.ry); }
         else if (film.filter == 1) { fx = sample_tent(u0, film.rx); fy = sample_tent(u1, film.ry); }

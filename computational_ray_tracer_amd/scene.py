@@ -207,6 +207,21 @@ class StratifiedSampler:
 
 
 @dataclass
+class SobolSampler:
+    """pbrt::SobolSampler(samplesPerPixel, fullResolution, randomize, seed) (samplers.h:227-327); the film
+    resolution comes from rt_film_set."""
+    samples_per_pixel: int = 16
+    randomize: int = capi.RT_SOBOL_FAST_OWEN
+    seed: int = 0
+
+    def spp(self):
+        return self.samples_per_pixel
+
+    def desc(self):
+        return capi.rt_sampler_desc(capi.RT_SAMPLER_SOBOL, self.samples_per_pixel, 1, 0, self.seed, self.randomize)
+
+
+@dataclass
 class IndependentSampler:
     """pbrt::IndependentSampler(samplesPerPixel, seed) (samplers.h:38-62)."""
     samples_per_pixel: int = 16

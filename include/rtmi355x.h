@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 typedef enum {
     RT_OK = 0,
@@ -132,14 +132,20 @@ typedef struct {
     float sensor_depth;
 } rt_camera_desc;
 
-enum { RT_SAMPLER_INDEPENDENT = 0, RT_SAMPLER_STRATIFIED = 1 };
+enum { RT_SAMPLER_INDEPENDENT = 0, RT_SAMPLER_STRATIFIED = 1, RT_SAMPLER_SOBOL = 2 };
+enum { RT_SOBOL_NONE = 0, RT_SOBOL_PERMUTE_DIGITS = 1, RT_SOBOL_FAST_OWEN = 2, RT_SOBOL_OWEN = 3 };
 /* pbrt::IndependentSampler(spp, seed) (samplers.h:38-62): x_samples = spp, y_samples ignored.
- * pbrt::StratifiedSampler(x, y, jitter, seed) (samplers.h:66-136). */
+ * pbrt::StratifiedSampler(x, y, jitter, seed) (samplers.h:66-136).
+ * pbrt::SobolSampler(spp, film resolution, randomize, seed) (samplers.h:227-327): x_samples = spp.  The
+ * reference declares SobolMatrices32 without defining it (HelperFunctions.h:208-210); the build generates the
+ * generator matrices for 32 dimensions from the Joe-Kuo direction numbers (dimensions >= 32 wrap to 2 as in
+ * samplers.h:270-283) and derives SobolIntervalToIndex's VdC tables itself (equal to HelperFunctions.h:212-470). */
 typedef struct {
     int kind;
     int x_samples, y_samples;
     int jitter;
     int seed;
+    int randomize;                   /* Sobol: RT_SOBOL_* */
 } rt_sampler_desc;
 
 enum { RT_FILTER_BOX = 0, RT_FILTER_TRIANGLE = 1, RT_FILTER_GAUSSIAN = 2, RT_FILTER_LANCZOS = 3 };

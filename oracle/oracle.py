@@ -41,6 +41,10 @@ def lib():
             "orc_pcg_draws": ([C.c_int, C.c_uint64, C.c_int64, C.c_int, P(C.c_uint32)], None),
             "orc_sampler_draws": ([P(capi.rt_sampler_desc), C.c_int, C.c_int, C.c_int, C.c_int, P(C.c_int), P(C.c_float)], C.c_int),
             "orc_sample_visible": ([C.c_float, P(C.c_float), P(C.c_float)], None),
+            "orc_sampler_draws_res": ([P(capi.rt_sampler_desc), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       P(C.c_int), P(C.c_float)], C.c_int),
+            "orc_sobol_index": ([C.c_int] * 5, C.c_int64),
+            "orc_sobol_sample": ([C.c_int64, C.c_int, C.c_int, C.c_uint32, C.c_int], C.c_float),
             "orc_visible_pdf": ([C.c_float], C.c_float),
             "orc_sample_visible_wavelength": ([C.c_float], C.c_float),
             "orc_disk_concentric": ([C.c_float, C.c_float, P(C.c_float)], None),

@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <queue>
 #include <vector>
 
@@ -243,18 +244,155 @@ struct RNG {
     }
 };
 
+// ============================================================================== Sobol (samplers.h:139-327)
+// SobolMatrices32 is declared but never defined in the reference (HelperFunctions.h:208-210): this build generates
+// 32 dimensions from the Joe-Kuo (new-joe-kuo-6.21201) direction numbers, dimension 0 = van der Corput.  The
+// SobolIntervalToIndex tables are derived by GF(2) inversion; they equal the reference's VdCSobolMatrices(Inv)
+// (HelperFunctions.h:212-470) for every m.
+static const int NSobolDims = 32, SobolMatrixSize = 52;
+struct SobolData {
+    uint32_t mats[NSobolDims * SobolMatrixSize];
+    uint64_t fwd[SobolMatrixSize], inv[SobolMatrixSize];
+    int m = 0;
+    void Build(int m_) {
+        static const int JK[31][9] = {  // s, a, m_1..m_s
+            {1, 0, 1}, {2, 1, 1, 3}, {3, 1, 1, 3, 1}, {3, 2, 1, 1, 1}, {4, 1, 1, 1, 3, 3}, {4, 4, 1, 3, 5, 13},
+            {5, 2, 1, 1, 5, 5, 17}, {5, 4, 1, 1, 5, 5, 5}, {5, 7, 1, 1, 7, 11, 19}, {5, 11, 1, 1, 5, 1, 1},
+            {5, 13, 1, 1, 1, 3, 11}, {5, 14, 1, 3, 5, 5, 31}, {6, 1, 1, 3, 3, 9, 7, 49}, {6, 13, 1, 1, 1, 15, 21, 21},
+            {6, 16, 1, 3, 1, 13, 27, 49}, {6, 19, 1, 1, 1, 15, 7, 5}, {6, 22, 1, 3, 1, 15, 13, 25},
+            {6, 25, 1, 1, 5, 5, 19, 61}, {7, 1, 1, 3, 7, 11, 23, 15, 103}, {7, 4, 1, 3, 7, 13, 13, 15, 69},
+            {7, 7, 1, 1, 3, 13, 7, 35, 63}, {7, 8, 1, 3, 5, 9, 1, 25, 53}, {7, 14, 1, 3, 1, 13, 9, 35, 107},
+            {7, 19, 1, 3, 1, 5, 27, 61, 31}, {7, 21, 1, 1, 5, 11, 19, 41, 61}, {7, 28, 1, 3, 5, 3, 3, 13, 69},
+            {7, 31, 1, 1, 7, 13, 1, 19, 1}, {7, 32, 1, 3, 7, 5, 13, 19, 59}, {7, 37, 1, 1, 3, 9, 25, 29, 41},
+            {7, 41, 1, 3, 5, 13, 23, 1, 55}, {7, 42, 1, 3, 7, 3, 13, 59, 17}};
+        for (int j = 0; j < SobolMatrixSize; ++j) mats[j] = j < 32 ? 1u << (31 - j) : 0u;
+        for (int d = 1; d < NSobolDims; ++d) {
+            int s = JK[d - 1][0], a = JK[d - 1][1];
+            uint64_t mm[SobolMatrixSize];
+            for (int i = 0; i < s; ++i) mm[i] = (uint64_t)JK[d - 1][2 + i];
+            for (int i = s; i < SobolMatrixSize; ++i) {
+                uint64_t v = mm[i - s] ^ (mm[i - s] << s);
+                for (int k = 1; k < s; ++k)
+                    if ((a >> (s - 1 - k)) & 1) v ^= mm[i - k] << k;
+                mm[i] = v;
+            }
+            for (int j = 0; j < SobolMatrixSize; ++j) mats[d * SobolMatrixSize + j] = (uint32_t)((mm[j] << (63 - j)) >> 32);
+        }
+        m = m_;
+        for (int c = 0; c < SobolMatrixSize; ++c) fwd[c] = inv[c] = 0;
+        if (m == 0) return;
+        auto top = [&](uint32_t v) { return (uint64_t)(v >> (32 - m)); };
+        int n = 2 * m;
+        for (int c = 0; c + n < SobolMatrixSize; ++c) fwd[c] = (top(mats[n + c]) << m) | top(mats[SobolMatrixSize + n + c]);
+        // columns j of the 2m x 2m map (index bit j -> pixel bits), inverted by Gauss-Jordan over GF(2)
+        uint64_t rows[64];
+        for (int r = 0; r < n; ++r) {
+            uint64_t row = 0;
+            for (int j = 0; j < n; ++j) {
+                uint64_t colj = (top(mats[j]) << m) | top(mats[SobolMatrixSize + j]);
+                row |= ((colj >> r) & 1ull) << j;
+            }
+            rows[r] = row | (1ull << (n + r));  // [M | I] needs 4m <= 64 bits: m <= 16
+        }
+        for (int col = 0; col < n; ++col) {
+            int piv = col;
+            while (!((rows[piv] >> col) & 1)) ++piv;
+            std::swap(rows[piv], rows[col]);
+            for (int r = 0; r < n; ++r)
+                if (r != col && ((rows[r] >> col) & 1)) rows[r] ^= rows[col];
+        }
+        for (int c = 0; c < n; ++c) {
+            uint64_t v = 0;
+            for (int r = 0; r < n; ++r) v |= ((rows[r] >> (n + c)) & 1ull) << r;
+            inv[c] = v;
+        }
+    }
+};
+// hash.h:96-104 Hash(int dimension, int seed): an 8-byte key
+static inline uint64_t Hash2(int a, int b) {
+    unsigned char buf[8];
+    std::memcpy(buf, &a, 4); std::memcpy(buf + 4, &b, 4);
+    return MurmurHash64A(buf, 8, 0);
+}
+static inline uint32_t ReverseBits32(uint32_t n) {  // HelperFunctions.h:154-162
+    n = (n << 16) | (n >> 16);
+    n = ((n & 0x00ff00ff) << 8) | ((n & 0xff00ff00) >> 8);
+    n = ((n & 0x0f0f0f0f) << 4) | ((n & 0xf0f0f0f0) >> 4);
+    n = ((n & 0x33333333) << 2) | ((n & 0xcccccccc) >> 2);
+    n = ((n & 0x55555555) << 1) | ((n & 0xaaaaaaaa) >> 1);
+    return n;
+}
+// samplers.h:198-209 SobolSample with the scramblers of 147-190
+static inline float SobolSampleF(const SobolData& D, int64_t a, int dimension, int randomize, uint32_t seed) {
+    uint32_t v = 0;
+    for (int i = dimension * SobolMatrixSize; a != 0; a >>= 1, i++)
+        if (a & 1) v ^= D.mats[i];
+    if (randomize == 1) {
+        v ^= seed;
+    } else if (randomize == 2) {
+        v = ReverseBits32(v);
+        v ^= v * 0x3d20adea;
+        v += seed;
+        v *= (seed >> 16) | 1;
+        v ^= v * 0x05526c56;
+        v ^= v * 0x53a22864;
+        v = ReverseBits32(v);
+    } else if (randomize == 3) {
+        if (seed & 1) v ^= 1u << 31;
+        for (int b = 1; b < 32; ++b) {
+            uint32_t mask = (~0u) << (32 - b);
+            if ((uint32_t)MixBits((v & mask) ^ seed) & (1u << b)) v ^= 1u << (31 - b);
+        }
+    }
+    const float FloatOneMinusEpsilon = 0x1.fffffep-1;
+    return std::min(v * 0x1p-32f, FloatOneMinusEpsilon);
+}
+// samplers.h:211-227 SobolIntervalToIndex
+static inline uint64_t SobolIntervalToIndex(const SobolData& D, uint32_t m, uint64_t frame, int px, int py) {
+    if (m == 0) return frame;
+    uint64_t index = frame << (2 * m);
+    uint64_t delta = 0;
+    for (int c = 0; frame; frame >>= 1, ++c)
+        if (frame & 1) delta ^= D.fwd[c];
+    uint64_t b = (((uint64_t)((uint32_t)px) << m) | ((uint32_t)py)) ^ delta;
+    for (int c = 0; b; b >>= 1, ++c)
+        if (b & 1) index ^= D.inv[c];
+    return index;
+}
+
 // ============================================================================== samplers
-// samplers.h:38-62 IndependentSampler ; samplers.h:66-136 StratifiedSampler
+// samplers.h:38-62 IndependentSampler ; samplers.h:66-136 StratifiedSampler ; samplers.h:229-327 SobolSampler
 struct Sampler {
-    int kind = 1;  // 0 = Independent, 1 = Stratified
+    int kind = 1;  // 0 = Independent, 1 = Stratified, 2 = Sobol
     int xPixelSamples = 1, yPixelSamples = 1, seed = 0;
     bool jitter = false;
     RNG rng;
     int px = 0, py = 0, sampleIndex = 0, dimension = 0;
+    int randomize = 0, scale = 1;                // Sobol
+    int64_t sobolIndex = 0;
+    std::shared_ptr<const SobolData> sobol;
+    void InitSobol(int resX, int resY) {         // samplers.h:236-245: scale = RoundUpPow2(max(res))
+        int v = std::max(resX, resY) - 1;
+        v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
+        scale = v + 1;
+        auto d = std::make_shared<SobolData>();
+        d->Build((int)std::log2((float)scale));
+        sobol = d;
+    }
+    float SobolDim(int dim) const {               // samplers.h:305-318 SampleDimension
+        uint32_t hash = randomize == 0 ? 0u : (uint32_t)Hash2(dim, seed);
+        return SobolSampleF(*sobol, sobolIndex, dim, randomize, hash);
+    }
 
     int SamplesPerPixel() const { return kind == 0 ? xPixelSamples : xPixelSamples * yPixelSamples; }
     // returns false where the reference prints "more sampels than pixels for strat" and keeps stale state
     bool StartPixelSample(int x, int y, int index, int dim) {
+        if (kind == 2) {  // samplers.h:258-263
+            px = x; py = y; sampleIndex = index;
+            dimension = std::max(2, dim);
+            sobolIndex = (int64_t)SobolIntervalToIndex(*sobol, (uint32_t)sobol->m, (uint64_t)index, x, y);
+            return true;
+        }
         if (kind == 1 && jitter == false && index >= SamplesPerPixel()) return false;  // samplers.h:83-87
         px = x; py = y; sampleIndex = index; dimension = dim;
         rng.SetSequence(Hash(x, y, seed));
@@ -263,6 +401,10 @@ struct Sampler {
     }
     float Get1D() {
         if (kind == 0) return rng.UniformF();
+        if (kind == 2) {  // samplers.h:266-271
+            if (dimension >= NSobolDims) dimension = 2;
+            return SobolDim(dimension++);
+        }
         uint64_t hash = Hash(px, py, dimension, seed);                                     // samplers.h:98
         int stratum = PermutationElement((uint32_t)sampleIndex, (uint32_t)SamplesPerPixel(), (uint32_t)hash);
         ++dimension;
@@ -271,6 +413,12 @@ struct Sampler {
     }
     vec2 Get2D() {
         if (kind == 0) { float a = rng.UniformF(); float b = rng.UniformF(); return {a, b}; }
+        if (kind == 2) {  // samplers.h:274-281
+            if (dimension + 1 >= NSobolDims) dimension = 2;
+            vec2 u = {SobolDim(dimension), SobolDim(dimension + 1)};
+            dimension += 2;
+            return u;
+        }
         if (sampleIndex >= SamplesPerPixel()) return {0, 0};                                // samplers.h:109-112
         uint64_t hash = Hash(px, py, dimension, seed);
         int stratum = PermutationElement((uint32_t)sampleIndex, (uint32_t)SamplesPerPixel(), (uint32_t)hash);
@@ -280,7 +428,14 @@ struct Sampler {
         float dy = jitter ? rng.UniformF() : 0.5f;
         return {((float)x + dx) / (float)xPixelSamples, ((float)y + dy) / (float)yPixelSamples};
     }
-    vec2 GetPixel2D() { return Get2D(); }
+    vec2 GetPixel2D() {
+        if (kind != 2) return Get2D();
+        // samplers.h:283-297: un-randomised dimensions 0 and 1, remapped into the pixel (clamped to [0, 1])
+        float u[2] = {SobolSampleF(*sobol, sobolIndex, 0, 0, 0), SobolSampleF(*sobol, sobolIndex, 1, 0, 0)};
+        float p[2] = {(float)px, (float)py};
+        for (int d = 0; d < 2; ++d) u[d] = gclamp(u[d] * (float)scale - p[d], 0.0f, OneMinusEpsilon);
+        return {u[0], u[1]};
+    }
 };
 
 // ============================================================================ sampling

@@ -110,6 +110,35 @@ int orc_sampler_draws(const rt_sampler_desc* d, int px, int py, int index, int n
     return w;
 }
 
+// like orc_sampler_draws for any sampler kind with a film resolution (Sobol scale); op 3 = GetPixel2D
+int orc_sampler_draws_res(const rt_sampler_desc* d, int res_x, int res_y, int px, int py, int index, int n_ops,
+                          const int* ops, float* out) {
+    Sampler s;
+    s.kind = d->kind; s.xPixelSamples = d->x_samples; s.yPixelSamples = d->y_samples;
+    s.jitter = d->jitter != 0; s.seed = d->seed; s.randomize = d->randomize;
+    if (d->kind == RT_SAMPLER_SOBOL) s.InitSobol(res_x, res_y);
+    if (!s.StartPixelSample(px, py, index, 0)) return -1;
+    int w = 0;
+    for (int k = 0; k < n_ops; ++k) {
+        if (ops[k] == 1) { out[w++] = s.Get1D(); continue; }
+        vec2 v = ops[k] == 3 ? s.GetPixel2D() : s.Get2D();
+        out[w++] = v.x; out[w++] = v.y;
+    }
+    return w;
+}
+float orc_sobol_sample(int64_t index, int dim, int randomize, uint32_t seed, int m) {
+    static std::shared_ptr<SobolData> d;
+    if (!d || d->m != m) { d = std::make_shared<SobolData>(); d->Build(m); }
+    return SobolSampleF(*d, index, dim, randomize, seed);
+}
+int64_t orc_sobol_index(int res_x, int res_y, int px, int py, int index) {
+    Sampler s;
+    s.kind = 2;
+    s.InitSobol(res_x, res_y);
+    s.StartPixelSample(px, py, index, 0);
+    return s.sobolIndex;
+}
+
 void orc_sample_visible(float u, float* lambda, float* pdf) {
     SW s = SampleVisible(u);
     std::memcpy(lambda, s.lambda, 32);
@@ -260,7 +289,9 @@ void* orc_scene_create(const rt_scene_desc* sc, const rt_camera_desc* cam, const
     S.camera = MakeCamera(cam);
     S.sampler.kind = smp->kind; S.sampler.xPixelSamples = smp->x_samples; S.sampler.yPixelSamples = smp->y_samples;
     S.sampler.jitter = smp->jitter != 0; S.sampler.seed = smp->seed;
+    S.sampler.randomize = smp->randomize;
     S.resX = film->res_x; S.resY = film->res_y;
+    if (smp->kind == RT_SAMPLER_SOBOL) S.sampler.InitSobol(film->res_x, film->res_y);
     S.filter.kind = film->filter; S.filter.rx = film->filter_radius[0]; S.filter.ry = film->filter_radius[1];
     S.filter.Init(film->filter_param);
     S.imagingRatio = film->imaging_ratio;

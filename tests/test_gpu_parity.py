@@ -258,3 +258,14 @@ def test_cameras_and_filters_bitexact(oracle_lib, cam, filt):
     fo = oracle_lib.OracleScene(cfg).render(0, 4)
     assert (fo[:, 0] > 0).mean() > 0.05
     assert np.array_equal(bits(fg), bits(fo))
+
+
+@pytest.mark.parametrize("randomize", [0, 1, 2, 3])
+def test_sobol_sampler_bitexact(oracle_lib, randomize):
+    """SobolSampler (samplers.h:229-327) with the build's matrices: Cornell path mode (None / PermuteDigits /
+    FastOwen / Owen), including the interval-to-index pixel mapping and the dimension wrap at 32."""
+    cfg = scene.cfg_cornell(res=(48, 40), spp_side=4, max_depth=8)
+    cfg.sampler = scene.SobolSampler(samples_per_pixel=16, randomize=randomize, seed=3)
+    fg = Renderer(cfg).render_pass(0, 6)
+    fo = oracle_lib.OracleScene(cfg).render(0, 6)
+    assert np.array_equal(bits(fg), bits(fo))
