@@ -1072,7 +1072,36 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         (rc = up(shapes.data(), shapes.size() * sizeof(DevShape), &psh)) ||
         (rc = up(lights.data(), lights.size() * sizeof(DevLight), &plt)))
         return rc;
+    // single-leaf octree: conservative boxes of runs of kClusterTris leaf tiles (pass-1 culling in the kernel); a
+    // box miss means none of its triangles can pass the watertight test's tMax-independent checks, so the
+    // inflation (1e-4 of the scene extent + 1e-3) only has to cover those checks' rounding
+    std::vector<float4> clus[2];
+    if (qcap == 1) {
+        const std::vector<float4>* tl[2] = {&tiles0, &tiles1};
+        const auto& R = ob.nodes[0];
+        float ext = std::max(std::max(R.mx.x - R.mn.x, R.mx.y - R.mn.y), R.mx.z - R.mn.z);
+        float pad = 1e-4f * ext + 1e-3f;
+        for (int st = 0; st < 2; ++st) {
+            int nt_leaf = (int)tl[st]->size() / 3;
+            for (int k0 = 0; k0 < nt_leaf; k0 += kClusterTris) {
+                float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+                for (int k = k0; k < std::min(nt_leaf, k0 + kClusterTris); ++k) {
+                    const float4* q = tl[st]->data() + 3 * k;
+                    float v[9] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w, q[2].x};
+                    for (int j = 0; j < 3; ++j)
+                        for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], v[3 * j + a]); mx[a] = std::max(mx[a], v[3 * j + a]); }
+                }
+                clus[st].push_back(make_float4(mn[0] - pad, mn[1] - pad, mn[2] - pad, 0.f));
+                clus[st].push_back(make_float4(mx[0] + pad, mx[1] + pad, mx[2] + pad, 0.f));
+            }
+        }
+    }
+    void *pc0 = nullptr, *pc1 = nullptr;
+    if ((rc = up(clus[0].data(), clus[0].size() * 16, &pc0)) || (rc = up(clus[1].data(), clus[1].size() * 16, &pc1)))
+        return rc;
     DevScene& d = c->dsc;
+    d.clusters[0] = (const float4*)pc0; d.clusters[1] = (const float4*)pc1;
+    d.n_clusters[0] = (int)clus[0].size() / 2; d.n_clusters[1] = (int)clus[1].size() / 2;
     d.nodeA = (const float4*)pA; d.nodeB = (const float4*)pB;
     d.leafRange[0] = (const int2*)pl0; d.leafRange[1] = (const int2*)pl1;
     d.tiles[0] = (const float4*)pt0; d.tiles[1] = (const float4*)pt1;

@@ -95,6 +95,8 @@ struct DevScene {
     int mis;                        // RT_INTEGRATOR_PATH_MIS
     int full;                       // path shading needs the general kernel (shapes, specular, >1 / non-quad lights, MIS)
     DevLight light0;
+    const float4* clusters[2];      // single-leaf scenes: (pmin, pmax) of each run of kClusterTris leaf tiles, inflated
+    int n_clusters[2];
     int qcap;                       // BFS group FIFO size (compiled variants); 0 = global-memory ring below
     int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
     int ring_mask;
@@ -131,7 +133,11 @@ struct GenOut {
 // kz, Shapes.h:1145): bin b holds rays at ray[b*bstride + i], i < count[b*cstride].  Entries are addressed by
 // a flat index k over bin 0, then 1, then 2, so every wave but the two at bin seams sees one kz.
 static const int kQStride = 64;
-static const int kBlockThreads = 256;  // threads per block of every kernel  // ints between queue counters: 256 B apart, never in one cache line
+static const int kBlockThreads = 256;  // threads per block of every kernel
+#ifndef RT_CLUSTER_TRIS
+#define RT_CLUSTER_TRIS 2
+#endif
+static const int kClusterTris = RT_CLUSTER_TRIS;  // leaf tiles per culling cluster (single-leaf scenes)  // ints between queue counters: 256 B apart, never in one cache line
 
 struct TraceIO {
     const float4* rayO; const float4* rayD;

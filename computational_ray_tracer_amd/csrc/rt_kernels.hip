@@ -31,6 +31,12 @@ __shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by eve
 #ifndef RT_TWO_PASS
 #define RT_TWO_PASS 1        // single-leaf scenes: cheap candidate pass over all triangles, full test on survivors
 #endif
+#ifndef RT_CLUSTER
+#define RT_CLUSTER 1         // single-leaf scenes: shadow rays skip triangle runs whose conservative box no lane of
+#endif                       // a wave reaches within tMax (2: closest-hit rays too; A/B: helps shadows only)
+#ifndef RT_RAY_SORT
+#define RT_RAY_SORT 0        // path queues: each block writes its rays ordered by major direction (6 keys)
+#endif
 #ifndef RT_KZ_BINS
 #define RT_KZ_BINS 0         // 1: path-mode ray queues split into dominant-axis bins (Cornell A/B: trace -7%, shade +23%)
 #endif
@@ -99,6 +105,37 @@ __device__ __forceinline__ long block_append_bin(int* counters, int bin, size_t 
     if (bin >= 0) pos = (long)bin * (long)bstride + lds[3 * NW + bin] + lds[bin * NW + wave] + rank;
     __syncthreads();
     return pos;
+}
+// Block-aggregated append into one contiguous chunk ordered by key (0..K-1; -1 = nothing to append), one atomicAdd
+// per block: the block's rays leave grouped by key, so the next launch's waves are direction-coherent.
+template <int K>
+__device__ __forceinline__ long block_append_sorted(int* counter, int key, int* lds) {
+    constexpr int NW = kBlock / 64;
+    int wave = threadIdx.x >> 6;
+    int rank = 0;
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        uint64_t mask = __ballot(key == b);
+        if (key == b)
+            rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (lane_id() == 0) lds[b * NW + wave] = __popcll(mask);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int i = 0; i < K * NW; ++i) { int cw = lds[i]; lds[i] = tot; tot += cw; }
+        lds[K * NW] = tot ? atomicAdd(counter, tot) : 0;
+    }
+    __syncthreads();
+    long pos = key >= 0 ? (long)lds[K * NW] + lds[key * NW + wave] + rank : -1;
+    __syncthreads();
+    return pos;
+}
+// major direction of a ray: dominant axis and its sign (6 keys)
+__device__ __forceinline__ int major_dir(V3 d) {
+    int k = dominant_axis(d);
+    float c = k == 0 ? d.x : (k == 1 ? d.y : d.z);
+    return 2 * k + (c < 0 ? 1 : 0);
 }
 // flat queue index -> element position (bins 0, 1, 2 of lengths c0, c1, rest)
 __device__ __forceinline__ size_t queue_pos(int k, int c0, int c1, size_t bstride) {
@@ -293,6 +330,27 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 // error-bound tail run per candidate, not once per triangle for whichever lane reached it
                 uint64_t cand = 0;
                 int k = 0;
+#if RT_CLUSTER
+                // conservative cluster boxes first: a cluster no lane of the wave reaches is skipped whole
+                // (closest hit: the box over [0, inf); any hit: over [0, tMax], exact for a fixed tMax)
+                const float4* cl = sc.clusters[set];
+                if ((ANYHIT || RT_CLUSTER > 1) && sc.n_clusters[set] * kClusterTris >= r.y) {
+                    const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
+                    for (int c = 0; c < sc.n_clusters[set]; ++c) {
+                        bool hb = box_hit(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t);
+                        if (__ballot(hb) == 0) continue;
+#pragma unroll
+                        for (int u = 0; u < kClusterTris; ++u) {
+                            int kk = c * kClusterTris + u;
+                            if (kk >= r.y) break;
+                            int e = 3 * (r.x + kk);
+                            if (hb && tri_candidate<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2)))
+                                cand |= 1ull << kk;
+                        }
+                    }
+                    k = r.y;
+                }
+#endif
                 for (; k + U <= r.y; k += U) {
                     int e = 3 * (r.x + k);
                     float4 T[3 * U];
@@ -579,7 +637,7 @@ template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
                                                        SampleIds ids, PathIO io, unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
-    __shared__ int lds[4 * (kBlock / 64) + 3];
+    __shared__ int lds[6 * (kBlock / 64) + 8];
     int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
     int n = c0 + c1 + c2;
     unsigned long long snn = 0, snt = 0, nsh = 0;
@@ -705,7 +763,11 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                 store8(io.LA, io.LB, slot, L);
             }
         }
+#if RT_RAY_SORT
+        long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
+#else
         long pn = block_append_bin(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
+#endif
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
     }
     count_add(ctr, C_SNODES, snn);
@@ -751,7 +813,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
                                                             DevFilm film, SampleIds ids, PathIO io,
                                                             unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
-    __shared__ int lds[4 * (kBlock / 64) + 3];
+    __shared__ int lds[6 * (kBlock / 64) + 8];
     int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
     int n = c0 + c1 + c2;
     unsigned long long snn = 0, snt = 0, nsh = 0;
@@ -969,7 +1031,11 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
                 }
             }
         }
+#if RT_RAY_SORT
+        long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
+#else
         long pn = block_append_bin(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
+#endif
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
     }
     count_add(ctr, C_SNODES, snn);
