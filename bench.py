@@ -60,6 +60,13 @@ def kernel_rooflines(st, traffic):
         "k_path_shade": (st["ms_shade"], st["launches_shade"], 312 * st["rays"] + 32 * st["shadow_rays"],
                          32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"]),
     }
+    if st["launches_trace"] == 0 and st["rays"] > 0:
+        # fused bounce (simple scenes): k_path_shade also casts the bounce's closest-hit rays, so it carries
+        # both units of §8(d) work: 40 B per ray cast + 312 B per shaded bounce + 32 B per shadow ray
+        del ks["k_trace_closest"]
+        ks["k_path_shade"] = (st["ms_shade"], st["launches_shade"], (40 + 312) * st["rays"] + 32 * st["shadow_rays"],
+                              32 * (st["nodes_tested"] + st["shadow_nodes_tested"])
+                              + 40 * (st["tris_tested"] + st["shadow_tris_tested"]))
     res = {}
     for name, (ms, launches, stream_b, scene_b) in ks.items():
         launches = max(1, launches)
@@ -100,7 +107,22 @@ def cpu_baseline(cfg, seconds):
             nidx = min(spp, int(nidx * grow))
     n = len(pix) * nidx
     ms = n / dt / 1e6
+    # single-thread figure: the same band's first rows on one thread, ~1/8 of the budget
+    r1 = max(1, min(rows, int(rows / threads / 8)))
+    p1 = pix[: r1 * W]
+    t0 = time.perf_counter()
+    o.render(0, nidx, nthreads=1, pixel_ids=p1)
+    dt1 = time.perf_counter() - t0
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": round(ms, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "single_thread": round(len(p1) * nidx / dt1 / 1e6, 4), "cpu_model": model,
             "sample": f"oracle C++ restatement (same octree BFS, watertight test, path integrator), {n} samples = "
                       f"{rows} full rows of the {W}x{H} Cornell frame x sample indices 0..{nidx - 1}, "
                       f"{threads} threads, {dt:.1f} s"}

@@ -418,18 +418,38 @@ RT_DEV bool tri_intersect(const TriRay& R, float tMax, float4 A, float4 B, float
     return true;
 }
 
+// One vertex translated, permuted and sheared exactly as tri_intersect does it: a pure function of the vertex and
+// the ray, so a vertex shared by two triangles is transformed once.
+struct XV {
+    float x, y, z;
+};
+template <int KZ>
+RT_DEV XV tri_xform(const TriRay& R, float a, float b, float c) {
+    constexpr int KX = KZ == 0 ? 1 : (KZ == 1 ? 2 : 0), KY = KZ == 0 ? 2 : (KZ == 1 ? 0 : 1);
+    const int kx = KZ >= 0 ? KX : R.kx, ky = KZ >= 0 ? KY : R.ky, kz = KZ >= 0 ? KZ : R.kz;
+    XV v;
+    v.x = sel3(kx, a, b, c) - R.ox; v.y = sel3(ky, a, b, c) - R.oy; v.z = sel3(kz, a, b, c) - R.oz;
+    v.x += R.Sx * v.z; v.y += R.Sy * v.z;
+    return v;
+}
+RT_DEV bool tri_candidate_x(const TriRay& R, XV q0, XV q1, XV q2);
 // The tMax-independent rejections of tri_intersect (same operations, same order): false means the reference
 // test rejects this triangle for every tMax, so a caller may skip it without changing any result.
 template <int KZ>
 RT_DEV bool tri_candidate(const TriRay& R, float4 A, float4 B, float4 Cc) {
-    constexpr int KX = KZ == 0 ? 1 : (KZ == 1 ? 2 : 0), KY = KZ == 0 ? 2 : (KZ == 1 ? 0 : 1);
-    const int kx = KZ >= 0 ? KX : R.kx, ky = KZ >= 0 ? KY : R.ky, kz = KZ >= 0 ? KZ : R.kz;
-    float p0x = sel3(kx, A.x, A.y, A.z) - R.ox, p0y = sel3(ky, A.x, A.y, A.z) - R.oy, p0z = sel3(kz, A.x, A.y, A.z) - R.oz;
-    float p1x = sel3(kx, A.w, B.x, B.y) - R.ox, p1y = sel3(ky, A.w, B.x, B.y) - R.oy, p1z = sel3(kz, A.w, B.x, B.y) - R.oz;
-    float p2x = sel3(kx, B.z, B.w, Cc.x) - R.ox, p2y = sel3(ky, B.z, B.w, Cc.x) - R.oy, p2z = sel3(kz, B.z, B.w, Cc.x) - R.oz;
-    p0x += R.Sx * p0z; p0y += R.Sy * p0z;
-    p1x += R.Sx * p1z; p1y += R.Sy * p1z;
-    p2x += R.Sx * p2z; p2y += R.Sy * p2z;
+    return tri_candidate_x(R, tri_xform<KZ>(R, A.x, A.y, A.z), tri_xform<KZ>(R, A.w, B.x, B.y),
+                           tri_xform<KZ>(R, B.z, B.w, Cc.x));
+}
+// A fan pair (a,b,c),(a,c,d) — the host flags tile pairs whose second triangle starts with the first one's
+// vertices 0 and 2 bit for bit — transforms 4 vertices instead of 6.  Bit i of the result = triangle i passes.
+template <int KZ>
+RT_DEV unsigned tri_candidate_pair(const TriRay& R, float4 A, float4 B, float4 Cc, float4 B2, float4 C2) {
+    XV v0 = tri_xform<KZ>(R, A.x, A.y, A.z), v1 = tri_xform<KZ>(R, A.w, B.x, B.y);
+    XV v2 = tri_xform<KZ>(R, B.z, B.w, Cc.x), v3 = tri_xform<KZ>(R, B2.z, B2.w, C2.x);
+    return (tri_candidate_x(R, v0, v1, v2) ? 1u : 0u) | (tri_candidate_x(R, v0, v2, v3) ? 2u : 0u);
+}
+RT_DEV bool tri_candidate_x(const TriRay& R, XV q0, XV q1, XV q2) {
+    float p0x = q0.x, p0y = q0.y, p0z = q0.z, p1x = q1.x, p1y = q1.y, p1z = q1.z, p2x = q2.x, p2y = q2.y, p2z = q2.z;
     float e0 = dop(p1x, p2y, p1y, p2x);
     float e1 = dop(p2x, p0y, p2y, p0x);
     float e2 = dop(p0x, p1y, p0y, p1x);

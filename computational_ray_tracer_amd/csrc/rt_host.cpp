@@ -589,6 +589,13 @@ int check_ready(rt_ctx* c) {
     return RT_OK;
 }
 
+#ifndef RT_CLUSTER_PAD_REL
+#define RT_CLUSTER_PAD_REL 1e-5f  // cluster-box inflation per unit of scene extent (see upload)
+#endif
+#ifndef RT_FUSED_BOUNCE
+#define RT_FUSED_BOUNCE 0
+#endif
+
 // one render pass over [ib, ie) into the device film
 int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     int rc = check_ready(c);
@@ -647,11 +654,15 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 int* qc_cur = c->d_qcount + 3 * kQStride * cur;
                 int* qc_nxt = c->d_qcount + 3 * kQStride * nxt;
                 HIPCHK(c, hipMemsetAsync(qc_nxt, 0, 3 * kQStride * sizeof(int), st));
-                TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, c->hitB, c->hitPrim};
-                e0 = ev_start(c, st);
-                HIPCHK(c, launch_trace_closest(st, c->grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
-                ev_mark(c, st, ST_TRACE, e0);
+                const bool fused = RT_FUSED_BOUNCE && !c->dsc.full;  // simple scenes: trace inside the shade kernel
+                if (!fused) {
+                    TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, c->hitB, c->hitPrim};
+                    e0 = ev_start(c, st);
+                    HIPCHK(c, launch_trace_closest(st, c->grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
+                    ev_mark(c, st, ST_TRACE, e0);
+                }
                 PathIO pio{};
+                pio.fused = fused ? 1 : 0;
                 pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = qc_cur;
                 pio.hitB = c->hitB; pio.hitPrim = c->hitPrim;
                 pio.nO = c->rayO + (size_t)nxt * qs; pio.nD = c->rayD + (size_t)nxt * qs;
@@ -1074,13 +1085,18 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         return rc;
     // single-leaf octree: conservative boxes of runs of kClusterTris leaf tiles (pass-1 culling in the kernel); a
     // box miss means none of its triangles can pass the watertight test's tMax-independent checks, so the
-    // inflation (1e-4 of the scene extent + 1e-3) only has to cover those checks' rounding
+    // inflation only has to cover those checks' rounding.  In the sheared frame every vertex coordinate carries
+    // at most ~4 ulp(M) of error, M = the largest |vertex - origin|; with origins inside 8 extents of the scene
+    // centre (cl_guard; farther rays never skip) M <= 9.8 ext, i.e. <= 2.4e-6 ext, and the pad is 1e-5 ext +
+    // 1e-3 — small enough that a wave of rays leaving one wall (origin offset 1e-4 (1 + max|p|)) skips it.
     std::vector<float4> clus[2];
     if (qcap == 1) {
         const std::vector<float4>* tl[2] = {&tiles0, &tiles1};
         const auto& R = ob.nodes[0];
         float ext = std::max(std::max(R.mx.x - R.mn.x, R.mx.y - R.mn.y), R.mx.z - R.mn.z);
-        float pad = 1e-4f * ext + 1e-3f;
+        float pad = RT_CLUSTER_PAD_REL * ext + 1e-3f;
+        c->dsc.cl_guard = make_float4(.5f * (R.mn.x + R.mx.x), .5f * (R.mn.y + R.mx.y), .5f * (R.mn.z + R.mx.z),
+                                      64.f * ext * ext);
         for (int st = 0; st < 2; ++st) {
             int nt_leaf = (int)tl[st]->size() / 3;
             for (int k0 = 0; k0 < nt_leaf; k0 += kClusterTris) {
@@ -1094,6 +1110,28 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
                 clus[st].push_back(make_float4(mn[0] - pad, mn[1] - pad, mn[2] - pad, 0.f));
                 clus[st].push_back(make_float4(mx[0] + pad, mx[1] + pad, mx[2] + pad, 0.f));
             }
+            // then the boxes of runs of kSuperClusters clusters (the union of their inflated boxes)
+            int nc = (int)clus[st].size() / 2;
+            for (int s0 = 0; kSuperClusters > 0 && s0 < nc; s0 += kSuperClusters) {
+                float4 a = clus[st][2 * s0], b = clus[st][2 * s0 + 1];
+                for (int k = s0 + 1; k < std::min(nc, s0 + kSuperClusters); ++k) {
+                    const float4 &ka = clus[st][2 * k], &kb = clus[st][2 * k + 1];
+                    a.x = std::min(a.x, ka.x); a.y = std::min(a.y, ka.y); a.z = std::min(a.z, ka.z);
+                    b.x = std::max(b.x, kb.x); b.y = std::max(b.y, kb.y); b.z = std::max(b.z, kb.z);
+                }
+                clus[st].push_back(a);
+                clus[st].push_back(b);
+            }
+            c->dsc.n_clusters[st] = nc;
+            // fan pairs: tile k+1 = (a, c, d) after tile k = (a, b, c), bit for bit (_quad / OBJ fan triangulation)
+            unsigned long long fp = 0;
+            for (int k = 0; k + 1 < std::min(nt_leaf, 64); k += 2) {
+                const float4* q = tl[st]->data() + 3 * k;
+                float v[9] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w, q[2].x};
+                float w[9] = {q[3].x, q[3].y, q[3].z, q[3].w, q[4].x, q[4].y, q[4].z, q[4].w, q[5].x};
+                if (!std::memcmp(w, v, 12) && !std::memcmp(w + 3, v + 6, 12)) fp |= 1ull << k;
+            }
+            c->dsc.fan_pairs[st] = fp;
         }
     }
     void *pc0 = nullptr, *pc1 = nullptr;
@@ -1101,7 +1139,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         return rc;
     DevScene& d = c->dsc;
     d.clusters[0] = (const float4*)pc0; d.clusters[1] = (const float4*)pc1;
-    d.n_clusters[0] = (int)clus[0].size() / 2; d.n_clusters[1] = (int)clus[1].size() / 2;
+    if (qcap != 1) d.n_clusters[0] = d.n_clusters[1] = 0;
     d.nodeA = (const float4*)pA; d.nodeB = (const float4*)pB;
     d.leafRange[0] = (const int2*)pl0; d.leafRange[1] = (const int2*)pl1;
     d.tiles[0] = (const float4*)pt0; d.tiles[1] = (const float4*)pt1;
@@ -1324,6 +1362,31 @@ int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_c
     if (!rc)
         for (int i = 0; i < n; ++i)
             if (prim[i] < 0) bt[4 * i] = bt[4 * i + 1] = bt[4 * i + 2] = bt[4 * i + 3] = 0.f;
+    return rc;
+}
+
+int rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float* rd, const float* tmax, int32_t* occluded) {
+    if (!c || n < 0 || (n && (!ro || !rd || !tmax || !occluded))) return RT_E_ARG;
+    if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
+    if (n == 0) return RT_OK;
+    hipSetDevice(c->device);
+    std::vector<float4> o(n), d(n);
+    for (int i = 0; i < n; ++i) {
+        o[i] = make_float4(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2], 0.f);
+        d[i] = make_float4(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2], tmax[i]);
+    }
+    float4 *dO = nullptr, *dD = nullptr;
+    int* dP = nullptr;
+    int rc = RT_OK;
+    if (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dP, n)) rc = fail(c, RT_E_OOM, "debug occlusion buffers");
+    if (!rc &&
+        (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+         launch_occluded(c->stream, c->dsc.qcap, c->dsc, n, dO, dD, dP, c->d_ctr) != hipSuccess ||
+         hipStreamSynchronize(c->stream) != hipSuccess ||
+         hipMemcpy(occluded, dP, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = fail(c, RT_E_HIP, std::string("debug occlusion: ") + hipGetErrorString(hipGetLastError()));
+    hipFree(dO); hipFree(dD); hipFree(dP);
     return rc;
 }
 

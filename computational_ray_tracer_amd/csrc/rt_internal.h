@@ -95,8 +95,11 @@ struct DevScene {
     int mis;                        // RT_INTEGRATOR_PATH_MIS
     int full;                       // path shading needs the general kernel (shapes, specular, >1 / non-quad lights, MIS)
     DevLight light0;
-    const float4* clusters[2];      // single-leaf scenes: (pmin, pmax) of each run of kClusterTris leaf tiles, inflated
+    const float4* clusters[2];      // single-leaf scenes: (pmin, pmax) of each run of kClusterTris leaf tiles, inflated,
+                                    // followed by the boxes of runs of kSuperClusters clusters
     int n_clusters[2];
+    float4 cl_guard;                  // (centre, radius²): rays starting farther out never skip a cluster
+    unsigned long long fan_pairs[2];  // single-leaf scenes: bit k (k even) = tiles k, k+1 are a fan pair (a,b,c),(a,c,d)
     int qcap;                       // BFS group FIFO size (compiled variants); 0 = global-memory ring below
     int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
     int ring_mask;
@@ -137,6 +140,10 @@ static const int kBlockThreads = 256;  // threads per block of every kernel
 #ifndef RT_CLUSTER_TRIS
 #define RT_CLUSTER_TRIS 2
 #endif
+#ifndef RT_SUPER_CLUSTERS
+#define RT_SUPER_CLUSTERS 0
+#endif
+static const int kSuperClusters = RT_SUPER_CLUSTERS;  // clusters per super-cluster box (0: none)
 static const int kClusterTris = RT_CLUSTER_TRIS;  // leaf tiles per culling cluster (single-leaf scenes)  // ints between queue counters: 256 B apart, never in one cache line
 
 struct TraceIO {
@@ -165,6 +172,7 @@ struct PathIO {
     const float4* lamA; const float4* lamB; float4* pdfA; float4* pdfB;  // pdf: TerminateSecondary writes it
     float* prevPdf;                                                       // pdf of the last diffuse bounce
     int depth, max_depth;
+    int fused;  // simple scenes: the closest-hit traversal runs inside the shade kernel (no hit records)
 };
 
 struct PathFilmIO {
@@ -184,6 +192,8 @@ hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& id
                            const DevSampler& smp, const DevFilm& film, const GenOut& out);
 hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
                                 unsigned long long* ctr);
+hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
+                           int* out, unsigned long long* ctr);
 hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
                                  const ShadeRefIO& io, unsigned long long* ctr);
 hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,

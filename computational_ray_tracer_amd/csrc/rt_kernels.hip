@@ -32,8 +32,15 @@ __shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by eve
 #define RT_TWO_PASS 1        // single-leaf scenes: cheap candidate pass over all triangles, full test on survivors
 #endif
 #ifndef RT_CLUSTER
-#define RT_CLUSTER 1         // single-leaf scenes: shadow rays skip triangle runs whose conservative box no lane of
-#endif                       // a wave reaches within tMax (2: closest-hit rays too; A/B: helps shadows only)
+#define RT_CLUSTER 3         // single-leaf scenes: skip triangle runs whose conservative box no lane of a wave
+#endif                       // reaches.  1: shadow rays only; 2: every ray; 3: shadow rays and closest-hit waves
+                             // whose rays share a dominant axis (camera rays)
+#ifndef RT_FAN_PAIRS
+#define RT_FAN_PAIRS 1       // single-leaf scenes: fan-triangulated quads transform their 4 vertices once per ray
+#endif
+#ifndef RT_TRACE_KZSORT
+#define RT_TRACE_KZSORT 0    // closest-hit launches regroup each block's rays by dominant axis in LDS
+#endif
 #ifndef RT_RAY_SORT
 #define RT_RAY_SORT 0        // path queues: each block writes its rays ordered by major direction (6 keys)
 #endif
@@ -131,6 +138,30 @@ __device__ __forceinline__ long block_append_sorted(int* counter, int key, int* 
     __syncthreads();
     return pos;
 }
+// Position of this thread's item when the block's items are ordered by key (0..K-1), stable within a key.
+// Every thread of the block must call it.
+template <int K>
+__device__ __forceinline__ int block_rank(int key, int* lds) {
+    constexpr int NW = kBlock / 64;
+    int wave = threadIdx.x >> 6;
+    int rank = 0;
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        uint64_t mask = __ballot(key == b);
+        if (key == b)
+            rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        if (lane_id() == 0) lds[b * NW + wave] = __popcll(mask);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int i = 0; i < K * NW; ++i) { int cw = lds[i]; lds[i] = tot; tot += cw; }
+    }
+    __syncthreads();
+    int pos = lds[key * NW + wave] + rank;
+    __syncthreads();
+    return pos;
+}
 // major direction of a ray: dominant axis and its sign (6 keys)
 __device__ __forceinline__ int major_dir(V3 d) {
     int k = dominant_axis(d);
@@ -144,6 +175,10 @@ __device__ __forceinline__ size_t queue_pos(int k, int c0, int c1, size_t bstrid
     return 2 * bstride + (size_t)(k - c0 - c1);
 }
 
+// the PCG increment of a path never changes after generation: only the 8-byte state half is written back
+__device__ __forceinline__ void store_rng_state(uint4* rng, int slot, uint64_t state) {
+    reinterpret_cast<uint2*>(rng)[2 * slot] = make_uint2((uint32_t)state, (uint32_t)(state >> 32));
+}
 __device__ __forceinline__ void count_add(unsigned long long* ctr, int slot, unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -323,6 +358,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 return false;
             };
             constexpr int U = RT_TRI_UNROLL;
+            static_assert(U % 2 == 0, "pass 1 walks fan pairs");
 #if RT_TWO_PASS
             if (r.y <= 64) {
                 // pass 1: every triangle's tMax-independent rejections (scalar-cache batches); pass 2: the full
@@ -330,15 +366,37 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 // error-bound tail run per candidate, not once per triangle for whichever lane reached it
                 uint64_t cand = 0;
                 int k = 0;
+                const uint64_t fp = sc.fan_pairs[set];  // bit k: leaf tiles k, k+1 share vertices (a,b,c),(a,c,d)
 #if RT_CLUSTER
                 // conservative cluster boxes first: a cluster no lane of the wave reaches is skipped whole
                 // (closest hit: the box over [0, inf); any hit: over [0, tMax], exact for a fixed tMax)
                 const float4* cl = sc.clusters[set];
-                if ((ANYHIT || RT_CLUSTER > 1) && sc.n_clusters[set] * kClusterTris >= r.y) {
+                const int ncl = sc.n_clusters[set];
+                constexpr bool kCull = ANYHIT || RT_CLUSTER == 2 || (RT_CLUSTER == 3 && KZ >= 0);
+                if (kCull && ncl * kClusterTris >= r.y) {
                     const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
-                    for (int c = 0; c < sc.n_clusters[set]; ++c) {
-                        bool hb = box_hit(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t);
+                    const float gx = o.x - sc.cl_guard.x, gy = o.y - sc.cl_guard.y, gz = o.z - sc.cl_guard.z;
+                    const bool far = gx * gx + gy * gy + gz * gz > sc.cl_guard.w;  // pad not sized for it
+                    bool hs = true;
+                    for (int c = 0; c < ncl; ++c) {
+                        if constexpr (kSuperClusters > 0) {
+                            constexpr int S = kSuperClusters > 0 ? kSuperClusters : 1;
+                            if (c % S == 0) {
+                                const int sb = 2 * (ncl + c / S);
+                                hs = far || box_hit(ldc4(cl, sb), ldc4(cl, sb + 1), o, inv, cl_t);
+                                if (__ballot(hs) == 0) { c += S - 1; continue; }
+                            }
+                        }
+                        bool hb = far || (hs && box_hit(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t));
                         if (__ballot(hb) == 0) continue;
+                        if (RT_FAN_PAIRS && kClusterTris == 2 && ((fp >> (2 * c)) & 1)) {
+                            int e = 3 * (r.x + 2 * c);
+                            if (hb)
+                                cand |= (uint64_t)tri_candidate_pair<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1),
+                                                                         ldc4(tiles, e + 2), ldc4(tiles, e + 4),
+                                                                         ldc4(tiles, e + 5)) << (2 * c);
+                            continue;
+                        }
 #pragma unroll
                         for (int u = 0; u < kClusterTris; ++u) {
                             int kk = c * kClusterTris + u;
@@ -357,14 +415,25 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
 #pragma unroll
                     for (int j = 0; j < 3 * U; ++j) T[j] = ldc4(tiles, e + j);
 #pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        if (tri_candidate<KZ>(R, T[3 * u], T[3 * u + 1], T[3 * u + 2])) cand |= 1ull << (k + u);
+                    for (int u = 0; u < U; u += 2) {
+                        if (RT_FAN_PAIRS && ((fp >> (k + u)) & 1)) {  // wave-uniform: a scalar branch
+                            cand |= (uint64_t)tri_candidate_pair<KZ>(R, T[3 * u], T[3 * u + 1], T[3 * u + 2],
+                                                                     T[3 * u + 4], T[3 * u + 5]) << (k + u);
+                        } else {
+                            if (tri_candidate<KZ>(R, T[3 * u], T[3 * u + 1], T[3 * u + 2])) cand |= 1ull << (k + u);
+                            if (tri_candidate<KZ>(R, T[3 * u + 3], T[3 * u + 4], T[3 * u + 5]))
+                                cand |= 1ull << (k + u + 1);
+                        }
+                    }
                 }
                 for (; k < r.y; ++k) {
                     int e = 3 * (r.x + k);
                     if (tri_candidate<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2))) cand |= 1ull << k;
                 }
                 nt += r.y;
+#ifdef RT_PROFILE_NO_PASS2  // timing experiments only: results are wrong
+                cand = 0;
+#endif
                 while (cand) {
                     int j = __builtin_ctzll(cand);
                     cand &= cand - 1;
@@ -524,9 +593,34 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
     if (io.count) { c0 = io.count[0]; c1 = io.count[kQStride]; c2 = io.count[2 * kQStride]; }
     int n = c0 + c1 + c2;
     unsigned long long nn = 0, nt = 0, nh = 0, nr = 0;
+#if RT_TRACE_KZSORT
+    // The block's rays are regrouped by dominant axis through LDS before traversal, so most waves take the
+    // compile-time-permuted watertight test; hits are written back at the rays' own queue positions.
+    __shared__ float4 s_o[kBlock], s_d[kBlock];
+    __shared__ int s_k[kBlock], s_lds[4 * (kBlock / 64)];
+    for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        {
+            int kk = base + threadIdx.x;
+            float4 oo = make_float4(0, 0, 0, 0), dd = oo;
+            int key = 3;
+            if (kk < n) {
+                size_t q = queue_pos(kk, c0, c1, io.bstride);
+                oo = io.rayO[q]; dd = io.rayD[q];
+                key = dominant_axis(v3(dd.x, dd.y, dd.z));
+            }
+            int p = block_rank<4>(key, s_lds);
+            s_o[p] = oo; s_d[p] = dd; s_k[p] = kk;
+            __syncthreads();
+        }
+        int k = s_k[threadIdx.x];
+        float4 o4 = s_o[threadIdx.x], d4 = s_d[threadIdx.x];
+        __syncthreads();
+        if (k >= n) continue;
+#else
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         size_t q = queue_pos(k, c0, c1, io.bstride);
         float4 o4 = io.rayO[q], d4 = io.rayD[q];
+#endif
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
         int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
                                              b0, b1, b2, t, nn, nt);
@@ -633,14 +727,24 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 // emitter hit → Le at depth 0 only (one-sided), then terminate; otherwise NEE on the quad light (Get2D,
 // shadow ray traced inline, pending contribution added on a miss) and a cosine-hemisphere bounce
 // (Get2D, β *= R) appended to the next queue.  Sampler state (PCG state + dimension) lives per path slot.
-template <int QCAP>
-__global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
+// FUSED: the bounce's closest-hit traversal runs here too (the ray is read once, the hit stays in registers), so
+// the VALU-bound traversal and the HBM-bound path-state traffic of different waves overlap on every CU.
+#ifndef RT_SHADE_WAVES
+#define RT_SHADE_WAVES 0     // >0: amdgpu_waves_per_eu floor for the path shade kernel (register budget)
+#endif
+#if RT_SHADE_WAVES > 0
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WAVES)))
+#else
+#define RT_SHADE_ATTR
+#endif
+template <int QCAP, bool FUSED>
+__global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
                                                        SampleIds ids, PathIO io, unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[6 * (kBlock / 64) + 8];
     int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
     int n = c0 + c1 + c2;
-    unsigned long long snn = 0, snt = 0, nsh = 0;
+    unsigned long long snn = 0, snt = 0, nsh = 0, tnn = 0, tnt = 0, tnh = 0, tnr = 0;
     for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         int k = base + threadIdx.x;
         bool wantShadow = false, wantNext = false;
@@ -654,7 +758,19 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
         if (k < n) {
             q = queue_pos(k, c0, c1, io.bstride);
             slot = io.slot[q];
-            int prim = io.hitPrim[k];
+            int prim;
+            float4 d4, hb;
+            if constexpr (FUSED) {
+                float4 o4 = io.rayO[q];
+                d4 = io.rayD[q];
+                hb = make_float4(0, 0, 0, 0);
+                prim = traverse_any<QCAP, false>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
+                                                 hb.x, hb.y, hb.z, hb.w, tnn, tnt);
+                tnh += prim >= 0;
+                tnr += 1;
+            } else {
+                prim = io.hitPrim[k];
+            }
             if (prim >= 0) {
                 float lam[8], beta[8];
                 load8(io.lamA, io.lamB, slot, lam);
@@ -662,7 +778,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                 float4 P0 = sc.triWorld[3 * prim], P1 = sc.triWorld[3 * prim + 1], P2 = sc.triWorld[3 * prim + 2];
                 V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
                 V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
-                float4 d4 = io.rayD[q];
+                if constexpr (!FUSED) d4 = io.rayD[q];
                 V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
                 DevMaterial dm = sc.materials[sc.triMaterial[prim]];
                 float4 mt = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
@@ -677,7 +793,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                 } else if (io.depth < io.max_depth) {
                     V3 nrm = ng;
                     if (vdot(nrm, rayd) > 0) nrm = v3(-nrm.x, -nrm.y, -nrm.z);
-                    float4 hb = io.hitB[k];
+                    if constexpr (!FUSED) hb = io.hitB[k];
                     V3 p = vadd(vadd(vmul(p0, hb.x), vmul(p1, hb.y)), vmul(p2, hb.z));
                     float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
                     V3 po = vadd(p, vmul(nrm, off));
@@ -740,7 +856,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
                     }
-                    io.rng[slot] = make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), rs.z, rs.w);
+                    store_rng_state(io.rng, slot, sm.rng.state);
                     io.dim[slot] = sm.dim;
                 }
             }
@@ -773,6 +889,12 @@ __global__ void __launch_bounds__(kBlock) k_path_shade(DevScene sc, const DevSpe
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
+    if constexpr (FUSED) {
+        count_add(ctr, C_NODES, tnn);
+        count_add(ctr, C_TRIS, tnt);
+        count_add(ctr, C_HITS, tnh);
+        count_add(ctr, C_RAYS, tnr);
+    }
 }
 
 // ------------------------------------------------------------------- path mode, general scenes (§8 a21/a22)
@@ -791,7 +913,7 @@ __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevF
     sm.px = x; sm.py = y; sm.index = index; sm.dim = io.dim[slot];
 }
 __device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm, uint4 rs) {
-    io.rng[slot] = make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), rs.z, rs.w);
+    store_rng_state(io.rng, slot, sm.rng.state);
     io.dim[slot] = sm.dim;
 }
 template <int QCAP>
@@ -806,6 +928,21 @@ __device__ __forceinline__ bool scene_occluded(const DevScene& sc, V3 o, V3 d, f
         if (shape_isect(sh, o, d, tmax, ph, th)) return true;
     }
     return false;
+}
+
+// parity entry: the shadow query of the path kernels on explicit rays (d.w = tmax)
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const float4* o, const float4* d, int* out,
+                                                     unsigned long long* ctr) {
+    unsigned long long nn = 0, nt = 0, ns = 0;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        float4 o4 = o[k], d4 = d[k];
+        out[k] = scene_occluded<QCAP>(sc, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, nn, nt) ? 1 : 0;
+        ++ns;
+    }
+    count_add(ctr, C_SNODES, nn);
+    count_add(ctr, C_STRIS, nt);
+    count_add(ctr, C_SHADOW, ns);
 }
 
 template <int QCAP>
@@ -1161,7 +1298,8 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
 #define RT_SHADE_CASE(Q)                                                                                         \
     case Q:                                                                                                      \
         if (sc.full) hipLaunchKernelGGL(k_path_shade_full<Q>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr);    \
-        else hipLaunchKernelGGL(k_path_shade<Q>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr);                 \
+        else if (io.fused) hipLaunchKernelGGL((k_path_shade<Q, true>), g, b, 0, st, sc, sp, smp, film, ids, io, ctr); \
+        else hipLaunchKernelGGL((k_path_shade<Q, false>), g, b, 0, st, sc, sp, smp, film, ids, io, ctr);          \
         break;
     switch (qcap) {
         RT_SHADE_CASE(0)
@@ -1170,6 +1308,20 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
         default: return hipErrorInvalidValue;
     }
 #undef RT_SHADE_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
+                           int* out, unsigned long long* ctr) {
+    int gb = grid_for(n, 0);
+    if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);
+    dim3 g(gb > 0 ? gb : 1), b(kBlock);
+    switch (qcap) {
+        case 0: hipLaunchKernelGGL(k_occluded<0>, g, b, 0, st, sc, n, o, d, out, ctr); break;
+        case 1: hipLaunchKernelGGL(k_occluded<1>, g, b, 0, st, sc, n, o, d, out, ctr); break;
+        case 16: hipLaunchKernelGGL(k_occluded<16>, g, b, 0, st, sc, n, o, d, out, ctr); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

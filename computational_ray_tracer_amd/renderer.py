@@ -98,6 +98,17 @@ class Renderer:
                                                             P(prim, C.c_int32), P(bt, C.c_float)))
         return prim, bt
 
+    def occluded(self, ro, rd, tmax):
+        """Shadow query of the path kernels (any hit within tmax): int32 0/1 per ray."""
+        ro = np.ascontiguousarray(ro, np.float32)
+        rd = np.ascontiguousarray(rd, np.float32)
+        tmax = np.ascontiguousarray(tmax, np.float32)
+        occ = np.zeros(len(ro), np.int32)
+        P = lambda a, t: a.ctypes.data_as(C.POINTER(t))
+        self._chk("rt_debug_occluded", self.lib.rt_debug_occluded(self.h, len(ro), P(ro, C.c_float), P(rd, C.c_float),
+                                                                  P(tmax, C.c_float), P(occ, C.c_int32)))
+        return occ
+
     def samples(self, pixel_ids, indices):
         pixel_ids = np.ascontiguousarray(pixel_ids, np.int32)
         indices = np.ascontiguousarray(indices, np.int32)

@@ -273,6 +273,9 @@ int rt_octree_export(rt_ctx* ctx, float* node_bounds, int32_t* node_child, int32
 /* K2 alone: closest hit of n world-space rays (ro, rd: 3n floats).  prim[n] (-1 = miss),
  * bt[4n] = (b0, b1, b2, t).  use_cull follows the reference's back-face flags. */
 int rt_debug_trace(rt_ctx* ctx, int n, const float* ro, const float* rd, int use_cull, int32_t* prim, float* bt);
+/* The path integrator's shadow query alone: any hit of n rays within (0, tmax[i]) against the octree and the
+ * analytic shapes (Octtree_Model.h:66-127 with the early exit, Shapes.h shape tests); occluded[n] = 0 / 1. */
+int rt_debug_occluded(rt_ctx* ctx, int n, const float* ro, const float* rd, const float* tmax, int32_t* occluded);
 /* K1..K3 for n explicit (pixel_id, index) samples (reference integrator). */
 int rt_debug_samples(rt_ctx* ctx, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out);
 

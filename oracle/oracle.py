@@ -70,6 +70,7 @@ def lib():
             "orc_octree_export": ([C.c_void_p, P(C.c_float), P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_int)], C.c_int),
             "orc_backface_flags": ([C.c_void_p, P(C.c_uint8)], C.c_int),
             "orc_trace": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), C.c_int, P(C.c_int), P(C.c_float), P(C.c_int64)], C.c_int),
+            "orc_occluded": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_int)], C.c_int),
             "orc_samples": ([C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(capi.rt_sample_record)], C.c_int),
             "orc_render": ([C.c_void_p, C.c_int, C.c_int, P(C.c_float), C.c_int, P(C.c_int64), P(C.c_int), C.c_int], C.c_int),
             "orc_resolve": ([C.c_void_p, P(C.c_float), P(C.c_uint8)], None),
@@ -140,6 +141,14 @@ class OracleScene:
         lib().orc_trace(self.h, n, fptr(ro), fptr(rd), int(use_cull), iptr(prim), fptr(bt),
                         cnt.ctypes.data_as(C.POINTER(C.c_int64)))
         return prim, bt, cnt
+
+    def occluded(self, ro, rd, tmax):
+        ro = np.ascontiguousarray(ro, np.float32)
+        rd = np.ascontiguousarray(rd, np.float32)
+        tmax = np.ascontiguousarray(tmax, np.float32)
+        occ = np.zeros(len(ro), np.int32)
+        lib().orc_occluded(self.h, len(ro), fptr(ro), fptr(rd), fptr(tmax), iptr(occ))
+        return occ
 
     def samples(self, pixel_ids, indices):
         from computational_ray_tracer_amd import capi

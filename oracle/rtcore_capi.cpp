@@ -366,6 +366,16 @@ int orc_trace(void* h, int n, const float* ro, const float* rd, int use_cull, in
     return 0;
 }
 
+// SceneOccluded (octree any hit, then analytic shapes), the path integrator's shadow query
+int orc_occluded(void* h, int n, const float* ro, const float* rd, const float* tmax, int* occluded) {
+    auto& S = static_cast<OracleScene*>(h)->S;
+    for (int i = 0; i < n; ++i) {
+        Ray r{{ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]}, {rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]}};
+        occluded[i] = SceneOccluded(S, r, tmax[i]) ? 1 : 0;
+    }
+    return 0;
+}
+
 int orc_samples(void* h, int n, const int* pixel_ids, const int* indices, rt_sample_record* out) {
     auto* o = static_cast<OracleScene*>(h);
     for (int i = 0; i < n; ++i) {

@@ -191,6 +191,12 @@ def test_cfg3_trace_random_rays_bitexact(cfg3_pair):
     assert (po >= 12).mean() > 0.3   # mesh triangles follow the 12 wall/light triangles
     assert np.array_equal(pg, po)
     assert np.array_equal(bits(bg), bits(bo))
+    # shadow query (LDS/HBM-ring FIFO traversal with early exit), tmax around the closest hit distance
+    t = np.where(po >= 0, bo[:, 3], 400.0)
+    tmax = (t * rng.choice([0.5, 0.999, 1.0, 1.001, 2.0], size=n)).astype(np.float32)
+    og = g.occluded(ro, rd, tmax)
+    assert np.array_equal(og, o.occluded(ro, rd, tmax))
+    assert 0.2 < og.mean() < 0.9
 
 
 def test_cfg3_path_film_bitexact(cfg3_pair):
@@ -222,6 +228,12 @@ def test_cfg4_trace_with_shapes_bitexact(cfg4_small, oracle_lib):
     assert (po >= ntri).mean() > 0.3
     assert np.array_equal(pg, po)
     assert np.array_equal(bits(bg), bits(bo))
+    # shadow query: octree any hit, then the shapes with the fixed tmax
+    t = np.where(po >= 0, bo[:, 3], 400.0)
+    tmax = (t * rng.choice([0.5, 0.999, 1.0, 1.001, 2.0], size=n)).astype(np.float32)
+    og = g.occluded(ro, rd, tmax)
+    assert np.array_equal(og, o.occluded(ro, rd, tmax))
+    assert 0.2 < og.mean() < 0.9
 
 
 @pytest.mark.parametrize("kind,depth", [("path", 5), ("mis", 5), ("mis", 1), ("path", 2)])
@@ -269,3 +281,57 @@ def test_sobol_sampler_bitexact(oracle_lib, randomize):
     fg = Renderer(cfg).render_pass(0, 6)
     fo = oracle_lib.OracleScene(cfg).render(0, 6)
     assert np.array_equal(bits(fg), bits(fo))
+
+
+def _cornell_surface_rays(model, rng, per_tri=64):
+    """Waves of 64 rays leaving one triangle of the Cornell box: origins on the surface offset along the normal by
+    0, the path integrator's 1e-4 (1 + max|p|), and values either side of the cluster-box pad; directions in the
+    hemisphere (so the waves are direction-coherent and exercise the cluster skipping of both traversals)."""
+    P = model.positions.astype(np.float64)[model.indices.astype(np.int64)][..., [0, 2, 1]]  # object -> world (perm_yz)
+    ro, rd = [], []
+    for t in range(len(P)):
+        a, b, c = P[t]
+        n = np.cross(b - a, c - a)
+        n /= np.linalg.norm(n)
+        u, v = rng.random(per_tri), rng.random(per_tri)
+        flip = u + v > 1
+        u[flip], v[flip] = 1 - u[flip], 1 - v[flip]
+        p = a + u[:, None] * (b - a) + v[:, None] * (c - a)
+        off = rng.choice([0.0, 1e-6, -1e-4, 1e-3, 0.006, 0.0066, 0.0072, 0.05], size=per_tri)
+        nee = 1e-4 * (1 + np.abs(p).max(axis=1))
+        off = np.where(rng.random(per_tri) < 0.5, nee, off)
+        for s in (1.0, -1.0):  # both sides of the surface
+            d = rng.normal(size=(per_tri, 3))
+            d *= np.sign(d @ (s * n))[:, None]
+            d /= np.linalg.norm(d, axis=1, keepdims=True)
+            ro.append(p + (s * off)[:, None] * n)
+            rd.append(d)
+    return np.concatenate(ro).astype(np.float32), np.concatenate(rd).astype(np.float32)
+
+
+def test_cornell_surface_rays_closest_and_occluded_bitexact(oracle_lib):
+    """Closest-hit and shadow (any-hit) queries from the box's own surfaces, in direction-coherent waves: the
+    single-leaf two-pass test, fan-pair vertex sharing and conservative cluster skipping must not change a bit."""
+    cfg = scene.cfg_cornell(res=(32, 32), spp_side=1)
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    rng = np.random.default_rng(11)
+    ro, rd = _cornell_surface_rays(cfg.model, rng)
+    pg, bg = g.trace(ro, rd, False)
+    po, bo, _ = o.trace(ro, rd, False)
+    assert np.array_equal(pg, po)
+    assert np.array_equal(bits(bg), bits(bo))
+    assert (pg >= 0).mean() > 0.4
+    # shadow queries: towards points on the light quad (tmax = 0.999 dist, as the integrator) and random tmax
+    L = cfg.model.lights[0]
+    u, v = rng.random(len(ro)), rng.random(len(ro))
+    tgt = np.asarray(L["p"]) + u[:, None] * np.asarray(L["e1"]) + v[:, None] * np.asarray(L["e2"])
+    w = tgt - ro.astype(np.float64)
+    dist = np.linalg.norm(w, axis=1)
+    sd = (w / dist[:, None]).astype(np.float32)
+    tmax = np.where(rng.random(len(ro)) < 0.7, 0.999 * dist, rng.random(len(ro)) * 800).astype(np.float32)
+    og = g.occluded(ro, sd, tmax)
+    oo = o.occluded(ro, sd, tmax)
+    assert np.array_equal(og, oo)
+    assert 0.05 < og.mean() < 0.95
+    og2 = g.occluded(ro, rd, tmax)
+    assert np.array_equal(og2, o.occluded(ro, rd, tmax))

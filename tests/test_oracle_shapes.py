@@ -92,3 +92,23 @@ def test_mis_and_nee_agree_on_cornell(oracle_lib):
         f = oracle_lib.OracleScene(cfg).render(0, 64, nthreads=8)
         means.append(f[:, :3].sum(0) / f[:, 3].sum())
     assert np.allclose(means[0], means[1], rtol=0.02), means
+
+
+def test_occluded_agrees_with_closest_hit(oracle_lib):
+    """SceneOccluded (the path integrator's shadow query: octree any hit, then shapes) reports a blocker exactly
+    when the closest hit lies inside (0, tmax), away from the rounding band at t ~ tmax."""
+    cfg = scene.cfg4_mixed(res=(16, 16), spp=(1, 1), frequency=4)
+    o = oracle_lib.OracleScene(cfg)
+    rng = np.random.default_rng(3)
+    n = 4000
+    ro = np.stack([rng.uniform(5, 550, n), rng.uniform(5, 543, n), rng.uniform(5, 554, n)], 1).astype(np.float32)
+    rd = rng.normal(size=(n, 3))
+    rd = (rd / np.linalg.norm(rd, axis=1, keepdims=True)).astype(np.float32)
+    p, bt, _ = o.trace(ro, rd, False)
+    t = np.where(p >= 0, bt[:, 3], np.inf)
+    tmax = rng.uniform(1, 700, n).astype(np.float32)
+    occ = o.occluded(ro, rd, tmax)
+    clear = np.abs(t - tmax) > 1e-3 * tmax
+    assert clear.mean() > 0.95
+    assert np.array_equal(occ[clear].astype(bool), (t < tmax)[clear])
+    assert 0.2 < occ.mean() < 0.8
