@@ -592,6 +592,9 @@ int check_ready(rt_ctx* c) {
 #ifndef RT_CLUSTER_PAD_REL
 #define RT_CLUSTER_PAD_REL 1e-5f  // cluster-box inflation per unit of scene extent (see upload)
 #endif
+#ifndef RT_LEAN_GENERATE
+#define RT_LEAN_GENERATE 1
+#endif
 #ifndef RT_FUSED_BOUNCE
 #define RT_FUSED_BOUNCE 0
 #endif
@@ -623,6 +626,8 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
         SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
         GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB,
                   path ? c->rng : nullptr, c->dim, path && c->dsc.full ? c->prevPdf : nullptr, c->betaA, c->betaB, c->LA, c->LB};
+        const bool lean = RT_LEAN_GENERATE && path && !c->dsc.full;  // simple path kernel: no β / L / pdf streams
+        go.lean = lean ? 1 : 0;
         hipEvent_t e0 = ev_start(c, st);
         HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
         ev_mark(c, st, ST_GEN, e0);
@@ -663,6 +668,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 }
                 PathIO pio{};
                 pio.fused = fused ? 1 : 0;
+                pio.lean = lean ? 1 : 0;
                 pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = qc_cur;
                 pio.hitB = c->hitB; pio.hitPrim = c->hitPrim;
                 pio.nO = c->rayO + (size_t)nxt * qs; pio.nD = c->rayD + (size_t)nxt * qs;
@@ -678,6 +684,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 cur = nxt;
             }
             PathFilmIO fio{c->d_work, c->n_work, nIdx, c->LA, c->LB, c->lamA, c->lamB, c->pdfA, c->pdfB, film};
+            fio.lean = lean ? 1 : 0;
             e0 = ev_start(c, st);
             HIPCHK(c, launch_path_film(st, 0, c->d_spec, fd, fio, c->d_ctr));
             ev_mark(c, st, ST_FILM, e0);

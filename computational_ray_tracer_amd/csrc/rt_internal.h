@@ -130,6 +130,7 @@ struct GenOut {
     uint4* rng; int* dim;                                 // path-mode sampler state (nullptr in reference mode)
     float* prevPdf;                                       // path mode, general kernel: set to 0 (camera ray)
     float4* betaA; float4* betaB; float4* LA; float4* LB;
+    int lean;  // simple path kernel: no β = 1 / L = 0 / pdf stores (depth 0 and the film kernel derive them)
 };
 
 // Ray queues.  A path-mode queue is split into 3 bins by the rays' dominant axis (the watertight test's
@@ -173,12 +174,14 @@ struct PathIO {
     float* prevPdf;                                                       // pdf of the last diffuse bounce
     int depth, max_depth;
     int fused;  // simple scenes: the closest-hit traversal runs inside the shade kernel (no hit records)
+    int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
 };
 
 struct PathFilmIO {
     const int* work_pixels; int n_pixels; int n_index;
     const float4* LA; const float4* LB; const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
     float4* film;
+    int lean;  // pdf = VisibleWavelengthsPDF(λ) recomputed here (nothing rewrites it on the simple path)
 };
 
 struct RecordIO {

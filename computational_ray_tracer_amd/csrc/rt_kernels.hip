@@ -202,6 +202,14 @@ __device__ __forceinline__ void load8(const float4* a, const float4* b, int s, f
     float4 p = a[s], q = b[s];
     v[0] = p.x; v[1] = p.y; v[2] = p.z; v[3] = p.w; v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
 }
+__device__ __forceinline__ void load8_or_zero(const float4* a, const float4* b, int s, float v[8], bool zero) {
+    if (zero) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 0.f;
+    } else {
+        load8(a, b, s, v);
+    }
+}
 __device__ __forceinline__ void store8(float4* a, float4* b, int s, const float v[8]) {
     a[s] = make_float4(v[0], v[1], v[2], v[3]);
     b[s] = make_float4(v[4], v[5], v[6], v[7]);
@@ -225,7 +233,7 @@ __global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevC
             float up = u + float(i) / 8;
             if (up > 1) up -= 1;
             lam[i] = sample_visible_wavelength(up);
-            pdf[i] = visible_pdf(lam[i]);
+            pdf[i] = out.lean ? 0.f : visible_pdf(lam[i]);
         }
         float u0, u1;
         sm.get_pixel2d(smp, u0, u1);  // Sampler::GetPixel2D (RayTracerTestApp.h:316)
@@ -288,15 +296,17 @@ __global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevC
         out.rayD[s] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
         out.slot[s] = s;
         store8(out.lamA, out.lamB, s, lam);
-        store8(out.pdfA, out.pdfB, s, pdf);
+        if (!out.lean) store8(out.pdfA, out.pdfB, s, pdf);
         if (out.rng) {
             out.rng[s] = make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
                                     (uint32_t)(sm.rng.inc >> 32));
             out.dim[s] = sm.dim;
-            out.betaA[s] = make_float4(1.f, 1.f, 1.f, 1.f);
-            out.betaB[s] = make_float4(1.f, 1.f, 1.f, 1.f);
-            out.LA[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-            out.LB[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!out.lean) {
+                out.betaA[s] = make_float4(1.f, 1.f, 1.f, 1.f);
+                out.betaB[s] = make_float4(1.f, 1.f, 1.f, 1.f);
+                out.LA[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+                out.LB[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             if (out.prevPdf) out.prevPdf[s] = 0.f;
         }
     }
@@ -745,9 +755,11 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
     int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
     int n = c0 + c1 + c2;
     unsigned long long snn = 0, snt = 0, nsh = 0, tnn = 0, tnt = 0, tnh = 0, tnr = 0;
+    // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
+    const bool d0 = io.lean && io.depth == 0;
     for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         int k = base + threadIdx.x;
-        bool wantShadow = false, wantNext = false;
+        bool wantShadow = false, wantNext = false, storedL = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int nbin = -1;
         V3 so = v3(0, 0, 0), sd = so;
@@ -774,7 +786,12 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
             if (prim >= 0) {
                 float lam[8], beta[8];
                 load8(io.lamA, io.lamB, slot, lam);
-                load8(io.betaA, io.betaB, slot, beta);
+                if (d0) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) beta[i] = 1.f;
+                } else {
+                    load8(io.betaA, io.betaB, slot, beta);
+                }
                 float4 P0 = sc.triWorld[3 * prim], P1 = sc.triWorld[3 * prim + 1], P2 = sc.triWorld[3 * prim + 2];
                 V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
                 V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
@@ -785,10 +802,11 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
                 if (mt.w > 0) {
                     if (io.depth == 0 && vdot(ng, rayd) < 0) {
                         float L[8];
-                        load8(io.LA, io.LB, slot, L);
+                        load8_or_zero(io.LA, io.LB, slot, L, d0);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.w * dense_query(sp->D65, lam[i]));
                         store8(io.LA, io.LB, slot, L);
+                        storedL = true;
                     }
                 } else if (io.depth < io.max_depth) {
                     V3 nrm = ng;
@@ -873,11 +891,16 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
             ++nsh;
             if (hit < 0) {
                 float L[8];
-                load8(io.LA, io.LB, slot, L);
+                load8_or_zero(io.LA, io.LB, slot, L, d0);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) L[i] += Ld[i];
                 store8(io.LA, io.LB, slot, L);
+                storedL = true;
             }
+        }
+        if (d0 && slot >= 0 && !storedL) {
+            const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            store8(io.LA, io.LB, slot, z);
         }
 #if RT_RAY_SORT
         long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
@@ -1191,7 +1214,12 @@ __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevF
             int s = i * io.n_pixels + j;
             float lam[8], pdf[8], L[8], rgb[3];
             load8(io.lamA, io.lamB, s, lam);
-            load8(io.pdfA, io.pdfB, s, pdf);
+            if (io.lean) {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) pdf[w] = visible_pdf(lam[w]);  // the value k_generate would have stored
+            } else {
+                load8(io.pdfA, io.pdfB, s, pdf);
+            }
             load8(io.LA, io.LB, s, L);
             to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
             const float w = 1.0f;
