@@ -21,8 +21,10 @@ RT_CAMERA_PERSPECTIVE, RT_CAMERA_ORTHOGRAPHIC, RT_CAMERA_PINHOLE, RT_CAMERA_THIN
 RT_SAMPLER_INDEPENDENT, RT_SAMPLER_STRATIFIED, RT_SAMPLER_SOBOL = 0, 1, 2
 RT_SOBOL_NONE, RT_SOBOL_PERMUTE_DIGITS, RT_SOBOL_FAST_OWEN, RT_SOBOL_OWEN = 0, 1, 2, 3
 RT_FILTER_BOX, RT_FILTER_TRIANGLE, RT_FILTER_GAUSSIAN, RT_FILTER_LANCZOS = 0, 1, 2, 3
+RT_SENSOR_XYZ, RT_SENSOR_CANON_EOS_100D, RT_SENSOR_COUNT = 0, 1, 18
+RT_ILLUM_D65, RT_ILLUM_A, RT_ILLUM_D50, RT_ILLUM_F1, RT_ILLUM_ACES_D60, RT_ILLUM_COUNT = 0, 1, 2, 3, 15, 16
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 F16 = C.c_float * 16
 F9 = C.c_float * 9
@@ -82,7 +84,8 @@ class rt_sampler_desc(C.Structure):
 
 class rt_film_desc(C.Structure):
     _fields_ = [("res_x", C.c_int), ("res_y", C.c_int), ("filter", C.c_int), ("filter_radius", F2),
-                ("imaging_ratio", C.c_float), ("filter_param", C.c_float)]
+                ("imaging_ratio", C.c_float), ("filter_param", C.c_float), ("sensor", C.c_int),
+                ("sensor_illum", C.c_int)]
 
 
 class rt_integrator_desc(C.Structure):
@@ -120,6 +123,7 @@ EXPORTS = [
     "rt_get_stats", "rt_reset_stats", "rt_octree_get_info", "rt_octree_export",
     "rt_debug_trace", "rt_debug_occluded", "rt_debug_samples",
     "rt_film_resolve_srgb", "rt_load_obj", "rt_mesh_free", "rt_image_write", "rt_rgb_to_sigmoid",
+    "rt_sensor_name", "rt_film_matrices",
 ]
 
 _lib = None
@@ -168,6 +172,8 @@ def load_library(path=None):
         "rt_mesh_free": ([P(rt_mesh)], None),
         "rt_image_write": ([C.c_char_p, C.c_int, C.c_int, P(C.c_uint8), C.c_int], C.c_int),
         "rt_rgb_to_sigmoid": ([P(C.c_float), P(C.c_float)], C.c_int),
+        "rt_sensor_name": ([C.c_int], C.c_char_p),
+        "rt_film_matrices": ([C.c_void_p, P(C.c_float), P(C.c_float)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -330,7 +330,7 @@ RT_DEV void to_sensor_rgb(const DevSpectra* sp, const float L_[8], const float l
     float L[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) L[i] = (pdf[i] != 0) ? L_[i] / pdf[i] : 0.f;
-    const float* bars[3] = {sp->X, sp->Y, sp->Z};
+    const float* bars[3] = {sp->SR, sp->SG, sp->SB};  // X/Y/Z for the XYZ sensor, camera curves otherwise
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         float sum = dense_query(bars[c], lam[0]) * L[0];

@@ -8,16 +8,19 @@
 //
 // There is no CPU fallback: every pass runs on the MI355X; rt_create fails without a gfx950 device.
 #include <algorithm>
+#include <cstddef>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <limits>
 #include <queue>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/rtmi355x.h"
 #include "../data/spectra_data.h"
+#include "../data/sensor_data.h"
 #include "rt_internal.h"
 
 using namespace rtmi;
@@ -693,6 +696,141 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     return RT_OK;
 }
 
+// ---------------------------------------------------------------------------------- PixelSensor (a18, a20)
+// glm float order throughout: mat3 is column-major (m[col * 3 + row]); inverse = glm's cofactor form; products
+// sum (a0 b0 + a1 b1) + a2 b2.
+void inv3(const float* a, float* o) {
+    auto m = [&](int col, int row) { return a[col * 3 + row]; };
+    float ood = 1.0f / (+m(0, 0) * (m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) -
+                        m(1, 0) * (m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) +
+                        m(2, 0) * (m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)));
+    o[0] = +(m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) * ood;
+    o[3] = -(m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2)) * ood;
+    o[6] = +(m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1)) * ood;
+    o[1] = -(m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) * ood;
+    o[4] = +(m(0, 0) * m(2, 2) - m(2, 0) * m(0, 2)) * ood;
+    o[7] = -(m(0, 0) * m(2, 1) - m(2, 0) * m(0, 1)) * ood;
+    o[2] = +(m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)) * ood;
+    o[5] = -(m(0, 0) * m(1, 2) - m(1, 0) * m(0, 2)) * ood;
+    o[8] = +(m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1)) * ood;
+}
+void mul3(const float* A, const float* B, float* o) {
+    for (int col = 0; col < 3; ++col)
+        for (int r = 0; r < 3; ++r)
+            o[col * 3 + r] = (A[0 * 3 + r] * B[col * 3 + 0] + A[1 * 3 + r] * B[col * 3 + 1]) + A[2 * 3 + r] * B[col * 3 + 2];
+}
+
+// Spectra::Init's named illuminants (spectrum.cpp:2620-2637): FromInterleaved(.., normalize = true)
+PLS named_illuminant(const HostSpectra& hs, int which) {
+    static const float* const tab[] = {rtdata::illum_d65, rtdata::illum_a, rtdata::illum_d50, rtdata::illum_f1,
+                                       rtdata::illum_f2, rtdata::illum_f3, rtdata::illum_f4, rtdata::illum_f5,
+                                       rtdata::illum_f6, rtdata::illum_f7, rtdata::illum_f8, rtdata::illum_f9,
+                                       rtdata::illum_f10, rtdata::illum_f11, rtdata::illum_f12, rtdata::illum_aces_d60};
+    static const int n[] = {rtdata::illum_d65_n, rtdata::illum_a_n, rtdata::illum_d50_n, rtdata::illum_f1_n,
+                            rtdata::illum_f2_n, rtdata::illum_f3_n, rtdata::illum_f4_n, rtdata::illum_f5_n,
+                            rtdata::illum_f6_n, rtdata::illum_f7_n, rtdata::illum_f8_n, rtdata::illum_f9_n,
+                            rtdata::illum_f10_n, rtdata::illum_f11_n, rtdata::illum_f12_n, rtdata::illum_aces_d60_n};
+    return hs.interleaved(tab[which], n[which], true);
+}
+
+// pixelsensor.h:104-117 ProjectReflectance: (b_i(λ) refl(λ)) illum(λ) summed over λ = 360..830 (float loop),
+// divided by Σ b2(λ) illum(λ)
+template <class R, class I, class B1, class B2, class B3>
+F3 project_reflectance(const R& refl, const I& illum, const B1& b1, const B2& b2, const B3& b3) {
+    float g = 0, r0 = 0, r1 = 0, r2 = 0;
+    for (float l = 360; l <= 830; ++l) {
+        g += b2.query(l) * illum.query(l);
+        r0 += b1.query(l) * refl.query(l) * illum.query(l);
+        r1 += b2.query(l) * refl.query(l) * illum.query(l);
+        r2 += b3.query(l) * refl.query(l) * illum.query(l);
+    }
+    return F3{r0 / g, r1 / g, r2 / g};
+}
+
+// XYZFromSensorRGB (pixelsensor.h:37-79) and the sRGB RGBFromXYZ (colorspace.cpp:13-28) of a film description,
+// plus the sensor's dense r/g/b curves.
+void sensor_matrices(const HostSpectra& hs, int sensor, int illum_id, float* xyz_from_sensor, float* rgb_from_xyz,
+                     DenseS bars[3]) {
+    auto xyz_of = [&](const PLS& s) {  // SpectrumToXYZ
+        float X = inner_product(hs.X, s), Y = inner_product(hs.Y, s), Z = inner_product(hs.Z, s);
+        return F3{X / 106.856895f, Y / 106.856895f, Z / 106.856895f};
+    };
+    auto xy_of = [](F3 c) { return std::pair<float, float>{c.x / (c.x + c.y + c.z), c.y / (c.x + c.y + c.z)}; };
+    auto xyY = [](float x, float y) { return y == 0 ? F3{0, 0, 0} : F3{x * 1.0f / y, 1.0f, (1 - x - y) * 1.0f / y}; };
+    // sRGB (colorspace.cpp:91-106): primaries, white = the D65 illuminant's xy
+    F3 W = xyz_of(hs.D65);
+    auto w = xy_of(W);
+    F3 R = xyY((float).64, (float).33), G = xyY((float).3, (float).6), Bp = xyY((float).15, (float).06);
+    float rgb[9] = {R.x, R.y, R.z, G.x, G.y, G.z, Bp.x, Bp.y, Bp.z}, irgb[9];
+    inv3(rgb, irgb);
+    F3 Cw = m3v(irgb, W);
+    float dg[9] = {Cw.x, 0, 0, 0, Cw.y, 0, 0, 0, Cw.z}, xyzFromRgb[9];
+    mul3(rgb, dg, xyzFromRgb);
+    inv3(xyzFromRgb, rgb_from_xyz);
+    PLS illum = named_illuminant(hs, illum_id);
+    if (sensor == RT_SENSOR_XYZ) {
+        bars[0] = hs.X; bars[1] = hs.Y; bars[2] = hs.Z;
+        // pixelsensor.h:70-79: WhiteBalance(SpectrumToXYZ(sensorIllum).xy, sRGB.w) (color.h:616-629, Bradford)
+        float lmsFromXyz[9] = {(float)0.8951, (float)-0.7502, (float)0.0389, (float)0.2664, (float)1.7135,
+                               (float)-0.0685, (float)-0.1614, (float)0.0367, (float)1.0296};
+        float xyzFromLms[9] = {(float)0.986993, (float)0.432305, (float)-0.00852866, (float)-0.147054, (float)0.51836,
+                               (float)0.0400428, (float)0.159963, (float)0.0492912, (float)0.968487};
+        auto sw = xy_of(xyz_of(illum));
+        F3 src = xyY(sw.first, sw.second), dst = xyY(w.first, w.second);
+        F3 sl = m3v(lmsFromXyz, src), dl = m3v(lmsFromXyz, dst);
+        float corr[9] = {dl.x / sl.x, 0, 0, 0, dl.y / sl.y, 0, 0, 0, dl.z / sl.z}, t1[9];
+        mul3(xyzFromLms, corr, t1);
+        mul3(t1, lmsFromXyz, xyz_from_sensor);
+        return;
+    }
+    // camera curves: PiecewiseLinearSpectrum::FromInterleaved(.., false) sampled densely (pixelsensor.h:41)
+    int cam = sensor - 1;
+    for (int ch = 0; ch < 3; ++ch)
+        bars[ch] = to_dense(hs.interleaved(rtdata::camera_curves[cam][ch], rtdata::camera_curves_n[cam][ch], false));
+    float rgbCamera[24][3], xyzOutput[24][3];
+    for (int i = 0; i < 24; ++i) {
+        PLS sw = hs.interleaved(rtdata::swatches[i], rtdata::swatches_n[i], false);
+        F3 c3 = project_reflectance(sw, illum, bars[0], bars[1], bars[2]);
+        rgbCamera[i][0] = c3.x; rgbCamera[i][1] = c3.y; rgbCamera[i][2] = c3.z;
+    }
+    float sensorWhiteG = inner_product(illum, bars[1]);
+    float sensorWhiteY = inner_product(illum, hs.Y);
+    for (int i = 0; i < 24; ++i) {
+        PLS sw = hs.interleaved(rtdata::swatches[i], rtdata::swatches_n[i], false);
+        F3 x3 = project_reflectance(sw, hs.D65d, hs.X, hs.Y, hs.Z);  // outputColorSpace->illuminant (dense D65)
+        float k = sensorWhiteY / sensorWhiteG;
+        xyzOutput[i][0] = x3.x * k; xyzOutput[i][1] = x3.y * k; xyzOutput[i][2] = x3.z * k;
+    }
+    // helpers.h:258-272 LinearLeastSquares<3>: AtA[i][j] / AtB[i][j] are glm [column i][row j]
+    float AtA[9] = {0}, AtB[9] = {0};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            for (int r = 0; r < 24; ++r) {
+                AtA[i * 3 + j] += rgbCamera[r][i] * rgbCamera[r][j];
+                AtB[i * 3 + j] += rgbCamera[r][i] * xyzOutput[r][j];
+            }
+    float AtAi[9], P[9];
+    inv3(AtA, AtAi);
+    mul3(AtAi, AtB, P);
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) xyz_from_sensor[c * 3 + r] = P[r * 3 + c];  // glm::transpose
+}
+
+int setup_sensor(rt_ctx* c, const rt_film_desc& d) {
+    DenseS bars[3];
+    sensor_matrices(c->hs, d.sensor, d.sensor_illum, c->resolveA, c->resolveB, bars);
+    float both[18];
+    std::memcpy(both, c->resolveA, 36);
+    std::memcpy(both + 9, c->resolveB, 36);
+    char* base = (char*)c->d_spec;
+    if (hipMemcpy(c->d_resolve, both, sizeof(both), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(base + offsetof(DevSpectra, SR), bars[0].v.data(), 4 * kSpecN, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(base + offsetof(DevSpectra, SG), bars[1].v.data(), 4 * kSpecN, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(base + offsetof(DevSpectra, SB), bars[2].v.data(), 4 * kSpecN, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(c, RT_E_HIP, "sensor upload");
+    return RT_OK;
+}
+
 }  // namespace
 
 // =========================================================================================== C-ABI
@@ -736,56 +874,12 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     std::memcpy(ds.bk7_value, c->hs.BK7.v.data(), 4 * ds.bk7_n);
     hipMemcpy(c->d_spec, &ds, sizeof(ds), hipMemcpyHostToDevice);
     hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * C_NCOUNTERS);
-    // a20 resolve matrices: XYZFromSensorRGB (WhiteBalance of identical whites, color.h:616-628) and the sRGB
-    // RGBFromXYZ (colorspace.cpp:13-28) — glm float order
     {
-        auto inv3 = [](const float* a, float* o) {
-            auto m = [&](int col, int row) { return a[col * 3 + row]; };
-            float ood = 1.0f / (+m(0, 0) * (m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) -
-                                m(1, 0) * (m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) +
-                                m(2, 0) * (m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)));
-            o[0] = +(m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) * ood;
-            o[3] = -(m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2)) * ood;
-            o[6] = +(m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1)) * ood;
-            o[1] = -(m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) * ood;
-            o[4] = +(m(0, 0) * m(2, 2) - m(2, 0) * m(0, 2)) * ood;
-            o[7] = -(m(0, 0) * m(2, 1) - m(2, 0) * m(0, 1)) * ood;
-            o[2] = +(m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)) * ood;
-            o[5] = -(m(0, 0) * m(1, 2) - m(1, 0) * m(0, 2)) * ood;
-            o[8] = +(m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1)) * ood;
-        };
-        auto mul3 = [](const float* A, const float* B, float* o) {
-            for (int col = 0; col < 3; ++col)
-                for (int r = 0; r < 3; ++r)
-                    o[col * 3 + r] = (A[0 * 3 + r] * B[col * 3 + 0] + A[1 * 3 + r] * B[col * 3 + 1]) + A[2 * 3 + r] * B[col * 3 + 2];
-        };
-        auto xyz_of = [&](const PLS& s) {
-            float X = inner_product(c->hs.X, s), Y = inner_product(c->hs.Y, s), Z = inner_product(c->hs.Z, s);
-            return F3{X / 106.856895f, Y / 106.856895f, Z / 106.856895f};
-        };
-        auto xyY = [](float x, float y) { return y == 0 ? F3{0, 0, 0} : F3{x * 1.0f / y, 1.0f, (1 - x - y) * 1.0f / y}; };
-        F3 W = xyz_of(c->hs.D65);
-        float wx = W.x / (W.x + W.y + W.z), wy = W.y / (W.x + W.y + W.z);
-        F3 R = xyY((float).64, (float).33), G = xyY((float).3, (float).6), Bp = xyY((float).15, (float).06);
-        float rgb[9] = {R.x, R.y, R.z, G.x, G.y, G.z, Bp.x, Bp.y, Bp.z}, irgb[9];
-        inv3(rgb, irgb);
-        F3 Cw = m3v(irgb, W);
-        float dg[9] = {Cw.x, 0, 0, 0, Cw.y, 0, 0, 0, Cw.z}, xyzFromRgb[9];
-        mul3(rgb, dg, xyzFromRgb);
-        inv3(xyzFromRgb, c->resolveB);
-        float lmsFromXyz[9] = {(float)0.8951, (float)-0.7502, (float)0.0389, (float)0.2664, (float)1.7135,
-                               (float)-0.0685, (float)-0.1614, (float)0.0367, (float)1.0296};
-        float xyzFromLms[9] = {(float)0.986993, (float)0.432305, (float)-0.00852866, (float)-0.147054, (float)0.51836,
-                               (float)0.0400428, (float)0.159963, (float)0.0492912, (float)0.968487};
-        F3 src = xyY(wx, wy), dst = xyY(wx, wy);
-        F3 sl = m3v(lmsFromXyz, src), dl = m3v(lmsFromXyz, dst);
-        float corr[9] = {dl.x / sl.x, 0, 0, 0, dl.y / sl.y, 0, 0, 0, dl.z / sl.z}, t1[9];
-        mul3(xyzFromLms, corr, t1);
-        mul3(t1, lmsFromXyz, c->resolveA);
-        float both[18];
-        std::memcpy(both, c->resolveA, 36);
-        std::memcpy(both + 9, c->resolveB, 36);
-        hipMemcpy(c->d_resolve, both, sizeof(both), hipMemcpyHostToDevice);
+        rt_film_desc fd{};  // XYZ sensor under D65 until rt_film_set says otherwise
+        if (setup_sensor(c, fd) != RT_OK) {
+            rt_destroy(c);
+            return RT_E_HIP;
+        }
     }
     *out = c;
     return RT_OK;
@@ -1200,8 +1294,12 @@ int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
     if (d->res_x <= 0 || d->res_y <= 0 || d->filter < RT_FILTER_BOX || d->filter > RT_FILTER_LANCZOS)
         return fail(c, RT_E_ARG, "invalid film");
     if ((size_t)d->res_x * d->res_y > ((size_t)1 << 27)) return fail(c, RT_E_LIMIT, "film too large");
+    if (d->sensor < 0 || d->sensor >= RT_SENSOR_COUNT || d->sensor_illum < 0 || d->sensor_illum >= RT_ILLUM_COUNT)
+        return fail(c, RT_E_ARG, "unknown sensor or sensor illuminant");
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);  // queued passes may still read the old tables
+    int rc = setup_sensor(c, *d);
+    if (rc) return rc;
     if (c->d_cdf) { hipFree(c->d_cdf); c->d_cdf = nullptr; c->cdf_n = 0; }
     if (d->filter == RT_FILTER_GAUSSIAN || d->filter == RT_FILTER_LANCZOS) {
         std::vector<float> tx, ty;
@@ -1214,6 +1312,21 @@ int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
     c->film = *d;
     c->have_film = true;
     c->work_dirty = true;
+    return RT_OK;
+}
+
+static_assert(rtdata::n_cameras + 1 == RT_SENSOR_COUNT, "camera table and RT_SENSOR_COUNT disagree");
+
+const char* rt_sensor_name(int sensor) {
+    if (sensor == RT_SENSOR_XYZ) return "xyz";
+    if (sensor < 1 || sensor >= RT_SENSOR_COUNT) return nullptr;
+    return rtdata::camera_names[sensor - 1];
+}
+
+int rt_film_matrices(rt_ctx* c, float* xyz_from_sensor9, float* rgb_from_xyz9) {
+    if (!c || !xyz_from_sensor9 || !rgb_from_xyz9) return RT_E_ARG;
+    std::memcpy(xyz_from_sensor9, c->resolveA, 36);
+    std::memcpy(rgb_from_xyz9, c->resolveB, 36);
     return RT_OK;
 }
 

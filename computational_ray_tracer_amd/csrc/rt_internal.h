@@ -24,6 +24,7 @@ struct DevSpectra {                 // Spectra::Init products (spectrum.cpp:2612
     int f1_n;
     float bk7_lambda[kF1Max], bk7_value[kF1Max];   // glass-BK7 eta, FromInterleaved(.., false) (spectrum.cpp:2674)
     int bk7_n;
+    float SR[kSpecN], SG[kSpecN], SB[kSpecN];      // the film's PixelSensor r_bar / g_bar / b_bar (dense)
 };
 
 struct DevCamera {

@@ -66,6 +66,13 @@ class Renderer:
             C.POINTER(capi.rt_pixel)), out.ctypes.data_as(C.POINTER(C.c_uint8))))
         return out
 
+    def film_matrices(self):
+        """(XYZFromSensorRGB, RGBFromXYZ) of the current film's sensor, column-major float32[9] each."""
+        a, b = np.zeros(9, np.float32), np.zeros(9, np.float32)
+        P = lambda x: x.ctypes.data_as(C.POINTER(C.c_float))
+        self._chk("rt_film_matrices", self.lib.rt_film_matrices(self.h, P(a), P(b)))
+        return a, b
+
     def stats(self):
         s = capi.rt_stats()
         self._chk("rt_get_stats", self.lib.rt_get_stats(self.h, C.byref(s)))

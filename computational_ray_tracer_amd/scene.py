@@ -234,6 +234,14 @@ class IndependentSampler:
         return capi.rt_sampler_desc(capi.RT_SAMPLER_INDEPENDENT, self.samples_per_pixel, 1, 0, self.seed)
 
 
+# PixelSensor choices (rt_film_desc.sensor): "xyz" then the camera curves of spectrum.cpp, in the same order as
+# tools/extract_spectra.py CAMERAS / rt_sensor_name
+SENSORS = ["xyz", "canon_eos_100d", "canon_eos_1dx_mkii", "canon_eos_200d", "canon_eos_200d_mkii", "canon_eos_5d",
+           "canon_eos_5d_mkii", "canon_eos_5d_mkiii", "canon_eos_5d_mkiv", "canon_eos_5ds", "canon_eos_m",
+           "hasselblad_l1d_20c", "nikon_d810", "nikon_d850", "sony_ilce_6400", "sony_ilce_7m3", "sony_ilce_7rm3",
+           "sony_ilce_9"]
+
+
 @dataclass
 class Film:
     """Film {film_dim, image_res, filter, pixel_sensor} (Film.h:11-20) with a BoxFilter/TriangleFilter of
@@ -243,6 +251,8 @@ class Film:
     filter_radius: tuple = (0.5, 0.5)
     imaging_ratio: float = float(np.float32(1.0) / np.float32(106.856895))
     filter_param: float = 0.0        # Gaussian sigma / Lanczos tau (0: the reference defaults 0.5 / 3)
+    sensor: int = capi.RT_SENSOR_XYZ  # or 1..17: SENSORS (the reference's camera response curves)
+    sensor_illum: int = capi.RT_ILLUM_D65
 
     def desc(self):
         d = capi.rt_film_desc()
@@ -251,6 +261,8 @@ class Film:
         d.filter_radius[:] = list(self.filter_radius)
         d.imaging_ratio = self.imaging_ratio
         d.filter_param = self.filter_param
+        d.sensor = self.sensor
+        d.sensor_illum = self.sensor_illum
         return d
 
     def new_pixels(self):

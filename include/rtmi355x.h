@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 typedef enum {
     RT_OK = 0,
@@ -149,6 +149,16 @@ typedef struct {
 } rt_sampler_desc;
 
 enum { RT_FILTER_BOX = 0, RT_FILTER_TRIANGLE = 1, RT_FILTER_GAUSSIAN = 2, RT_FILTER_LANCZOS = 3 };
+/* PixelSensor (pixelsensor.h:37-79).  RT_SENSOR_XYZ: r/g/b = CIE X/Y/Z, XYZFromSensorRGB = WhiteBalance(sensor
+ * illuminant white -> sRGB white).  1..17: the camera response curves the reference names in spectrum.cpp
+ * (rt_sensor_name), XYZFromSensorRGB fitted over the 24 Macbeth swatches under the sensor illuminant exactly as
+ * pixelsensor.h:37-68 does it (glm column-major LinearLeastSquares, helpers.h:258-272). */
+enum { RT_SENSOR_XYZ = 0, RT_SENSOR_CANON_EOS_100D = 1, RT_SENSOR_COUNT = 18 };
+/* Named illuminants of Spectra::Init (spectrum.cpp:2620-2637, all Y-normalised): the sensor illuminant. */
+enum {
+    RT_ILLUM_D65 = 0, RT_ILLUM_A = 1, RT_ILLUM_D50 = 2, RT_ILLUM_F1 = 3, /* F1..F12 = 3..14 */
+    RT_ILLUM_ACES_D60 = 15, RT_ILLUM_COUNT = 16
+};
 /* Film (Film.h:11-20) + its filter + XYZ PixelSensor (pixelsensor.h:70-87).  Filters: Box (filters.h:66-93),
  * Triangle (267-296, deterministic coin), Gaussian (96-154, sigma = filter_param) and LanczosSinc (223-264,
  * tau = filter_param), the last two sampled through the reference's tabulated Continuous_Inversion_Sampler
@@ -159,6 +169,8 @@ typedef struct {
     float filter_radius[2];
     float imaging_ratio;             /* 1/CIE_Y_integral in the reference app (RayTracerTestApp.h:149) */
     float filter_param;              /* Gaussian sigma (0 -> 0.5) / Lanczos tau (0 -> 3)               */
+    int sensor;                      /* RT_SENSOR_XYZ or a camera (1..RT_SENSOR_COUNT-1)               */
+    int sensor_illum;                /* RT_ILLUM_*: sensorIllum of the PixelSensor constructors        */
 } rt_film_desc;
 
 enum { RT_INTEGRATOR_REFERENCE = 0, RT_INTEGRATOR_PATH = 1, RT_INTEGRATOR_PATH_MIS = 2 };
@@ -259,6 +271,10 @@ int rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_
 /* RGBAlbedoSpectrum coefficients for an sRGB reflectance in [0,1]^3 (replaces the missing RGBToSpectrumTable file,
  * color.cpp:26-72, 114): grey = the closed form of color.cpp:35-37, otherwise a Gauss-Newton fit in CIELAB. */
 int rt_rgb_to_sigmoid(const float* rgb, float* coeffs);
+/* Name of a PixelSensor (RT_SENSOR_XYZ -> "xyz", 1.. -> the reference's camera name), NULL when out of range. */
+const char* rt_sensor_name(int sensor);
+/* The film's resolve matrices (column-major, glm layout): XYZFromSensorRGB of the current sensor, sRGB RGBFromXYZ. */
+int rt_film_matrices(rt_ctx* ctx, float* xyz_from_sensor9, float* rgb_from_xyz9);
 
 /* ---- instrumentation ---------------------------------------------------------------------------- */
 int rt_get_stats(rt_ctx* ctx, rt_stats* out);

@@ -76,6 +76,7 @@ def lib():
             "orc_resolve": ([C.c_void_p, P(C.c_float), P(C.c_uint8)], None),
             "orc_resolve_srgb": ([C.c_void_p, P(C.c_float), P(C.c_uint8)], None),
             "orc_resolve_matrices": ([C.c_void_p, P(C.c_float), P(C.c_float)], None),
+            "orc_sensor_training": ([C.c_void_p, P(C.c_float), P(C.c_float)], None),
         }
         for name, (a, r) in sig.items():
             f = getattr(L, name)
@@ -173,6 +174,18 @@ class OracleScene:
                          pp, npx)
         self.counters = cnt
         return film
+
+    def resolve_matrices(self):
+        """(XYZFromSensorRGB, RGBFromXYZ) as column-major float32[9] (glm layout)."""
+        a, b = np.zeros(9, np.float32), np.zeros(9, np.float32)
+        lib().orc_resolve_matrices(self.h, fptr(a), fptr(b))
+        return a, b
+
+    def sensor_training(self):
+        """Camera sensors: the 24 swatches' (camera RGB, target XYZ) rows of the least-squares fit."""
+        a, b = np.zeros((24, 3), np.float32), np.zeros((24, 3), np.float32)
+        lib().orc_sensor_training(self.h, fptr(a), fptr(b))
+        return a, b
 
     def resolve(self, film, srgb=False):
         out = np.zeros((self.res[0] * self.res[1], 3), np.uint8)

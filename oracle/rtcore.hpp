@@ -544,8 +544,46 @@ struct Spectra {
         D65 = FromInterleaved(rtdata::illum_d65, rtdata::illum_d65_n, true);
         F1 = FromInterleaved(rtdata::illum_f1, rtdata::illum_f1_n, true);
         D65dense = MakeDense(D65);
+        SR = X; SG = Y; SB = Z;
     }
+    Dense SR, SG, SB;    // the film's PixelSensor r_bar, g_bar, b_bar (XYZ sensor: X, Y, Z)
 };
+
+// Spectra::Init named illuminants (spectrum.cpp:2620-2637, normalized): RT_ILLUM_* order
+static inline Piecewise NamedIlluminant(const Spectra& sp, int which) {
+    switch (which) {
+        case 1: return sp.FromInterleaved(rtdata::illum_a, rtdata::illum_a_n, true);
+        case 2: return sp.FromInterleaved(rtdata::illum_d50, rtdata::illum_d50_n, true);
+        case 3: return sp.FromInterleaved(rtdata::illum_f1, rtdata::illum_f1_n, true);
+        case 4: return sp.FromInterleaved(rtdata::illum_f2, rtdata::illum_f2_n, true);
+        case 5: return sp.FromInterleaved(rtdata::illum_f3, rtdata::illum_f3_n, true);
+        case 6: return sp.FromInterleaved(rtdata::illum_f4, rtdata::illum_f4_n, true);
+        case 7: return sp.FromInterleaved(rtdata::illum_f5, rtdata::illum_f5_n, true);
+        case 8: return sp.FromInterleaved(rtdata::illum_f6, rtdata::illum_f6_n, true);
+        case 9: return sp.FromInterleaved(rtdata::illum_f7, rtdata::illum_f7_n, true);
+        case 10: return sp.FromInterleaved(rtdata::illum_f8, rtdata::illum_f8_n, true);
+        case 11: return sp.FromInterleaved(rtdata::illum_f9, rtdata::illum_f9_n, true);
+        case 12: return sp.FromInterleaved(rtdata::illum_f10, rtdata::illum_f10_n, true);
+        case 13: return sp.FromInterleaved(rtdata::illum_f11, rtdata::illum_f11_n, true);
+        case 14: return sp.FromInterleaved(rtdata::illum_f12, rtdata::illum_f12_n, true);
+        case 15: return sp.FromInterleaved(rtdata::illum_aces_d60, rtdata::illum_aces_d60_n, true);
+        default: return sp.D65;
+    }
+}
+
+// pixelsensor.h:104-117 PixelSensor::ProjectReflectance
+template <class R, class I, class B1, class B2, class B3>
+static inline vec3 ProjectReflectance(const R& refl, const I& illum, const B1& b1, const B2& b2, const B3& b3) {
+    vec3 result{0, 0, 0};
+    float g_integral = 0;
+    for (float lambda = 360; lambda <= 830; ++lambda) {
+        g_integral += b2.Query(lambda) * illum.Query(lambda);
+        result.x += b1.Query(lambda) * refl.Query(lambda) * illum.Query(lambda);
+        result.y += b2.Query(lambda) * refl.Query(lambda) * illum.Query(lambda);
+        result.z += b3.Query(lambda) * refl.Query(lambda) * illum.Query(lambda);
+    }
+    return vec3{result.x / g_integral, result.y / g_integral, result.z / g_integral};
+}
 
 // 8-wavelength sampled values (spectrum.h:52-343)
 struct SW { float lambda[8], pdf[8]; };
@@ -576,7 +614,7 @@ static inline Sigmoid SigmoidFromGrey(float g) { return {0, 0, (g - .5f) / std::
 // pixelsensor.h:81-87 ToSensorRGB (XYZ sensor: r_bar=X, g_bar=Y, b_bar=Z), imagingRatio = 1/CIE_Y_integral
 static inline void ToSensorRGB(const Spectra& sp, SS L, const SW& w, float imagingRatio, float rgb[3]) {
     for (int i = 0; i < 8; ++i) L.v[i] = (w.pdf[i] != 0) ? L.v[i] / w.pdf[i] : 0.f;  // spectrum.h:643-649
-    const Dense* bars[3] = {&sp.X, &sp.Y, &sp.Z};
+    const Dense* bars[3] = {&sp.SR, &sp.SG, &sp.SB};
     for (int c = 0; c < 3; ++c) {
         float prod[8];
         for (int i = 0; i < 8; ++i) prod[i] = bars[c]->Query(w.lambda[i]) * L.v[i];

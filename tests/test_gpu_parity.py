@@ -7,7 +7,7 @@ path integrator (same op order on both sides; tolerance 0, stated per test).
 import numpy as np
 import pytest
 
-from computational_ray_tracer_amd import scene
+from computational_ray_tracer_amd import capi, scene
 from computational_ray_tracer_amd.renderer import Renderer, records_to_arrays
 
 pytestmark = pytest.mark.gpu
@@ -335,3 +335,29 @@ def test_cornell_surface_rays_closest_and_occluded_bitexact(oracle_lib):
     assert 0.05 < og.mean() < 0.95
     og2 = g.occluded(ro, rd, tmax)
     assert np.array_equal(og2, o.occluded(ro, rd, tmax))
+
+
+@pytest.mark.parametrize("sensor,illum", [(0, 1), (1, 1), (9, 0), (17, 2)])
+def test_pixel_sensor_film_and_resolve_bitexact(oracle_lib, sensor, illum):
+    """XYZ sensor under another illuminant and camera-curve sensors (pixelsensor.h:37-87): the film kernel's
+    sensor curves, the host's XYZFromSensorRGB and the resolve bytes all equal the oracle's."""
+    cfg = scene.cfg_cornell(res=(48, 32), spp_side=2)
+    cfg.film.sensor, cfg.film.sensor_illum = sensor, illum
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    ga, gb = g.film_matrices()
+    oa, ob = o.resolve_matrices()
+    assert np.array_equal(bits(ga), bits(oa)) and np.array_equal(bits(gb), bits(ob))
+    fg = g.render_pass(0, 4)
+    fo = o.render(0, 4)
+    assert np.array_equal(bits(fg), bits(fo))
+    assert np.array_equal(g.resolve(fg), o.resolve(fo))
+    assert np.array_equal(g.resolve(fg, srgb=True), o.resolve(fo, srgb=True))
+
+
+def test_pixel_sensor_reference_integrator_bitexact(oracle_lib):
+    cfg = scene.cfg0_reference(res=(64, 64), frequency=16, n_index=3)
+    cfg.film.sensor, cfg.film.sensor_illum = capi.RT_SENSOR_CANON_EOS_100D, capi.RT_ILLUM_A
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    fg = g.render_pass(0, 3)
+    fo = o.render(0, 3)
+    assert np.array_equal(bits(fg), bits(fo))
