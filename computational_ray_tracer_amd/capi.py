@@ -22,6 +22,7 @@ RT_SAMPLER_INDEPENDENT, RT_SAMPLER_STRATIFIED, RT_SAMPLER_SOBOL = 0, 1, 2
 RT_SOBOL_NONE, RT_SOBOL_PERMUTE_DIGITS, RT_SOBOL_FAST_OWEN, RT_SOBOL_OWEN = 0, 1, 2, 3
 RT_FILTER_BOX, RT_FILTER_TRIANGLE, RT_FILTER_GAUSSIAN, RT_FILTER_LANCZOS = 0, 1, 2, 3
 RT_SENSOR_XYZ, RT_SENSOR_CANON_EOS_100D, RT_SENSOR_COUNT = 0, 1, 18
+RT_OCTREE_BUILD_DEVICE, RT_OCTREE_BUILD_HOST = 0, 1
 RT_ILLUM_D65, RT_ILLUM_A, RT_ILLUM_D50, RT_ILLUM_F1, RT_ILLUM_ACES_D60, RT_ILLUM_COUNT = 0, 1, 2, 3, 15, 16
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
 ABI_VERSION = 5
@@ -34,7 +35,7 @@ F8 = C.c_float * 8
 
 
 class rt_options(C.Structure):
-    _fields_ = [("device", C.c_int), ("reserved", C.c_int * 7)]
+    _fields_ = [("device", C.c_int), ("octree_build", C.c_int), ("reserved", C.c_int * 6)]
 
 
 class rt_pixel(C.Structure):

@@ -186,18 +186,24 @@ struct OctBuild {
         const F3* p = &(*tri3)[3 * (size_t)t];
         return tri_box_overlap(c, half, p[0], p[1], p[2]);
     }
-    void split(int id) {
-        F3 mn = nodes[id].mn, mx = nodes[id].mx;
+    // the 8 padded child boxes of a node (Octtree_Model.h:279-300): top fl, fr, bl, br, bottom fl, fr, bl, br
+    static void child_boxes(F3 mn, F3 mx, F3 cmn[8], F3 cmx[8]) {
         F3 h = {(mx.x - mn.x) / 2.0f, (mx.y - mn.y) / 2.0f, (mx.z - mn.z) / 2.0f};
         F3 C = f3add(mn, h);
         h = f3add(h, {0.01f, 0.01f, 0.01f});
-        // child order: top fl, fr, bl, br, bottom fl, fr, bl, br (Octtree_Model.h:287-300)
         const F3 lo[8] = {{-h.x, 0, -h.z}, {0, 0, -h.z}, {-h.x, 0, 0}, {0, 0, 0},
                           {-h.x, -h.y, -h.z}, {0, -h.y, -h.z}, {-h.x, -h.y, 0}, {0, -h.y, 0}};
         const F3 hi[8] = {{0, h.y, 0}, {h.x, h.y, 0}, {0, h.y, h.z}, {h.x, h.y, h.z},
                           {0, 0, 0}, {h.x, 0, 0}, {0, 0, h.z}, {h.x, 0, h.z}};
+        for (int k = 0; k < 8; ++k) { cmn[k] = f3add(C, lo[k]); cmx[k] = f3add(C, hi[k]); }
+    }
+    void split(int id) {
         Node ch[8];
-        for (int k = 0; k < 8; ++k) { ch[k].mn = f3add(C, lo[k]); ch[k].mx = f3add(C, hi[k]); }
+        {
+            F3 cmn[8], cmx[8];
+            child_boxes(nodes[id].mn, nodes[id].mx, cmn, cmx);
+            for (int k = 0; k < 8; ++k) { ch[k].mn = cmn[k]; ch[k].mx = cmx[k]; }
+        }
         for (int t : nodes[id].tris)
             for (int k = 0; k < 8; ++k)
                 if (overlap(t, ch[k])) ch[k].tris.push_back(t);
@@ -227,6 +233,184 @@ struct OctBuild {
     }
 };
 
+// On-device build of the same tree (rt_octree.hip: the level-synchronous form of the sequential insertion).  The
+// device classifies and scatters each level; the host decides the splits (k = max(capacity, s0 + 1, M + 1) <= len),
+// lays out the next level in BFS order and at the end renumbers the nodes in the order the sequential build
+// creates them: by the triangle whose insertion triggered the split, then BFS order within that insertion.
+int octree_build_device(hipStream_t st, OctBuild& ob, int nt, std::string& err) {
+    struct LNode {
+        F3 mn, mx;
+        int begin, len, s0, level;
+        int first_child = -1, trigger = -1;
+    };
+    auto ok = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess) err = std::string("octree build: ") + what + ": " + hipGetErrorString(e);
+        return e == hipSuccess;
+    };
+    std::vector<void*> owned;
+    auto dmalloc = [&](void** p, size_t bytes) {
+        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+        if (e == hipSuccess) owned.push_back(*p);
+        return e;
+    };
+    struct Free {
+        std::vector<void*>& v;
+        ~Free() { for (void* p : v) hipFree(p); }
+    } free_all{owned};
+    const std::vector<F3>& tri3 = *ob.tri3;
+    float* d_tri9 = nullptr;
+    int *d_ent = nullptr, *d_seg = nullptr, *d_stats = nullptr, *d_job = nullptr, *d_s0 = nullptr;
+    unsigned char* d_mask = nullptr;
+    float* d_cbox = nullptr;
+    if (!ok(dmalloc((void**)&d_tri9, sizeof(F3) * tri3.size()), "alloc") ||
+        !ok(hipMemcpyAsync(d_tri9, tri3.data(), sizeof(F3) * tri3.size(), hipMemcpyHostToDevice, st), "upload"))
+        return RT_E_HIP;
+    // root pass: A_root = the triangles overlapping the root box, in insertion order
+    std::vector<int> iota(nt);
+    for (int t = 0; t < nt; ++t) iota[t] = t;
+    size_t cap_ent = std::max<size_t>(nt, 1), cap_nodes = 1, cap_mask = cap_ent;
+    int* d_next = nullptr;
+    if (!ok(dmalloc((void**)&d_ent, 4 * cap_ent), "alloc") || !ok(dmalloc((void**)&d_next, 4 * cap_ent), "alloc") ||
+        !ok(dmalloc((void**)&d_mask, cap_ent), "alloc") || !ok(dmalloc((void**)&d_cbox, 4 * 48), "alloc") ||
+        !ok(dmalloc((void**)&d_seg, 4 * 2), "alloc") || !ok(dmalloc((void**)&d_stats, 4 * 9), "alloc") ||
+        !ok(dmalloc((void**)&d_job, 4 * 12), "alloc") || !ok(dmalloc((void**)&d_s0, 4 * 8), "alloc"))
+        return RT_E_OOM;
+    {
+        float box[48];
+        const F3 rmn = ob.nodes[0].mn, rmx = ob.nodes[0].mx;
+        for (int k = 0; k < 8; ++k) {
+            box[6 * k] = rmn.x; box[6 * k + 1] = rmn.y; box[6 * k + 2] = rmn.z;
+            box[6 * k + 3] = rmx.x; box[6 * k + 4] = rmx.y; box[6 * k + 5] = rmx.z;
+        }
+        int seg[2] = {0, nt}, job[12] = {0, nt, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stats[9];
+        if (!ok(hipMemcpyAsync(d_ent, iota.data(), 4 * (size_t)nt, hipMemcpyHostToDevice, st), "upload") ||
+            !ok(hipMemcpyAsync(d_cbox, box, sizeof(box), hipMemcpyHostToDevice, st), "upload") ||
+            !ok(hipMemcpyAsync(d_seg, seg, sizeof(seg), hipMemcpyHostToDevice, st), "upload") ||
+            !ok(hipMemcpyAsync(d_job, job, sizeof(job), hipMemcpyHostToDevice, st), "upload") ||
+            !ok(launch_oct_classify(st, 1, d_cbox, d_seg, d_ent, d_tri9, d_mask, d_stats), "classify") ||
+            !ok(launch_oct_scatter(st, 1, 1, d_job, d_ent, d_mask, d_next, d_s0), "scatter") ||
+            !ok(hipMemcpyAsync(stats, d_stats, sizeof(stats), hipMemcpyDeviceToHost, st), "download") ||
+            !ok(hipStreamSynchronize(st), "sync"))
+            return RT_E_HIP;
+        std::swap(d_ent, d_next);
+        LNode root{rmn, rmx, 0, stats[1], 0, 0};
+        ob.nodes.clear();
+        std::vector<LNode> all{root};
+        std::vector<std::vector<int>> level_ents;
+        std::vector<int> frontier{0};
+        size_t cap_next = cap_ent;
+        while (!frontier.empty()) {
+            const int n = (int)frontier.size();
+            std::vector<float> cbox(48 * (size_t)n);
+            std::vector<int> segs(2 * (size_t)n);
+            int total = 0;
+            for (int i = 0; i < n; ++i) {
+                const LNode& N = all[frontier[i]];
+                F3 cmn[8], cmx[8];
+                OctBuild::child_boxes(N.mn, N.mx, cmn, cmx);
+                for (int k = 0; k < 8; ++k) {
+                    float* q = &cbox[48 * (size_t)i + 6 * k];
+                    q[0] = cmn[k].x; q[1] = cmn[k].y; q[2] = cmn[k].z; q[3] = cmx[k].x; q[4] = cmx[k].y; q[5] = cmx[k].z;
+                }
+                segs[2 * i] = N.begin; segs[2 * i + 1] = N.len;
+                total = std::max(total, N.begin + N.len);
+            }
+            if ((size_t)n > cap_nodes) {
+                cap_nodes = 2 * (size_t)n;
+                for (void* p : {(void*)d_cbox, (void*)d_seg, (void*)d_stats, (void*)d_job, (void*)d_s0}) {
+                    hipFree(p);
+                    owned.erase(std::find(owned.begin(), owned.end(), p));
+                }
+                if (!ok(dmalloc((void**)&d_cbox, 4 * 48 * cap_nodes), "alloc") ||
+                    !ok(dmalloc((void**)&d_seg, 4 * 2 * cap_nodes), "alloc") ||
+                    !ok(dmalloc((void**)&d_stats, 4 * 9 * cap_nodes), "alloc") ||
+                    !ok(dmalloc((void**)&d_job, 4 * 12 * cap_nodes), "alloc") ||
+                    !ok(dmalloc((void**)&d_s0, 4 * 8 * cap_nodes), "alloc"))
+                    return RT_E_OOM;
+            }
+            if ((size_t)total > cap_mask) {  // one mask byte per entry of the largest level
+                cap_mask = 2 * (size_t)total;
+                hipFree(d_mask);
+                owned.erase(std::find(owned.begin(), owned.end(), (void*)d_mask));
+                if (!ok(dmalloc((void**)&d_mask, cap_mask), "alloc")) return RT_E_OOM;
+            }
+            std::vector<int> stats(9 * (size_t)n);
+            level_ents.emplace_back((size_t)total);
+            if (!ok(hipMemcpyAsync(d_cbox, cbox.data(), 4 * cbox.size(), hipMemcpyHostToDevice, st), "upload") ||
+                !ok(hipMemcpyAsync(d_seg, segs.data(), 4 * segs.size(), hipMemcpyHostToDevice, st), "upload") ||
+                !ok(launch_oct_classify(st, n, d_cbox, d_seg, d_ent, d_tri9, d_mask, d_stats), "classify") ||
+                !ok(hipMemcpyAsync(stats.data(), d_stats, 4 * stats.size(), hipMemcpyDeviceToHost, st), "download") ||
+                !ok(hipMemcpyAsync(level_ents.back().data(), d_ent, 4 * (size_t)total, hipMemcpyDeviceToHost, st),
+                    "download") ||
+                !ok(hipStreamSynchronize(st), "sync"))
+                return RT_E_HIP;
+            // splits, in frontier (BFS) order; children laid out contiguously in the next level's sequence array
+            std::vector<int> jobs, next_frontier;
+            int running = 0;
+            for (int i = 0; i < n; ++i) {
+                LNode& N = all[frontier[i]];
+                const int* S = &stats[9 * (size_t)i];
+                int k = std::max(std::max(ob.capacity, N.s0 + 1), S[0] + 1);
+                if (k > N.len) continue;
+                N.trigger = level_ents.back()[(size_t)N.begin + k - 1];
+                N.first_child = (int)all.size();
+                int job[12] = {N.begin, N.len, k, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                F3 cmn[8], cmx[8];
+                OctBuild::child_boxes(N.mn, N.mx, cmn, cmx);
+                const int lvl = N.level;
+                for (int c = 0; c < 8; ++c) {
+                    job[3 + c] = running;
+                    all.push_back(LNode{cmn[c], cmx[c], running, S[1 + c], 0, lvl + 1});
+                    next_frontier.push_back((int)all.size() - 1);
+                    running += S[1 + c];
+                }
+                jobs.insert(jobs.end(), job, job + 12);
+            }
+            if (jobs.empty()) break;
+            const int nj = (int)jobs.size() / 12;
+            if ((size_t)running > cap_next) {
+                cap_next = 2 * (size_t)running;
+                hipFree(d_next);
+                owned.erase(std::find(owned.begin(), owned.end(), (void*)d_next));
+                if (!ok(dmalloc((void**)&d_next, 4 * cap_next), "alloc")) return RT_E_OOM;
+            }
+            std::vector<int> s0(8 * (size_t)nj);
+            if (!ok(hipMemcpyAsync(d_job, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice, st), "upload") ||
+                !ok(launch_oct_scatter(st, nj, 8, d_job, d_ent, d_mask, d_next, d_s0), "scatter") ||
+                !ok(hipMemcpyAsync(s0.data(), d_s0, 4 * s0.size(), hipMemcpyDeviceToHost, st), "download") ||
+                !ok(hipStreamSynchronize(st), "sync"))
+                return RT_E_HIP;
+            for (int j = 0; j < nj; ++j)
+                for (int c = 0; c < 8; ++c) all[next_frontier[8 * j + c]].s0 = s0[8 * (size_t)j + c];
+            std::swap(d_ent, d_next);
+            std::swap(cap_ent, cap_next);
+            frontier.swap(next_frontier);
+        }
+        // renumber: the sequential build appends a split node's 8 children when its trigger triangle is inserted
+        std::vector<int> splits;
+        for (int i = 0; i < (int)all.size(); ++i)
+            if (all[i].first_child >= 0) splits.push_back(i);
+        std::stable_sort(splits.begin(), splits.end(), [&](int a, int b) { return all[a].trigger < all[b].trigger; });
+        std::vector<int> seq(all.size(), -1);
+        seq[0] = 0;
+        for (size_t r = 0; r < splits.size(); ++r)
+            for (int c = 0; c < 8; ++c) seq[all[splits[r]].first_child + c] = 1 + 8 * (int)r + c;
+        ob.nodes.assign(all.size(), OctBuild::Node{});
+        for (int i = 0; i < (int)all.size(); ++i) {
+            const LNode& N = all[i];
+            OctBuild::Node& o = ob.nodes[seq[i]];
+            o.mn = N.mn; o.mx = N.mx;
+            if (N.first_child >= 0) {
+                o.first_child = seq[N.first_child];
+            } else {
+                const std::vector<int>& E = level_ents[N.level];
+                o.tris.assign(E.begin() + N.begin, E.begin() + N.begin + N.len);
+            }
+        }
+    }
+    return RT_OK;
+}
+
 // ---------------------------------------------------------------------------------------- buffers
 template <class T>
 struct DBuf {
@@ -238,6 +422,7 @@ struct DBuf {
 
 struct rt_ctx {
     int device = 0;
+    int octree_build = RT_OCTREE_BUILD_DEVICE;
     hipStream_t stream = nullptr;
     std::string err;
     bool have_scene = false, have_cam = false, have_smp = false, have_film = false, have_integ = false;
@@ -850,6 +1035,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RT_E_NODEVICE;
     rt_ctx* c = new rt_ctx();
     c->device = dev;
+    c->octree_build = opt ? opt->octree_build : RT_OCTREE_BUILD_DEVICE;
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return RT_E_HIP;
@@ -1011,7 +1197,13 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
     root.mn = rmn;
     root.mx = rmx;
     ob.nodes.push_back(root);
-    for (int t = 0; t < nt; ++t) ob.add(t);
+    if (c->octree_build == RT_OCTREE_BUILD_HOST) {
+        for (int t = 0; t < nt; ++t) ob.add(t);
+    } else {
+        std::string err;
+        int brc = octree_build_device(c->stream, ob, nt, err);
+        if (brc) return fail(c, brc, err);
+    }
     const int nn = (int)ob.nodes.size();
     // flatten: node SoA + two tile sets
     std::vector<float4> nA(nn), nB(nn);

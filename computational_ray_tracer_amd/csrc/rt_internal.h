@@ -198,6 +198,10 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
                                 unsigned long long* ctr);
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
                            int* out, unsigned long long* ctr);
+hipError_t launch_oct_classify(hipStream_t st, int nnodes, const float* cbox, const int* seg, const int* ent,
+                               const float* tri9, unsigned char* mask, int* stats);
+hipError_t launch_oct_scatter(hipStream_t st, int njobs, int nchild, const int* job, const int* ent,
+                              const unsigned char* mask, int* ent_next, int* s0);
 hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
                                  const ShadeRefIO& io, unsigned long long* ctr);
 hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,

@@ -11,10 +11,11 @@ from . import capi
 class Renderer:
     """One rt_ctx bound to one GPU.  Configured from a scene.Config (or the individual descriptors)."""
 
-    def __init__(self, cfg=None, device=0):
+    def __init__(self, cfg=None, device=0, octree_build=capi.RT_OCTREE_BUILD_DEVICE):
         self.lib = capi.load_library()
         opt = capi.rt_options()
         opt.device = device
+        opt.octree_build = octree_build
         h = C.c_void_p()
         rc = self.lib.rt_create(C.byref(opt), C.byref(h))
         if rc != capi.RT_OK:

@@ -39,8 +39,11 @@ typedef struct rt_ctx rt_ctx;
 
 typedef struct {
     int device;        /* HIP device ordinal                                              */
-    int reserved[7];
+    int octree_build;  /* RT_OCTREE_BUILD_DEVICE (default) or RT_OCTREE_BUILD_HOST         */
+    int reserved[6];
 } rt_options;
+/* Where rt_scene_upload builds the octree (Octtree_Model.h:33-63): both give the reference's tree bit for bit. */
+enum { RT_OCTREE_BUILD_DEVICE = 0, RT_OCTREE_BUILD_HOST = 1 };
 
 /* Film pixel, layout-identical to `pixel {glm::vec3 rgbsum; float weightsum;}` (Film.h:6-9). */
 typedef struct { float r, g, b, w; } rt_pixel;

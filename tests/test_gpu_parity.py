@@ -361,3 +361,68 @@ def test_pixel_sensor_reference_integrator_bitexact(oracle_lib):
     fg = g.render_pass(0, 3)
     fo = o.render(0, 3)
     assert np.array_equal(bits(fg), bits(fo))
+
+
+def _soup_config(pos, capacity):
+    n = len(pos) // 3
+    m = scene.TriModel(pos.astype(np.float32), np.tile([0, 0, 1], (len(pos), 1)).astype(np.float32),
+                       np.arange(len(pos), dtype=np.uint32).reshape(n, 3), rigid=np.eye(4) @ scene.PERM_YZ,
+                       octree_capacity=capacity, tri_material=np.zeros(n, np.int32))
+    m.materials = [(scene.grey_sigmoid(0.5), 0.0)]
+    return scene.Config("soup", m, scene.cornell_camera((8, 8)), scene.StratifiedSampler(1, 1, True, 0),
+                        scene.Film(res=(8, 8)), scene.Integrator(capi.RT_INTEGRATOR_PATH, max_depth=2), 0, 1)
+
+
+def _soups():
+    rng = np.random.default_rng(21)
+    out = []
+    # random triangle soup (small and large triangles) at several capacities
+    c = rng.uniform(0, 100, (3000, 1, 3))
+    soup = c + rng.normal(size=(3000, 3, 3)) * rng.choice([0.5, 5.0, 30.0], (3000, 1, 1))
+    out += [(soup[rng.random(3000) < 0.3][:600] / 3, 4), (soup, 40)]
+    # clustered: 300 copies of one tiny triangle among a few hundred others -> repeated aborted splits
+    tiny = np.array([[[10, 10, 10], [10.01, 10, 10], [10, 10.01, 10]]]).repeat(300, 0)
+    other = rng.uniform(0, 50, (400, 1, 3)) + rng.normal(size=(400, 3, 3))
+    mix = np.concatenate([other[:200], tiny, other[200:]])
+    out.append((mix, 40))
+    # axis-aligned grid of quads (ties on child-box boundaries)
+    g = []
+    for i in range(30):
+        for j in range(30):
+            a, b, cc, d = [i, j, 0], [i + 1, j, 0], [i + 1, j + 1, 0], [i, j + 1, 0]
+            g += [[a, b, cc], [a, cc, d]]
+    out.append((np.array(g, float) * 3.0, 8))
+    return out
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_device_octree_build_equals_sequential(oracle_lib, case):
+    """rt_options.octree_build: the level-synchronous device build (rt_octree.hip) reproduces the reference's
+    insertion-order tree — same nodes, same numbering, same leaf lists — as the host's sequential build and the
+    oracle, including aborted splits, tiny capacities and triangles on child-box boundaries."""
+    tris, cap = _soups()[case]
+    cfg = _soup_config(tris.reshape(-1, 3)[:, [0, 2, 1]], cap)   # object space = world with y/z swapped
+    gd = Renderer(cfg, octree_build=capi.RT_OCTREE_BUILD_DEVICE).octree()
+    gh = Renderer(cfg, octree_build=capi.RT_OCTREE_BUILD_HOST).octree()
+    go = oracle_lib.OracleScene(cfg).octree()
+    for a in (gh, go):
+        assert np.array_equal(bits(gd["bounds"]), bits(a["bounds"]))
+        assert np.array_equal(gd["child"], a["child"])
+        assert np.array_equal(gd["leaf_count"], a["leaf_count"])
+        assert np.array_equal(gd["refs"], a["refs"])
+    assert len(gd["child"]) > 9
+
+
+def test_device_octree_build_cfg3_matches_host(cfg3_pair):
+    import time
+    cfg, gdev, _ = cfg3_pair
+    t0 = time.perf_counter()
+    gh = Renderer(cfg, octree_build=capi.RT_OCTREE_BUILD_HOST)
+    t_host = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    gd = Renderer(cfg, octree_build=capi.RT_OCTREE_BUILD_DEVICE)
+    t_dev = time.perf_counter() - t0
+    a, b = gd.octree(), gh.octree()
+    for k in ("bounds", "child", "leaf_count", "refs"):
+        assert np.array_equal(bits(a[k]) if k == "bounds" else a[k], bits(b[k]) if k == "bounds" else b[k])
+    print(f"\nCFG3 scene upload: host build {t_host * 1e3:.0f} ms, device build {t_dev * 1e3:.0f} ms")
