@@ -29,8 +29,13 @@ RT_DEV void sincos_det(float x, float& s, float& c) {
     s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
     c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
 }
+#ifdef RT_PROFILE_FLOAT_WARPS  // timing experiments only: float atanh/cosh (results differ from the oracle)
+RT_DEV float f_atanh(float x) { return atanhf(x); }
+RT_DEV float f_cosh(float x) { return coshf(x); }
+#else
 RT_DEV float f_atanh(float x) { return (float)atanh((double)x); }
 RT_DEV float f_cosh(float x) { return (float)cosh((double)x); }
+#endif
 
 // helpers.h:50-54
 RT_DEV float gamma_n(int n) {

@@ -421,6 +421,13 @@ struct DBuf {
 }  // namespace
 
 struct rt_ctx {
+    // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers, scene quantisation
+    float4 *sO = nullptr, *sD = nullptr;
+    int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;
+    unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
+    void* sTemp = nullptr;
+    size_t sTempBytes = 0, sCap = 0;
+    float4 sort_lo{}, sort_scale{};
     int device = 0;
     int octree_build = RT_OCTREE_BUILD_DEVICE;
     hipStream_t stream = nullptr;
@@ -500,7 +507,31 @@ void free_scene(rt_ctx* c) {
     c->have_scene = false;
 }
 
+void free_sort_workspace(rt_ctx* c) {
+    void* ptrs[] = {c->sO, c->sD, c->sS, c->sVals, c->sValsAlt, c->sKeys, c->sKeysAlt, c->sTemp};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    c->sO = c->sD = nullptr;
+    c->sS = c->sVals = c->sValsAlt = nullptr;
+    c->sKeys = c->sKeysAlt = nullptr;
+    c->sTemp = nullptr;
+    c->sTempBytes = c->sCap = 0;
+}
+
+int ensure_sort_workspace(rt_ctx* c, size_t n) {
+    if (c->sCap >= n) return RT_OK;
+    free_sort_workspace(c);
+    HIPCHK(c, dalloc(&c->sO, n)); HIPCHK(c, dalloc(&c->sD, n)); HIPCHK(c, dalloc(&c->sS, n));
+    HIPCHK(c, dalloc(&c->sVals, n)); HIPCHK(c, dalloc(&c->sValsAlt, n));
+    HIPCHK(c, dalloc(&c->sKeys, n)); HIPCHK(c, dalloc(&c->sKeysAlt, n));
+    c->sTempBytes = sort_rays_temp_bytes((int)n);
+    HIPCHK(c, hipMalloc(&c->sTemp, std::max<size_t>(c->sTempBytes, 16)));
+    c->sCap = n;
+    return RT_OK;
+}
+
 void free_workspace(rt_ctx* c) {
+    free_sort_workspace(c);
     void* ptrs[] = {c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->betaA, c->betaB,
                     c->LA, c->LB, c->slot, c->hitPrim, c->dim, c->rng, c->prevPdf};
     for (void* p : ptrs)
@@ -780,6 +811,12 @@ int check_ready(rt_ctx* c) {
 #ifndef RT_CLUSTER_PAD_REL
 #define RT_CLUSTER_PAD_REL 1e-5f  // cluster-box inflation per unit of scene extent (see upload)
 #endif
+#ifndef RT_SORT_RAYS
+#define RT_SORT_RAYS 1  // multi-level octrees: coherence-sort each bounce's rays (rt_sort.hip)
+#endif
+#ifndef RT_KZ_BINS_HOST
+#define RT_KZ_BINS_HOST 0  // must match the kernels' RT_KZ_BINS: the sort reads bin 0 as one contiguous queue
+#endif
 #ifndef RT_LEAN_GENERATE
 #define RT_LEAN_GENERATE 1
 #endif
@@ -806,6 +843,8 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     B = std::min(B, ie - ib);
     size_t nmax = (size_t)B * c->n_work;
     if ((rc = ensure_workspace(c, nmax, path))) return rc;
+    const bool sort_rays = RT_SORT_RAYS && path && c->dsc.qcap != 1 && !RT_KZ_BINS_HOST;
+    if (sort_rays && (rc = ensure_sort_workspace(c, nmax))) return rc;
     DevCamera cam = dev_camera(c->cam);
     DevFilm fd = dev_film(c);
     for (int b0 = ib; b0 < ie; b0 += B) {
@@ -841,12 +880,24 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 if (depth == c->integ.max_depth && depth > 0 && !c->dsc.full) break;
                 int nxt = cur ^ 1;
                 const size_t qs = 3 * nmax;  // one queue = 3 bins of nmax
-                float4* cO = c->rayO + (size_t)cur * qs;
-                float4* cD = c->rayD + (size_t)cur * qs;
-                int* cS = c->slot + (size_t)cur * qs;
+                const float4* cO = c->rayO + (size_t)cur * qs;
+                const float4* cD = c->rayD + (size_t)cur * qs;
+                const int* cS = c->slot + (size_t)cur * qs;
                 int* qc_cur = c->d_qcount + 3 * kQStride * cur;
                 int* qc_nxt = c->d_qcount + 3 * kQStride * nxt;
                 HIPCHK(c, hipMemsetAsync(qc_nxt, 0, 3 * kQStride * sizeof(int), st));
+                // multi-level octrees: bounce rays regrouped by (octant, origin Morton code) before the trace
+                if (sort_rays && depth > 0) {
+                    int nq = 0;
+                    HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, st));
+                    HIPCHK(c, hipStreamSynchronize(st));
+                    SortRaysIO so{cO, cD, cS, c->sO, c->sD, c->sS, c->sKeys, c->sKeysAlt, c->sVals, c->sValsAlt,
+                                  c->sTemp, c->sTempBytes, c->sort_lo, c->sort_scale};
+                    e0 = ev_start(c, st);
+                    HIPCHK(c, launch_sort_rays(st, nq, so));
+                    ev_mark(c, st, ST_TRACE, e0);
+                    cO = c->sO; cD = c->sD; cS = c->sS;
+                }
                 const bool fused = RT_FUSED_BOUNCE && !c->dsc.full;  // simple scenes: trace inside the shade kernel
                 if (!fused) {
                     TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, c->hitB, c->hitPrim};
@@ -1188,6 +1239,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
         m4v(s->object_to_render, q.x, q.y, q.z, 1.f, o);
         rmn = {std::min(rmn.x, o[0]), std::min(rmn.y, o[1]), std::min(rmn.z, o[2])};
         rmx = {std::max(rmx.x, o[0]), std::max(rmx.y, o[1]), std::max(rmx.z, o[2])};
+    }
+    {  // ray coherence sort: origins quantised to 9 bits per axis over the root box
+        F3 e = f3sub(rmx, rmn);
+        auto sc = [](float x) { return x > 0 ? 512.0f / x : 0.0f; };
+        c->sort_lo = make_float4(rmn.x, rmn.y, rmn.z, 0.f);
+        c->sort_scale = make_float4(sc(e.x), sc(e.y), sc(e.z), 0.f);
     }
     // octree build (all triangles, culled and degenerate included — the reference inserts every triangle)
     OctBuild ob;

@@ -198,6 +198,15 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
                                 unsigned long long* ctr);
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
                            int* out, unsigned long long* ctr);
+struct SortRaysIO {
+    const float4* o; const float4* d; const int* slot;   // the queue (bin 0, contiguous)
+    float4* so; float4* sd; int* ss;                      // the sorted side queue
+    unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
+    void* temp; size_t temp_bytes;
+    float4 lo, scale;                                     // origin quantisation: (p - lo) * scale in [0, 512)
+};
+size_t sort_rays_temp_bytes(int nmax);
+hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io);
 hipError_t launch_oct_classify(hipStream_t st, int nnodes, const float* cbox, const int* seg, const int* ent,
                                const float* tri9, unsigned char* mask, int* stats);
 hipError_t launch_oct_scatter(hipStream_t st, int njobs, int nchild, const int* job, const int* ent,
