@@ -814,6 +814,9 @@ int check_ready(rt_ctx* c) {
 #ifndef RT_SORT_RAYS
 #define RT_SORT_RAYS 1  // multi-level octrees: coherence-sort each bounce's rays (rt_sort.hip)
 #endif
+#ifndef RT_SORT_SINGLE_LEAF
+#define RT_SORT_SINGLE_LEAF 0  // also sort on single-leaf scenes (the Cornell box)
+#endif
 #ifndef RT_KZ_BINS_HOST
 #define RT_KZ_BINS_HOST 0  // must match the kernels' RT_KZ_BINS: the sort reads bin 0 as one contiguous queue
 #endif
@@ -843,7 +846,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     B = std::min(B, ie - ib);
     size_t nmax = (size_t)B * c->n_work;
     if ((rc = ensure_workspace(c, nmax, path))) return rc;
-    const bool sort_rays = RT_SORT_RAYS && path && c->dsc.qcap != 1 && !RT_KZ_BINS_HOST;
+    const bool sort_rays = RT_SORT_RAYS && path && (c->dsc.qcap != 1 || RT_SORT_SINGLE_LEAF) && !RT_KZ_BINS_HOST;
     if (sort_rays && (rc = ensure_sort_workspace(c, nmax))) return rc;
     DevCamera cam = dev_camera(c->cam);
     DevFilm fd = dev_film(c);

@@ -6,8 +6,21 @@
 
 #include "rt_internal.h"
 
+#ifndef RT_SORT_KEY
+#define RT_SORT_KEY 4
+#endif
+#ifndef RT_SORT_DIRB
+#define RT_SORT_DIRB 3       // direction: octant + 2 x DIRB bits of the octahedral position
+#endif
+#ifndef RT_SORT_ORGB
+#define RT_SORT_ORGB 7       // origin: ORGB bits per axis (Morton)
+#endif
+
 namespace rtmi {
 namespace {
+
+constexpr int kKeyBits = RT_SORT_KEY == 4 ? 3 + 2 * RT_SORT_DIRB + 3 * RT_SORT_ORGB : 30;
+static_assert(kKeyBits <= 32, "sort key wider than 32 bits");
 
 __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every third bit of 27
     v &= 0x1ffu;
@@ -30,7 +43,21 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const float4
         unsigned m = spread3(q((p.x - lo.x) * scale.x)) << 2 | spread3(q((p.y - lo.y) * scale.y)) << 1 |
                      spread3(q((p.z - lo.z) * scale.z));
         unsigned oct = (v.x < 0.f ? 4u : 0u) | (v.y < 0.f ? 2u : 0u) | (v.z < 0.f ? 1u : 0u);
-        keys[k] = oct << 27 | m;
+#if RT_SORT_KEY == 1
+        keys[k] = m << 3 | oct;  // origin-major
+#elif RT_SORT_KEY == 4
+        {  // octant, then the octahedral position on a 2^B x 2^B grid, then an origin Morton code of 3 x ORGB bits
+            constexpr int B = RT_SORT_DIRB, OB = RT_SORT_ORGB;
+            float s = fabsf(v.x) + fabsf(v.y) + fabsf(v.z);
+            const float G = (float)(1 << B);
+            unsigned ux = (unsigned)fminf(fabsf(v.x) / s * G, G - 1), uy = (unsigned)fminf(fabsf(v.y) / s * G, G - 1);
+            unsigned mo = spread3(q((p.x - lo.x) * scale.x) >> (9 - OB)) << 2 |
+                          spread3(q((p.y - lo.y) * scale.y) >> (9 - OB)) << 1 | spread3(q((p.z - lo.z) * scale.z) >> (9 - OB));
+            keys[k] = ((oct << (2 * B) | ux << B | uy) << (3 * OB)) | mo;
+        }
+#else
+        keys[k] = oct << 27 | m;  // direction octant first
+#endif
         vals[k] = k;
     }
 }
@@ -53,7 +80,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int*
 size_t sort_rays_temp_bytes(int nmax) {
     size_t bytes = 0;
     hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned*)nullptr, (unsigned*)nullptr,
-                                       (const int*)nullptr, (int*)nullptr, nmax, 0, 30);
+                                       (const int*)nullptr, (int*)nullptr, nmax, 0, kKeyBits);
     return bytes;
 }
 
@@ -65,7 +92,7 @@ hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
                        io.vals);
     size_t bytes = io.temp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
-                                                      30, st);
+                                                      kKeyBits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.o, io.d, io.slot, io.so,
                        io.sd, io.ss);
