@@ -21,6 +21,9 @@
 #include "../../include/rtmi355x.h"
 #include "../data/spectra_data.h"
 #include "../data/sensor_data.h"
+#ifndef RT_DYN_SCHED
+#define RT_DYN_SCHED 2  // path-mode trace / shade launches take chunks from a ticket counter (BlockChunks):
+#endif                  // 0 never, 1 always, 2 multi-level octrees only (single-leaf scenes: equal per-ray cost)
 #include "rt_internal.h"
 
 using namespace rtmi;
@@ -464,7 +467,8 @@ struct rt_ctx {
     int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
     float* prevPdf = nullptr;
     uint4* rng = nullptr;
-    int* d_qcount = nullptr;   // queue q, bin b length at [(3q + b) * kQStride] (separate cache lines)
+    int* d_qcount = nullptr;   // queue q: bin b length at [q * kQRegion + b * kQStride], trace / shade chunk tickets
+                               // at [q * kQRegion + 3 / 4 * kQStride] (separate cache lines)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     float* d_cdf = nullptr;    // Gaussian / Lanczos filter tables: x then y, cdf_n + 1 floats each
@@ -848,6 +852,9 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     if ((rc = ensure_workspace(c, nmax, path))) return rc;
     const bool sort_rays = RT_SORT_RAYS && path && (c->dsc.qcap != 1 || RT_SORT_SINGLE_LEAF) && !RT_KZ_BINS_HOST;
     if (sort_rays && (rc = ensure_sort_workspace(c, nmax))) return rc;
+    // Cornell-like single-leaf scenes cost the same per ray: static chunks on a resident grid beat tickets there
+    // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
+    const bool dyn = RT_DYN_SCHED == 1 || (RT_DYN_SCHED == 2 && c->dsc.qcap != 1);
     DevCamera cam = dev_camera(c->cam);
     DevFilm fd = dev_film(c);
     for (int b0 = ib; b0 < ie; b0 += B) {
@@ -876,7 +883,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
         } else {
             // camera rays fill bin 0 of queue 0 (flat order); bins 1, 2 start empty
             int cur = 0;
-            HIPCHK(c, hipMemsetAsync(c->d_qcount, 0, 6 * kQStride * sizeof(int), st));
+            HIPCHK(c, hipMemsetAsync(c->d_qcount, 0, 2 * kQRegion * sizeof(int), st));
             HIPCHK(c, hipMemcpyAsync(c->d_qcount, &nS, sizeof(int), hipMemcpyHostToDevice, st));
             for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
                 // the last trace can only add emitter hits, which count only after specular bounces or with MIS
@@ -886,9 +893,10 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 const float4* cO = c->rayO + (size_t)cur * qs;
                 const float4* cD = c->rayD + (size_t)cur * qs;
                 const int* cS = c->slot + (size_t)cur * qs;
-                int* qc_cur = c->d_qcount + 3 * kQStride * cur;
-                int* qc_nxt = c->d_qcount + 3 * kQStride * nxt;
-                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, 3 * kQStride * sizeof(int), st));
+                int* qc_cur = c->d_qcount + kQRegion * cur;
+                int* qc_nxt = c->d_qcount + kQRegion * nxt;
+                // the next queue's bin lengths and the chunk tickets its trace and shade launches will use
+                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, kQRegion * sizeof(int), st));
                 // multi-level octrees: bounce rays regrouped by (octant, origin Morton code) before the trace
                 if (sort_rays && depth > 0) {
                     int nq = 0;
@@ -903,7 +911,8 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 }
                 const bool fused = RT_FUSED_BOUNCE && !c->dsc.full;  // simple scenes: trace inside the shade kernel
                 if (!fused) {
-                    TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, c->hitB, c->hitPrim};
+                    TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, c->hitB, c->hitPrim,
+                                 dyn ? qc_cur + 3 * kQStride : nullptr};
                     e0 = ev_start(c, st);
                     HIPCHK(c, launch_trace_closest(st, c->grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
                     ev_mark(c, st, ST_TRACE, e0);
@@ -920,6 +929,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 pio.lamA = c->lamA; pio.lamB = c->lamB; pio.pdfA = c->pdfA; pio.pdfB = c->pdfB;
                 pio.prevPdf = c->prevPdf;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
+                pio.ticket = dyn ? qc_cur + 4 * kQStride : nullptr;
                 e0 = ev_start(c, st);
                 HIPCHK(c, launch_path_shade(st, c->grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
                 ev_mark(c, st, ST_SHADE, e0);
@@ -1096,7 +1106,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     }
     c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
     c->hs.init();
-    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 6 * kQStride) != hipSuccess ||
+    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 2 * kQRegion) != hipSuccess ||
         dalloc(&c->d_ctr, (size_t)C_NCOUNTERS) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
         rt_destroy(c);
         return RT_E_OOM;

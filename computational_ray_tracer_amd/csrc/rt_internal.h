@@ -138,6 +138,7 @@ struct GenOut {
 // kz, Shapes.h:1145): bin b holds rays at ray[b*bstride + i], i < count[b*cstride].  Entries are addressed by
 // a flat index k over bin 0, then 1, then 2, so every wave but the two at bin seams sees one kz.
 static const int kQStride = 64;
+static const int kQRegion = 5 * kQStride;  // one queue's counters: 3 bin lengths + 2 chunk tickets
 static const int kBlockThreads = 256;  // threads per block of every kernel
 #ifndef RT_CLUSTER_TRIS
 #define RT_CLUSTER_TRIS 2
@@ -155,6 +156,7 @@ struct TraceIO {
     int set;                  // tile set: 0 = all triangles, 1 = back-face culled
     float4* hitB;             // (b0, b1, b2, t) at flat index
     int* hitPrim;
+    int* ticket = nullptr;    // dynamic chunk counter (zeroed before the launch) or nullptr: static grid-stride
 };
 
 struct ShadeRefIO {
@@ -176,6 +178,7 @@ struct PathIO {
     int depth, max_depth;
     int fused;  // simple scenes: the closest-hit traversal runs inside the shade kernel (no hit records)
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
+    int* ticket;  // dynamic chunk counter (zeroed before the launch) or nullptr: static grid-stride
 };
 
 struct PathFilmIO {

@@ -13,6 +13,10 @@
 // and dominant-axis bin, so trace waves see one watertight-test permutation.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <type_traits>
+#include <unordered_map>
+
 #include "rt_device.h"
 
 namespace rtmi {
@@ -173,6 +177,80 @@ __device__ __forceinline__ size_t queue_pos(int k, int c0, int c1, size_t bstrid
     if (k < c0) return (size_t)k;
     if (k < c0 + c1) return bstride + (size_t)(k - c0);
     return 2 * bstride + (size_t)(k - c0 - c1);
+}
+
+// Work distribution of the persistent queue kernels.  With a ticket counter (zeroed before the launch) a block takes
+// the next chunk of RT_DYN_ITEMS x kBlock items whenever it finishes one, so blocks whose rays are expensive
+// (incoherent bounces, big leaves) do not hold back the launch; the next ticket is requested while the current chunk
+// runs.  Without one, block b takes chunks b, b + grid, ... of RT_STATIC_ITEMS x kBlock items.  Every thread of the
+// block must call next().
+#ifndef RT_DYN_ITEMS
+#define RT_DYN_ITEMS 1     // items per thread per ticket (dynamic chunks)
+#endif
+#ifndef RT_STATIC_ITEMS
+#define RT_STATIC_ITEMS 2  // items per thread per chunk without a ticket
+#endif
+struct BlockChunks {
+    int* ticket;
+    int pref, it, size, lane, step;
+    __device__ __forceinline__ explicit BlockChunks(int* t)
+        : ticket(t), pref(0), it(0), size((t ? RT_DYN_ITEMS : RT_STATIC_ITEMS) * kBlock), lane(threadIdx.x),
+          step(kBlock) {
+        if (ticket && threadIdx.x == 0) pref = atomicAdd(ticket, 1);
+    }
+    // first item of the block's next chunk (>= n once the queue is drained)
+    __device__ __forceinline__ int next(int* lds) {
+        if (!ticket) return (blockIdx.x + (it++) * gridDim.x) * size;
+        if (threadIdx.x == 0) { *lds = pref; pref = atomicAdd(ticket, 1); }
+        __syncthreads();
+        int c = *lds;
+        __syncthreads();
+        return c * size;
+    }
+};
+
+// The same for kernels without block-level synchronisation: with a ticket each wave takes RT_WAVE_ITEMS x 64 items
+// per ticket; without one the block-static mapping of BlockChunks.
+#ifndef RT_SHADE_WAVE
+#define RT_SHADE_WAVE 1    // multi-level octrees: shade kernels take per-wave tickets and append per wave
+#endif
+#ifndef RT_WAVE_ITEMS
+#define RT_WAVE_ITEMS 1
+#endif
+struct WaveChunks {
+    int* ticket;
+    int pref, it, size, lane, step;
+    __device__ __forceinline__ explicit WaveChunks(int* t) : ticket(t), pref(0), it(0) {
+        if (ticket) {
+            size = RT_WAVE_ITEMS * 64; lane = lane_id(); step = 64;
+            if (lane == 0) pref = atomicAdd(ticket, 1);
+        } else {
+            size = RT_STATIC_ITEMS * kBlock; lane = threadIdx.x; step = kBlock;
+        }
+    }
+    __device__ __forceinline__ int next() {
+        if (!ticket) return (blockIdx.x + (it++) * gridDim.x) * size;
+        int c = __shfl(pref, 0);
+        if (lane == 0) pref = atomicAdd(ticket, 1);
+        return c * size;
+    }
+    __device__ __forceinline__ int next(int*) { return next(); }
+};
+// Append to the next binned queue: per wave (one atomic per bin per wave; WaveChunks kernels, no block-level
+// synchronisation) or per block (block_append_bin).
+template <bool WAVE>
+__device__ __forceinline__ long queue_append(int* counters, int bin, size_t bstride, int* lds) {
+    if constexpr (!WAVE) {
+        return block_append_bin(counters, bin, bstride, lds);
+    } else {
+        long pos = -1;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            int p = wave_append(counters + b * kQStride, bin == b);
+            if (bin == b) pos = (long)b * (long)bstride + p;
+        }
+        return pos;
+    }
 }
 
 // the PCG increment of a path never changes after generation: only the 8-byte state half is written back
@@ -627,7 +705,10 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
         __syncthreads();
         if (k >= n) continue;
 #else
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    // no block-level synchronisation here: each wave takes its own tickets (WaveChunks)
+    WaveChunks chunks(io.ticket);
+    for (int cb = chunks.next(); cb < n; cb = chunks.next())
+    for (int k = cb + chunks.lane; k < cb + chunks.size && k < n; k += chunks.step) {
         size_t q = queue_pos(k, c0, c1, io.bstride);
         float4 o4 = io.rayO[q], d4 = io.rayD[q];
 #endif
@@ -757,8 +838,13 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
     unsigned long long snn = 0, snt = 0, nsh = 0, tnn = 0, tnt = 0, tnh = 0, tnr = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
-    for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-        int k = base + threadIdx.x;
+    // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
+    constexpr bool WAVE = RT_SHADE_WAVE && QCAP != 1;
+    __shared__ int s_tk;
+    std::conditional_t<WAVE, WaveChunks, BlockChunks> chunks(io.ticket);
+    for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
+    for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
+        int k = base + chunks.lane;
         bool wantShadow = false, wantNext = false, storedL = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int nbin = -1;
@@ -905,7 +991,7 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
 #if RT_RAY_SORT
         long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
 #else
-        long pn = block_append_bin(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
+        long pn = queue_append<WAVE>(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
 #endif
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
     }
@@ -977,8 +1063,13 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
     int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
     int n = c0 + c1 + c2;
     unsigned long long snn = 0, snt = 0, nsh = 0;
-    for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-        int k = base + threadIdx.x;
+    // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
+    constexpr bool WAVE = RT_SHADE_WAVE && QCAP != 1;
+    __shared__ int s_tk;
+    std::conditional_t<WAVE, WaveChunks, BlockChunks> chunks(io.ticket);
+    for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
+    for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
+        int k = base + chunks.lane;
         bool wantNext = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int nbin = -1, slot = -1;
@@ -1194,7 +1285,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
 #if RT_RAY_SORT
         long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
 #else
-        long pn = block_append_bin(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
+        long pn = queue_append<WAVE>(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
 #endif
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
     }
@@ -1285,6 +1376,36 @@ static inline int grid_for(int n, int grid) {
     return g < 1 ? 1 : g;
 }
 
+#ifndef RT_GRID_OCC
+#define RT_GRID_OCC 1
+#endif
+// Persistent grid-stride kernels: every block gets the same share of the queue, so launching more blocks than can
+// be resident at once (grid = 8 per CU, occupancy 4-5 per CU) runs a second, under-occupied round of blocks.
+// RT_GRID_OCC clamps the grid to exactly the resident block count of the kernel (`grid` is CUs x 8).
+template <class F>
+static int resident_grid(F kern, int gb, int grid) {
+#if RT_GRID_OCC
+    static std::mutex mu;
+    static std::unordered_map<const void*, int> cache;
+    int per_cu = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find((const void*)kern);
+        if (it == cache.end()) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, 0) != hipSuccess) per_cu = 0;
+            cache[(const void*)kern] = per_cu;
+        } else {
+            per_cu = it->second;
+        }
+    }
+    if (per_cu > 0) {
+        int res = per_cu * (grid / 8);
+        if (res > 0 && gb > res) gb = res;
+    }
+#endif
+    return gb;
+}
+
 hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& ids, const DevCamera& cam,
                            const DevSampler& smp, const DevFilm& film, const GenOut& out) {
     hipLaunchKernelGGL(k_generate, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
@@ -1295,11 +1416,11 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
                                 unsigned long long* ctr) {
     int gb = grid_for(io.count ? grid * kBlock : io.n, grid);
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
-    dim3 g(gb), b(kBlock);
+    dim3 b(kBlock);
     switch (qcap) {
-        case 0: hipLaunchKernelGGL(k_trace_closest<0>, g, b, 0, st, sc, io, ctr); break;
-        case 1: hipLaunchKernelGGL(k_trace_closest<1>, g, b, 0, st, sc, io, ctr); break;
-        case 16: hipLaunchKernelGGL(k_trace_closest<16>, g, b, 0, st, sc, io, ctr); break;
+        case 0: hipLaunchKernelGGL(k_trace_closest<0>, dim3(resident_grid(k_trace_closest<0>, gb, grid)), b, 0, st, sc, io, ctr); break;
+        case 1: hipLaunchKernelGGL(k_trace_closest<1>, dim3(resident_grid(k_trace_closest<1>, gb, grid)), b, 0, st, sc, io, ctr); break;
+        case 16: hipLaunchKernelGGL(k_trace_closest<16>, dim3(resident_grid(k_trace_closest<16>, gb, grid)), b, 0, st, sc, io, ctr); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1322,12 +1443,18 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
                              unsigned long long* ctr) {
     int gb = grid > 0 ? grid : 1;
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
-    dim3 g(gb), b(kBlock);
+    dim3 b(kBlock);
 #define RT_SHADE_CASE(Q)                                                                                         \
     case Q:                                                                                                      \
-        if (sc.full) hipLaunchKernelGGL(k_path_shade_full<Q>, g, b, 0, st, sc, sp, smp, film, ids, io, ctr);    \
-        else if (io.fused) hipLaunchKernelGGL((k_path_shade<Q, true>), g, b, 0, st, sc, sp, smp, film, ids, io, ctr); \
-        else hipLaunchKernelGGL((k_path_shade<Q, false>), g, b, 0, st, sc, sp, smp, film, ids, io, ctr);          \
+        if (sc.full)                                                                                             \
+            hipLaunchKernelGGL(k_path_shade_full<Q>, dim3(resident_grid(k_path_shade_full<Q>, gb, grid)), b, 0, st, \
+                               sc, sp, smp, film, ids, io, ctr);                                                 \
+        else if (io.fused)                                                                                       \
+            hipLaunchKernelGGL((k_path_shade<Q, true>), dim3(resident_grid(k_path_shade<Q, true>, gb, grid)), b, 0, \
+                               st, sc, sp, smp, film, ids, io, ctr);                                             \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_path_shade<Q, false>), dim3(resident_grid(k_path_shade<Q, false>, gb, grid)), b, \
+                               0, st, sc, sp, smp, film, ids, io, ctr);                                          \
         break;
     switch (qcap) {
         RT_SHADE_CASE(0)
@@ -1355,7 +1482,7 @@ hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, 
 
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr) {
-    hipLaunchKernelGGL(k_path_film, dim3(grid_for(io.n_pixels, grid)), dim3(kBlock), 0, st, sp, film, io, ctr);
+    hipLaunchKernelGGL(k_path_film, dim3(resident_grid(k_path_film, grid_for(io.n_pixels, grid), grid)), dim3(kBlock), 0, st, sp, film, io, ctr);
     return hipGetLastError();
 }
 
