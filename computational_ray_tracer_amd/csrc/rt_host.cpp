@@ -9,6 +9,7 @@
 // There is no CPU fallback: every pass runs on the MI355X; rt_create fails without a gfx950 device.
 #include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -21,6 +22,9 @@
 #include "../../include/rtmi355x.h"
 #include "../data/spectra_data.h"
 #include "../data/sensor_data.h"
+#ifndef RT_LANES
+#define RT_LANES 2  // path-mode batches in flight on separate streams (4 lanes with 4 Mi-sample batches: 1150)
+#endif
 #ifndef RT_DYN_SCHED
 #define RT_DYN_SCHED 2  // path-mode trace / shade launches take chunks from a ticket counter (BlockChunks):
 #endif                  // 0 never, 1 always, 2 multi-level octrees only (single-leaf scenes: equal per-ray cost)
@@ -423,13 +427,32 @@ struct DBuf {
 
 }  // namespace
 
-struct rt_ctx {
-    // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers, scene quantisation
+// The device buffers of one batch in flight (grown on demand).  Path mode keeps kLanes of them so that consecutive
+// batches run concurrently on separate streams: one batch's VALU-bound traversal overlaps the other's HBM-bound
+// path-state traffic.
+static const int kLanes = 4;
+struct Work {
+    size_t cap = 0;
+    float4 *rayO = nullptr, *rayD = nullptr, *lamA = nullptr, *lamB = nullptr, *pdfA = nullptr, *pdfB = nullptr;
+    float4* hitB = nullptr;
+    float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr;
+    int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
+    float* prevPdf = nullptr;
+    uint4* rng = nullptr;
+    int* d_qcount = nullptr;   // queue q: bin b length at [q * kQRegion + b * kQStride], trace / shade chunk tickets
+                               // at [q * kQRegion + (RT_NBINS, RT_NBINS + 1) * kQStride] (separate cache lines)
+    // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers
     float4 *sO = nullptr, *sD = nullptr;
     int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
     void* sTemp = nullptr;
     size_t sTempBytes = 0, sCap = 0;
+    hipStream_t stream = nullptr;  // lanes >= 1: own stream (lane 0 runs on the caller's stream)
+    hipEvent_t film_done = nullptr;
+};
+
+struct rt_ctx {
+    // coherence sort of path queues (multi-level octrees): scene quantisation of the sort key
     float4 sort_lo{}, sort_scale{};
     int device = 0;
     int octree_build = RT_OCTREE_BUILD_DEVICE;
@@ -459,16 +482,11 @@ struct rt_ctx {
     bool work_dirty = true;
     int n_work = 0;
     int* d_work = nullptr;
-    // workspace (grown on demand)
-    size_t cap = 0;
-    float4 *rayO = nullptr, *rayD = nullptr, *lamA = nullptr, *lamB = nullptr, *pdfA = nullptr, *pdfB = nullptr;
-    float4* hitB = nullptr;
-    float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr;
-    int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
-    float* prevPdf = nullptr;
-    uint4* rng = nullptr;
-    int* d_qcount = nullptr;   // queue q: bin b length at [q * kQRegion + b * kQStride], trace / shade chunk tickets
-                               // at [q * kQRegion + 3 / 4 * kQStride] (separate cache lines)
+    // batch workspaces, one per lane (path mode runs kLanes batches concurrently on separate streams)
+    Work ws[kLanes];
+    int lanes = RT_LANES;  // batches in flight in path mode (RTMI_LANES overrides)
+    int grid_div = 1;      // persistent-grid divisor with lanes > 1 (RTMI_GRID_DIV overrides; A/B: 1 beats 2)
+    size_t batch_samples = 0;  // samples in flight per batch (0: 8 Mi path / 16 Mi reference; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     float* d_cdf = nullptr;    // Gaussian / Lanczos filter tables: x then y, cdf_n + 1 floats each
@@ -511,60 +529,72 @@ void free_scene(rt_ctx* c) {
     c->have_scene = false;
 }
 
-void free_sort_workspace(rt_ctx* c) {
-    void* ptrs[] = {c->sO, c->sD, c->sS, c->sVals, c->sValsAlt, c->sKeys, c->sKeysAlt, c->sTemp};
+void free_sort_workspace(Work& w) {
+    void* ptrs[] = {w.sO, w.sD, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sTemp};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    c->sO = c->sD = nullptr;
-    c->sS = c->sVals = c->sValsAlt = nullptr;
-    c->sKeys = c->sKeysAlt = nullptr;
-    c->sTemp = nullptr;
-    c->sTempBytes = c->sCap = 0;
+    w.sO = w.sD = nullptr;
+    w.sS = w.sVals = w.sValsAlt = nullptr;
+    w.sKeys = w.sKeysAlt = nullptr;
+    w.sTemp = nullptr;
+    w.sTempBytes = w.sCap = 0;
 }
 
-int ensure_sort_workspace(rt_ctx* c, size_t n) {
-    if (c->sCap >= n) return RT_OK;
-    free_sort_workspace(c);
-    HIPCHK(c, dalloc(&c->sO, n)); HIPCHK(c, dalloc(&c->sD, n)); HIPCHK(c, dalloc(&c->sS, n));
-    HIPCHK(c, dalloc(&c->sVals, n)); HIPCHK(c, dalloc(&c->sValsAlt, n));
-    HIPCHK(c, dalloc(&c->sKeys, n)); HIPCHK(c, dalloc(&c->sKeysAlt, n));
-    c->sTempBytes = sort_rays_temp_bytes((int)n);
-    HIPCHK(c, hipMalloc(&c->sTemp, std::max<size_t>(c->sTempBytes, 16)));
-    c->sCap = n;
+int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
+    if (w.sCap >= n) return RT_OK;
+    free_sort_workspace(w);
+    HIPCHK(c, dalloc(&w.sO, n)); HIPCHK(c, dalloc(&w.sD, n)); HIPCHK(c, dalloc(&w.sS, n));
+    HIPCHK(c, dalloc(&w.sVals, n)); HIPCHK(c, dalloc(&w.sValsAlt, n));
+    HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n));
+    w.sTempBytes = sort_rays_temp_bytes((int)n);
+    HIPCHK(c, hipMalloc(&w.sTemp, std::max<size_t>(w.sTempBytes, 16)));
+    w.sCap = n;
     return RT_OK;
 }
 
+// batch buffers only (the queue counters, stream and event of a lane live as long as the context)
+void free_workspace(Work& w) {
+    free_sort_workspace(w);
+    void* ptrs[] = {w.rayO, w.rayD, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.betaA, w.betaB,
+                    w.LA, w.LB, w.slot, w.hitPrim, w.dim, w.rng, w.prevPdf};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    w.rayO = w.rayD = w.lamA = w.lamB = w.pdfA = w.pdfB = w.hitB = nullptr;
+    w.betaA = w.betaB = w.LA = w.LB = nullptr;
+    w.slot = w.hitPrim = w.dim = nullptr;
+    w.rng = nullptr;
+    w.prevPdf = nullptr;
+    w.cap = 0;
+}
 void free_workspace(rt_ctx* c) {
-    free_sort_workspace(c);
-    void* ptrs[] = {c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->betaA, c->betaB,
-                    c->LA, c->LB, c->slot, c->hitPrim, c->dim, c->rng, c->prevPdf};
-    for (void* p : ptrs)
-        if (p) hipFree(p);
-    c->rayO = c->rayD = c->lamA = c->lamB = c->pdfA = c->pdfB = c->hitB = nullptr;
-    c->betaA = c->betaB = c->LA = c->LB = nullptr;
-    c->slot = c->hitPrim = c->dim = nullptr;
-    c->rng = nullptr;
-    c->prevPdf = nullptr;
-    c->cap = 0;
+    for (Work& w : c->ws) free_workspace(w);
 }
 
-int ensure_workspace(rt_ctx* c, size_t n, bool path) {
-    if (c->cap >= n && (!path || c->betaA)) return RT_OK;
-    free_workspace(c);
-    // path mode: queue arrays hold 2 ping-pong queues x 3 dominant-axis bins of n entries each
-    size_t nq = path ? 6 * n : n;
-    HIPCHK(c, dalloc(&c->rayO, nq)); HIPCHK(c, dalloc(&c->rayD, nq)); HIPCHK(c, dalloc(&c->slot, nq));
-    HIPCHK(c, dalloc(&c->lamA, n)); HIPCHK(c, dalloc(&c->lamB, n));
-    HIPCHK(c, dalloc(&c->pdfA, n)); HIPCHK(c, dalloc(&c->pdfB, n));
-    HIPCHK(c, dalloc(&c->hitB, n)); HIPCHK(c, dalloc(&c->hitPrim, n));
-    if (path) {
-        HIPCHK(c, dalloc(&c->betaA, n)); HIPCHK(c, dalloc(&c->betaB, n));
-        HIPCHK(c, dalloc(&c->LA, n)); HIPCHK(c, dalloc(&c->LB, n));
-        HIPCHK(c, dalloc(&c->dim, n)); HIPCHK(c, dalloc(&c->rng, n)); HIPCHK(c, dalloc(&c->prevPdf, n));
+int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
+    if (!w.d_qcount) HIPCHK(c, dalloc(&w.d_qcount, 2 * kQRegion));
+    if (&w != &c->ws[0]) {
+        if (!w.stream) HIPCHK(c, hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+        if (!w.film_done) HIPCHK(c, hipEventCreateWithFlags(&w.film_done, hipEventDisableTiming));
+    } else if (!w.film_done) {
+        HIPCHK(c, hipEventCreateWithFlags(&w.film_done, hipEventDisableTiming));
     }
-    c->cap = n;
+    if (w.cap >= n && (!path || w.betaA)) return RT_OK;
+    free_workspace(w);
+    // path mode: queue arrays hold 2 ping-pong queues x RT_NBINS bins of n entries each
+    size_t nq = path ? 2 * RT_NBINS * n : n;
+    HIPCHK(c, dalloc(&w.rayO, nq)); HIPCHK(c, dalloc(&w.rayD, nq)); HIPCHK(c, dalloc(&w.slot, nq));
+    HIPCHK(c, dalloc(&w.lamA, n)); HIPCHK(c, dalloc(&w.lamB, n));
+    HIPCHK(c, dalloc(&w.pdfA, n)); HIPCHK(c, dalloc(&w.pdfB, n));
+    HIPCHK(c, dalloc(&w.hitB, n)); HIPCHK(c, dalloc(&w.hitPrim, n));
+    if (path) {
+        HIPCHK(c, dalloc(&w.betaA, n)); HIPCHK(c, dalloc(&w.betaB, n));
+        HIPCHK(c, dalloc(&w.LA, n)); HIPCHK(c, dalloc(&w.LB, n));
+        HIPCHK(c, dalloc(&w.dim, n)); HIPCHK(c, dalloc(&w.rng, n)); HIPCHK(c, dalloc(&w.prevPdf, n));
+    }
+    w.cap = n;
     return RT_OK;
 }
+int ensure_workspace(rt_ctx* c, size_t n, bool path) { return ensure_workspace(c, c->ws[0], n, path); }
 
 hipEvent_t ev_get(rt_ctx* c) {
     if (!c->pool.empty()) {
@@ -845,103 +875,155 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     bool path = c->integ.kind == RT_INTEGRATOR_PATH || c->integ.kind == RT_INTEGRATOR_PATH_MIS;
     c->dsc.mis = c->integ.kind == RT_INTEGRATOR_PATH_MIS;
     c->dsc.full = c->scene_full || c->dsc.mis;
-    const size_t target = path ? (size_t)8 << 20 : (size_t)16 << 20;  // samples in flight per batch
+    const size_t target = c->batch_samples ? c->batch_samples : path ? (size_t)8 << 20 : (size_t)16 << 20;
     int B = (int)std::max<size_t>(1, target / (size_t)c->n_work);
     B = std::min(B, ie - ib);
     size_t nmax = (size_t)B * c->n_work;
-    if ((rc = ensure_workspace(c, nmax, path))) return rc;
-    const bool sort_rays = RT_SORT_RAYS && path && (c->dsc.qcap != 1 || RT_SORT_SINGLE_LEAF) && !RT_KZ_BINS_HOST;
-    if (sort_rays && (rc = ensure_sort_workspace(c, nmax))) return rc;
-    // Cornell-like single-leaf scenes cost the same per ray: static chunks on a resident grid beat tickets there
-    // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
-    const bool dyn = RT_DYN_SCHED == 1 || (RT_DYN_SCHED == 2 && c->dsc.qcap != 1);
     DevCamera cam = dev_camera(c->cam);
     DevFilm fd = dev_film(c);
-    for (int b0 = ib; b0 < ie; b0 += B) {
-        int nIdx = std::min(B, ie - b0);
-        int nS = nIdx * c->n_work;
-        SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
-        GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB,
-                  path ? c->rng : nullptr, c->dim, path && c->dsc.full ? c->prevPdf : nullptr, c->betaA, c->betaB, c->LA, c->LB};
-        const bool lean = RT_LEAN_GENERATE && path && !c->dsc.full;  // simple path kernel: no β / L / pdf streams
-        go.lean = lean ? 1 : 0;
-        hipEvent_t e0 = ev_start(c, st);
-        HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
-        ev_mark(c, st, ST_GEN, e0);
-        if (!path) {
-            TraceIO tio{c->rayO, c->rayD, nullptr, nS, 0, c->cull ? 1 : 0, c->hitB, c->hitPrim};
+    if (!path) {
+        Work& w = c->ws[0];
+        if ((rc = ensure_workspace(c, w, nmax, false))) return rc;
+        for (int b0 = ib; b0 < ie; b0 += B) {
+            int nIdx = std::min(B, ie - b0);
+            int nS = nIdx * c->n_work;
+            SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
+            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, nullptr, w.dim, nullptr,
+                      w.betaA, w.betaB, w.LA, w.LB};
+            go.lean = 0;
+            hipEvent_t e0 = ev_start(c, st);
+            HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
+            ev_mark(c, st, ST_GEN, e0);
+            TraceIO tio{w.rayO, w.rayD, nullptr, nS, 0, c->cull ? 1 : 0, w.hitB, w.hitPrim};
             e0 = ev_start(c, st);
             HIPCHK(c, launch_trace_closest(st, 0, c->dsc.qcap, c->dsc, tio, c->d_ctr));
             ev_mark(c, st, ST_TRACE, e0);
             ShadeRefIO sio = shade_ref_io(c);
             sio.work_pixels = c->d_work; sio.n_pixels = c->n_work; sio.n_index = nIdx;
-            sio.rayD = c->rayD; sio.lamA = c->lamA; sio.lamB = c->lamB; sio.pdfA = c->pdfA; sio.pdfB = c->pdfB;
-            sio.hitB = c->hitB; sio.hitPrim = c->hitPrim; sio.film = film;
+            sio.rayD = w.rayD; sio.lamA = w.lamA; sio.lamB = w.lamB; sio.pdfA = w.pdfA; sio.pdfB = w.pdfB;
+            sio.hitB = w.hitB; sio.hitPrim = w.hitPrim; sio.film = film;
             e0 = ev_start(c, st);
             HIPCHK(c, launch_ref_shade_film(st, 0, c->dsc, c->d_spec, fd, sio, c->d_ctr));
             ev_mark(c, st, ST_FILM, e0);
-        } else {
-            // camera rays fill bin 0 of queue 0 (flat order); bins 1, 2 start empty
-            int cur = 0;
-            HIPCHK(c, hipMemsetAsync(c->d_qcount, 0, 2 * kQRegion * sizeof(int), st));
-            HIPCHK(c, hipMemcpyAsync(c->d_qcount, &nS, sizeof(int), hipMemcpyHostToDevice, st));
-            for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
-                // the last trace can only add emitter hits, which count only after specular bounces or with MIS
-                if (depth == c->integ.max_depth && depth > 0 && !c->dsc.full) break;
-                int nxt = cur ^ 1;
-                const size_t qs = 3 * nmax;  // one queue = 3 bins of nmax
-                const float4* cO = c->rayO + (size_t)cur * qs;
-                const float4* cD = c->rayD + (size_t)cur * qs;
-                const int* cS = c->slot + (size_t)cur * qs;
-                int* qc_cur = c->d_qcount + kQRegion * cur;
-                int* qc_nxt = c->d_qcount + kQRegion * nxt;
+        }
+        return RT_OK;
+    }
+
+    // ---- path mode: up to c->lanes batches in flight, batch k on lane k mod lanes (lane 0 = the caller's stream).
+    // Within a lane everything is stream-ordered; across lanes only the film kernels are chained (batch k's film
+    // after batch k-1's), so every pixel still adds its sample indices in increasing order.
+    const int nbatch = (ie - ib + B - 1) / B;
+    const int lanes = std::max(1, std::min(std::min(c->lanes, kLanes), nbatch));
+    const bool sort_rays = RT_SORT_RAYS && (c->dsc.qcap != 1 || RT_SORT_SINGLE_LEAF) && !RT_KZ_BINS_HOST;
+    for (int l = 0; l < lanes; ++l) {
+        if ((rc = ensure_workspace(c, c->ws[l], nmax, true))) return rc;
+        if (sort_rays && (rc = ensure_sort_workspace(c, c->ws[l], nmax))) return rc;
+    }
+    // Cornell-like single-leaf scenes cost the same per ray: static chunks on a resident grid beat tickets there
+    // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
+    const bool dyn = RT_DYN_SCHED == 1 || (RT_DYN_SCHED == 2 && c->dsc.qcap != 1);
+    const bool lean = RT_LEAN_GENERATE && !c->dsc.full;  // simple path kernel: no β / L / pdf streams
+    const bool fused = RT_FUSED_BOUNCE && !c->dsc.full;  // simple scenes: trace inside the shade kernel
+    // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
+    // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
+    // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
+    const int grid = lanes > 1 ? std::max(8, c->grid / std::max(1, c->grid_div)) : c->grid;
+    auto lstream = [&](int l) { return l == 0 ? st : c->ws[l].stream; };
+    if (lanes > 1) {  // lanes 1.. start after the caller's earlier work on st
+        HIPCHK(c, hipEventRecord(c->ws[0].film_done, st));
+        for (int l = 1; l < lanes; ++l) HIPCHK(c, hipStreamWaitEvent(c->ws[l].stream, c->ws[0].film_done, 0));
+    }
+    const size_t qs = RT_NBINS * nmax;  // one queue = RT_NBINS bins of nmax
+    int last_film = -1;                 // lane of the most recent film launch
+    for (int g0 = ib; g0 < ie; g0 += B * lanes) {
+        int nIdx[kLanes] = {0}, cur[kLanes] = {0};
+        for (int l = 0; l < lanes; ++l) {
+            int b0 = g0 + l * B;
+            if (b0 >= ie) break;
+            Work& w = c->ws[l];
+            hipStream_t s = lstream(l);
+            nIdx[l] = std::min(B, ie - b0);
+            int nS = nIdx[l] * c->n_work;
+            SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
+            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, w.rng, w.dim,
+                      c->dsc.full ? w.prevPdf : nullptr, w.betaA, w.betaB, w.LA, w.LB};
+            go.lean = lean ? 1 : 0;
+            hipEvent_t e0 = ev_start(c, s);
+            HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
+            ev_mark(c, s, ST_GEN, e0);
+            // camera rays fill bin 0 of queue 0 (flat order); the other bins start empty
+            HIPCHK(c, hipMemsetAsync(w.d_qcount, 0, 2 * kQRegion * sizeof(int), s));
+            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)w.d_qcount, nS, 1, s));
+        }
+        for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
+            // the last trace can only add emitter hits, which count only after specular bounces or with MIS
+            if (depth == c->integ.max_depth && depth > 0 && !c->dsc.full) break;
+            for (int l = 0; l < lanes && nIdx[l] > 0; ++l) {
+                Work& w = c->ws[l];
+                hipStream_t s = lstream(l);
+                SampleIds ids{c->d_work, c->n_work, g0 + l * B, nullptr, nullptr};
+                int nxt = cur[l] ^ 1;
+                const float4* cO = w.rayO + (size_t)cur[l] * qs;
+                const float4* cD = w.rayD + (size_t)cur[l] * qs;
+                const int* cS = w.slot + (size_t)cur[l] * qs;
+                int* qc_cur = w.d_qcount + kQRegion * cur[l];
+                int* qc_nxt = w.d_qcount + kQRegion * nxt;
                 // the next queue's bin lengths and the chunk tickets its trace and shade launches will use
-                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, kQRegion * sizeof(int), st));
+                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, kQRegion * sizeof(int), s));
+                hipEvent_t e0;
                 // multi-level octrees: bounce rays regrouped by (octant, origin Morton code) before the trace
                 if (sort_rays && depth > 0) {
                     int nq = 0;
-                    HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, st));
-                    HIPCHK(c, hipStreamSynchronize(st));
-                    SortRaysIO so{cO, cD, cS, c->sO, c->sD, c->sS, c->sKeys, c->sKeysAlt, c->sVals, c->sValsAlt,
-                                  c->sTemp, c->sTempBytes, c->sort_lo, c->sort_scale};
-                    e0 = ev_start(c, st);
-                    HIPCHK(c, launch_sort_rays(st, nq, so));
-                    ev_mark(c, st, ST_TRACE, e0);
-                    cO = c->sO; cD = c->sD; cS = c->sS;
+                    HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, s));
+                    HIPCHK(c, hipStreamSynchronize(s));
+                    SortRaysIO so{cO, cD, cS, w.sO, w.sD, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt,
+                                  w.sTemp, w.sTempBytes, c->sort_lo, c->sort_scale};
+                    e0 = ev_start(c, s);
+                    HIPCHK(c, launch_sort_rays(s, nq, so));
+                    ev_mark(c, s, ST_TRACE, e0);
+                    cO = w.sO; cD = w.sD; cS = w.sS;
                 }
-                const bool fused = RT_FUSED_BOUNCE && !c->dsc.full;  // simple scenes: trace inside the shade kernel
                 if (!fused) {
-                    TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, c->hitB, c->hitPrim,
-                                 dyn ? qc_cur + 3 * kQStride : nullptr};
-                    e0 = ev_start(c, st);
-                    HIPCHK(c, launch_trace_closest(st, c->grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
-                    ev_mark(c, st, ST_TRACE, e0);
+                    TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, w.hitB, w.hitPrim,
+                                dyn ? qc_cur + RT_NBINS * kQStride : nullptr};
+                    e0 = ev_start(c, s);
+                    HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
+                    ev_mark(c, s, ST_TRACE, e0);
                 }
                 PathIO pio{};
                 pio.fused = fused ? 1 : 0;
                 pio.lean = lean ? 1 : 0;
                 pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = qc_cur;
-                pio.hitB = c->hitB; pio.hitPrim = c->hitPrim;
-                pio.nO = c->rayO + (size_t)nxt * qs; pio.nD = c->rayD + (size_t)nxt * qs;
-                pio.nSlot = c->slot + (size_t)nxt * qs; pio.nCount = qc_nxt; pio.bstride = nmax;
-                pio.rng = c->rng; pio.dim = c->dim; pio.betaA = c->betaA; pio.betaB = c->betaB;
-                pio.LA = c->LA; pio.LB = c->LB;
-                pio.lamA = c->lamA; pio.lamB = c->lamB; pio.pdfA = c->pdfA; pio.pdfB = c->pdfB;
-                pio.prevPdf = c->prevPdf;
+                pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
+                pio.nO = w.rayO + (size_t)nxt * qs; pio.nD = w.rayD + (size_t)nxt * qs;
+                pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt; pio.bstride = nmax;
+                pio.rng = w.rng; pio.dim = w.dim; pio.betaA = w.betaA; pio.betaB = w.betaB;
+                pio.LA = w.LA; pio.LB = w.LB;
+                pio.lamA = w.lamA; pio.lamB = w.lamB; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
+                pio.prevPdf = w.prevPdf;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
-                pio.ticket = dyn ? qc_cur + 4 * kQStride : nullptr;
-                e0 = ev_start(c, st);
-                HIPCHK(c, launch_path_shade(st, c->grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
-                ev_mark(c, st, ST_SHADE, e0);
-                cur = nxt;
+                pio.ticket = dyn ? qc_cur + (RT_NBINS + 1) * kQStride : nullptr;
+                e0 = ev_start(c, s);
+                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
+                ev_mark(c, s, ST_SHADE, e0);
+                cur[l] = nxt;
             }
-            PathFilmIO fio{c->d_work, c->n_work, nIdx, c->LA, c->LB, c->lamA, c->lamB, c->pdfA, c->pdfB, film};
+        }
+        for (int l = 0; l < lanes && nIdx[l] > 0; ++l) {
+            Work& w = c->ws[l];
+            hipStream_t s = lstream(l);
+            if (last_film >= 0 && last_film != l) HIPCHK(c, hipStreamWaitEvent(s, c->ws[last_film].film_done, 0));
+            PathFilmIO fio{c->d_work, c->n_work, nIdx[l], w.LA, w.LB, w.lamA, w.lamB, w.pdfA, w.pdfB, film};
             fio.lean = lean ? 1 : 0;
-            e0 = ev_start(c, st);
-            HIPCHK(c, launch_path_film(st, 0, c->d_spec, fd, fio, c->d_ctr));
-            ev_mark(c, st, ST_FILM, e0);
+            hipEvent_t e0 = ev_start(c, s);
+            HIPCHK(c, launch_path_film(s, 0, c->d_spec, fd, fio, c->d_ctr));
+            ev_mark(c, s, ST_FILM, e0);
+            HIPCHK(c, hipEventRecord(w.film_done, s));
+            last_film = l;
         }
     }
+    // the caller's stream resumes after every lane's last film
+    for (int l = 1; l < lanes; ++l) HIPCHK(c, hipStreamWaitEvent(st, c->ws[l].film_done, 0));
     return RT_OK;
 }
 
@@ -1105,8 +1187,11 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
         return RT_E_HIP;
     }
     c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
+    if (const char* e = std::getenv("RTMI_LANES")) c->lanes = std::max(1, std::min(kLanes, std::atoi(e)));
+    if (const char* e = std::getenv("RTMI_GRID_DIV")) c->grid_div = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
     c->hs.init();
-    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->d_qcount, 2 * kQRegion) != hipSuccess ||
+    if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->ws[0].d_qcount, 2 * kQRegion) != hipSuccess ||
         dalloc(&c->d_ctr, (size_t)C_NCOUNTERS) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
         rt_destroy(c);
         return RT_E_OOM;
@@ -1139,11 +1224,18 @@ void rt_destroy(rt_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    for (Work& w : c->ws)
+        if (w.stream) hipStreamSynchronize(w.stream);
     harvest(c);
     for (hipEvent_t e : c->pool) hipEventDestroy(e);
     free_scene(c);
     free_workspace(c);
-    void* ptrs[] = {c->d_spec, c->d_qcount, c->d_ctr, c->d_resolve, c->d_work, c->d_film, c->d_cdf, c->d_sobol_mats,
+    for (Work& w : c->ws) {
+        if (w.d_qcount) hipFree(w.d_qcount);
+        if (w.film_done) hipEventDestroy(w.film_done);
+        if (w.stream) hipStreamDestroy(w.stream);
+    }
+    void* ptrs[] = {c->d_spec, c->d_ctr, c->d_resolve, c->d_work, c->d_film, c->d_cdf, c->d_sobol_mats,
                     c->d_sobol_fwd};
     for (void* p : ptrs)
         if (p) hipFree(p);
@@ -1796,14 +1888,14 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
         hipMemcpy(dp, pixel_ids, 4 * (size_t)n, hipMemcpyHostToDevice);
         hipMemcpy(di, indices, 4 * (size_t)n, hipMemcpyHostToDevice);
         SampleIds ids{nullptr, 1, 0, dp, di};
-        GenOut go{c->rayO, c->rayD, c->slot, c->lamA, c->lamB, c->pdfA, c->pdfB, nullptr, nullptr, nullptr,
+        GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].slot, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA, c->ws[0].pdfB, nullptr, nullptr, nullptr,
                   nullptr, nullptr, nullptr, nullptr};
         DevFilm fd = dev_film(c);
-        TraceIO tio{c->rayO, c->rayD, nullptr, n, 0, c->cull ? 1 : 0, c->hitB, c->hitPrim};
+        TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, nullptr, n, 0, c->cull ? 1 : 0, c->ws[0].hitB, c->ws[0].hitPrim};
         ShadeRefIO sio = shade_ref_io(c);
-        sio.rayD = c->rayD; sio.lamA = c->lamA; sio.lamB = c->lamB; sio.pdfA = c->pdfA; sio.pdfB = c->pdfB;
-        sio.hitB = c->hitB; sio.hitPrim = c->hitPrim;
-        RecordIO rio{n, c->rayO, c->rayD, c->lamA, c->lamB, c->pdfA, c->pdfB, c->hitB, c->hitPrim, dout, 39};
+        sio.rayD = c->ws[0].rayD; sio.lamA = c->ws[0].lamA; sio.lamB = c->ws[0].lamB; sio.pdfA = c->ws[0].pdfA; sio.pdfB = c->ws[0].pdfB;
+        sio.hitB = c->ws[0].hitB; sio.hitPrim = c->ws[0].hitPrim;
+        RecordIO rio{n, c->ws[0].rayO, c->ws[0].rayD, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA, c->ws[0].pdfB, c->ws[0].hitB, c->ws[0].hitPrim, dout, 39};
         if (launch_generate(c->stream, 0, n, ids, dev_camera(c->cam), smp, fd, go) != hipSuccess ||
             launch_trace_closest(c->stream, 0, c->dsc.qcap, c->dsc, tio, c->d_ctr) != hipSuccess ||
             launch_records(c->stream, c->dsc, c->d_spec, fd, sio, rio) != hipSuccess ||

@@ -138,7 +138,10 @@ struct GenOut {
 // kz, Shapes.h:1145): bin b holds rays at ray[b*bstride + i], i < count[b*cstride].  Entries are addressed by
 // a flat index k over bin 0, then 1, then 2, so every wave but the two at bin seams sees one kz.
 static const int kQStride = 64;
-static const int kQRegion = 5 * kQStride;  // one queue's counters: 3 bin lengths + 2 chunk tickets
+#ifndef RT_NBINS
+#define RT_NBINS 3  // bins of a path-mode ray queue (RT_BIN_MODE in rt_kernels.hip decides a ray's bin)
+#endif
+static const int kQRegion = (RT_NBINS + 2) * kQStride;  // one queue's counters: bin lengths + 2 chunk tickets
 static const int kBlockThreads = 256;  // threads per block of every kernel
 #ifndef RT_CLUSTER_TRIS
 #define RT_CLUSTER_TRIS 2

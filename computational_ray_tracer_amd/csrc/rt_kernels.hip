@@ -51,6 +51,9 @@ __shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by eve
 #ifndef RT_KZ_BINS
 #define RT_KZ_BINS 0         // 1: path-mode ray queues split into dominant-axis bins (Cornell A/B: trace -7%, shade +23%)
 #endif
+#ifndef RT_BIN_MODE
+#define RT_BIN_MODE (RT_KZ_BINS ? 1 : 0)  // next-queue bin of a bounce ray: 0 one bin, 1 dominant axis,
+#endif                                    // 2 origin triangle pair (prim >> 1, mod RT_NBINS)
 #ifndef RT_KZ_SPECIALIZE
 #define RT_KZ_SPECIALIZE 1   // compile-time watertight permutation for dominant-axis-uniform waves
 #endif
@@ -92,28 +95,28 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     return pred ? base + rank : -1;
 }
 
-// Block-aggregated append into a 3-bin queue (bin = the ray's dominant axis, -1 = nothing to append):
-// one atomicAdd per bin per block.  Returns the element position (bin region + index) or -1.
+// Block-aggregated append into an RT_NBINS-bin queue (bin -1 = nothing to append): one atomicAdd per non-empty bin
+// per block.  Returns the element position (bin region + index) or -1.
 __device__ __forceinline__ long block_append_bin(int* counters, int bin, size_t bstride, int* lds) {
     constexpr int NW = kBlock / 64;
     int wave = threadIdx.x >> 6;
     int rank = 0;
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
+    for (int b = 0; b < RT_NBINS; ++b) {
         uint64_t mask = __ballot(bin == b);
         if (bin == b)
             rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
         if (lane_id() == 0) lds[b * NW + wave] = __popcll(mask);
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
-        int b = threadIdx.x, tot = 0;
+    for (int b = threadIdx.x; b < RT_NBINS; b += kBlock) {
+        int tot = 0;
         for (int w = 0; w < NW; ++w) { int cw = lds[b * NW + w]; lds[b * NW + w] = tot; tot += cw; }
-        lds[3 * NW + b] = tot ? atomicAdd(counters + b * kQStride, tot) : 0;
+        lds[RT_NBINS * NW + b] = tot ? atomicAdd(counters + b * kQStride, tot) : 0;
     }
     __syncthreads();
     long pos = -1;
-    if (bin >= 0) pos = (long)bin * (long)bstride + lds[3 * NW + bin] + lds[bin * NW + wave] + rank;
+    if (bin >= 0) pos = (long)bin * (long)bstride + lds[RT_NBINS * NW + bin] + lds[bin * NW + wave] + rank;
     __syncthreads();
     return pos;
 }
@@ -172,12 +175,30 @@ __device__ __forceinline__ int major_dir(V3 d) {
     float c = k == 0 ? d.x : (k == 1 ? d.y : d.z);
     return 2 * k + (c < 0 ? 1 : 0);
 }
-// flat queue index -> element position (bins 0, 1, 2 of lengths c0, c1, rest)
-__device__ __forceinline__ size_t queue_pos(int k, int c0, int c1, size_t bstride) {
-    if (k < c0) return (size_t)k;
-    if (k < c0 + c1) return bstride + (size_t)(k - c0);
-    return 2 * bstride + (size_t)(k - c0 - c1);
-}
+// Lengths of the RT_NBINS bins of a queue (device counters, kQStride apart) and flat index -> element position
+// (bin b occupies [b * bstride, b * bstride + c[b])).
+struct QueueCounts {
+    int c[RT_NBINS];
+    int n;
+    __device__ __forceinline__ QueueCounts(const int* count, int fixed_n) {
+#pragma unroll
+        for (int b = 0; b < RT_NBINS; ++b) c[b] = count ? count[b * kQStride] : (b == 0 ? fixed_n : 0);
+        n = 0;
+#pragma unroll
+        for (int b = 0; b < RT_NBINS; ++b) n += c[b];
+    }
+    __device__ __forceinline__ size_t pos(int k, size_t bstride) const {
+        size_t off = 0;
+#pragma unroll
+        for (int b = 0; b < RT_NBINS - 1; ++b) {
+            bool later = k >= c[b];
+            k = later ? k - c[b] : k;
+            off = later ? off + bstride : off;
+            if (!later) return off + (size_t)k;
+        }
+        return off + (size_t)k;
+    }
+};
 
 // Work distribution of the persistent queue kernels.  With a ticket counter (zeroed before the launch) a block takes
 // the next chunk of RT_DYN_ITEMS x kBlock items whenever it finishes one, so blocks whose rays are expensive
@@ -245,12 +266,18 @@ __device__ __forceinline__ long queue_append(int* counters, int bin, size_t bstr
     } else {
         long pos = -1;
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
+        for (int b = 0; b < RT_NBINS; ++b) {
             int p = wave_append(counters + b * kQStride, bin == b);
             if (bin == b) pos = (long)b * (long)bstride + p;
         }
         return pos;
     }
+}
+
+__device__ __forceinline__ int ray_bin(int prim, V3 wi) {
+    if constexpr (RT_BIN_MODE == 1) return dominant_axis(wi);
+    else if constexpr (RT_BIN_MODE == 2) return (prim >> 1) % RT_NBINS;
+    else return 0;
 }
 
 // the PCG increment of a path never changes after generation: only the 8-byte state half is written back
@@ -677,9 +704,8 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
-    int c0 = io.n, c1 = 0, c2 = 0;
-    if (io.count) { c0 = io.count[0]; c1 = io.count[kQStride]; c2 = io.count[2 * kQStride]; }
-    int n = c0 + c1 + c2;
+    const QueueCounts qc(io.count, io.n);
+    const int n = qc.n;
     unsigned long long nn = 0, nt = 0, nh = 0, nr = 0;
 #if RT_TRACE_KZSORT
     // The block's rays are regrouped by dominant axis through LDS before traversal, so most waves take the
@@ -692,7 +718,7 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
             float4 oo = make_float4(0, 0, 0, 0), dd = oo;
             int key = 3;
             if (kk < n) {
-                size_t q = queue_pos(kk, c0, c1, io.bstride);
+                size_t q = qc.pos(kk, io.bstride);
                 oo = io.rayO[q]; dd = io.rayD[q];
                 key = dominant_axis(v3(dd.x, dd.y, dd.z));
             }
@@ -709,7 +735,7 @@ __global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO i
     WaveChunks chunks(io.ticket);
     for (int cb = chunks.next(); cb < n; cb = chunks.next())
     for (int k = cb + chunks.lane; k < cb + chunks.size && k < n; k += chunks.step) {
-        size_t q = queue_pos(k, c0, c1, io.bstride);
+        size_t q = qc.pos(k, io.bstride);
         float4 o4 = io.rayO[q], d4 = io.rayD[q];
 #endif
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
@@ -832,9 +858,9 @@ template <int QCAP, bool FUSED>
 __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
                                                        SampleIds ids, PathIO io, unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
-    __shared__ int lds[6 * (kBlock / 64) + 8];
-    int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
-    int n = c0 + c1 + c2;
+    __shared__ int lds[(RT_NBINS + 6) * (kBlock / 64) + RT_NBINS + 8];
+    const QueueCounts qc(io.count, 0);
+    const int n = qc.n;
     unsigned long long snn = 0, snt = 0, nsh = 0, tnn = 0, tnt = 0, tnh = 0, tnr = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
@@ -854,7 +880,7 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
         int slot = -1;
         size_t q = 0;
         if (k < n) {
-            q = queue_pos(k, c0, c1, io.bstride);
+            q = qc.pos(k, io.bstride);
             slot = io.slot[q];
             int prim;
             float4 d4, hb;
@@ -956,7 +982,7 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
                         for (int i = 0; i < 8; ++i) beta[i] *= R[i];
                         store8(io.betaA, io.betaB, slot, beta);
                         wantNext = true;
-                        nbin = RT_KZ_BINS ? dominant_axis(wi) : 0;
+                        nbin = ray_bin(prim, wi);
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
                     }
@@ -1059,9 +1085,9 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
                                                             DevFilm film, SampleIds ids, PathIO io,
                                                             unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
-    __shared__ int lds[6 * (kBlock / 64) + 8];
-    int c0 = io.count[0], c1 = io.count[kQStride], c2 = io.count[2 * kQStride];
-    int n = c0 + c1 + c2;
+    __shared__ int lds[(RT_NBINS + 6) * (kBlock / 64) + RT_NBINS + 8];
+    const QueueCounts qc(io.count, 0);
+    const int n = qc.n;
     unsigned long long snn = 0, snt = 0, nsh = 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = RT_SHADE_WAVE && QCAP != 1;
@@ -1074,7 +1100,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int nbin = -1, slot = -1;
         if (k < n) {
-            size_t q = queue_pos(k, c0, c1, io.bstride);
+            size_t q = qc.pos(k, io.bstride);
             slot = io.slot[q];
             int prim = io.hitPrim[k];
             if (prim >= 0) {
@@ -1150,7 +1176,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
                         wantNext = true;
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                        nbin = RT_KZ_BINS ? dominant_axis(wi) : 0;
+                        nbin = ray_bin(prim, wi);
                         io.prevPdf[slot] = 0.f;
                     } else {
                         Smp sm;
@@ -1189,7 +1215,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
                             wantNext = true;
                             nO = make_float4(po.x, po.y, po.z, 0.f);
                             nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                            nbin = RT_KZ_BINS ? dominant_axis(wi) : 0;
+                            nbin = ray_bin(prim, wi);
                             io.prevPdf[slot] = 0.f;
                         } else {  // Lambert: NEE per light, then a cosine-hemisphere bounce
                             V3 po = vadd(p, vmul(nrm, off));
@@ -1273,7 +1299,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const D
                                 wantNext = true;
                                 nO = make_float4(po.x, po.y, po.z, 0.f);
                                 nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                                nbin = RT_KZ_BINS ? dominant_axis(wi) : 0;
+                                nbin = ray_bin(prim, wi);
                                 io.prevPdf[slot] = z * InvPi;
                             }
                         }

@@ -125,6 +125,26 @@ def test_cornell_path_film_bitexact(oracle_lib):
     assert bad.sum() == 0, f"{bad.sum()} pixels differ; max |diff| {np.abs(fg - fo).max()}"
 
 
+@pytest.mark.parametrize("lanes,scene_kind", [(2, "cornell"), (1, "cornell"), (2, "mesh")])
+def test_concurrent_batches_film_bitexact(oracle_lib, monkeypatch, lanes, scene_kind):
+    """Several batches per pass (RTMI_BATCH_SAMPLES) alternating between the two lane streams, including an odd
+    batch count and a ragged last batch: the film chain must keep every pixel's index order (tolerance 0)."""
+    monkeypatch.setenv("RTMI_BATCH_SAMPLES", str(48 * 40 * 2))   # 2 indices per batch
+    monkeypatch.setenv("RTMI_LANES", str(lanes))
+    if scene_kind == "cornell":
+        cfg = scene.cfg_cornell(res=(48, 40), spp_side=3)
+    else:
+        cfg = scene.cfg3_blob(res=(48, 40), spp_side=3, max_depth=3, frequency=20)
+    g = Renderer(cfg)
+    fg = g.render_pass(0, 7)                                      # batches {0,1} {2,3} {4,5} {6}
+    f2 = g.new_film()
+    g.render_pass(0, 3, f2)                                       # a pass boundary inside a lane group
+    g.render_pass(3, 7, f2)
+    fo = oracle_lib.OracleScene(cfg).render(0, 7)
+    assert np.array_equal(bits(fg), bits(fo))
+    assert np.array_equal(bits(f2), bits(fo))
+
+
 def test_shards_sum_to_full_film(oracle_lib):
     from computational_ray_tracer_amd.distributed import shard_pixels
     cfg = scene.cfg_cornell(res=(80, 48), spp_side=2)
