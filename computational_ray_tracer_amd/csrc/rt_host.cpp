@@ -449,6 +449,7 @@ struct Work {
     size_t sTempBytes = 0, sCap = 0;
     hipStream_t stream = nullptr;  // lanes >= 1: own stream (lane 0 runs on the caller's stream)
     hipEvent_t film_done = nullptr;
+    hipEvent_t trace_done = nullptr;  // RTMI_PAIR: the lanes' closest-hit launches take turns
 };
 
 struct rt_ctx {
@@ -486,6 +487,7 @@ struct rt_ctx {
     Work ws[kLanes];
     int lanes = RT_LANES;  // batches in flight in path mode (RTMI_LANES overrides)
     int grid_div = 1;      // persistent-grid divisor with lanes > 1 (RTMI_GRID_DIV overrides; A/B: 1 beats 2)
+    int pair = 0;          // RTMI_PAIR=1: closest-hit launches of the lanes never overlap (trace pairs with shade)
     size_t batch_samples = 0;  // samples in flight per batch (0: 8 Mi path / 16 Mi reference; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
@@ -578,6 +580,7 @@ int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
     } else if (!w.film_done) {
         HIPCHK(c, hipEventCreateWithFlags(&w.film_done, hipEventDisableTiming));
     }
+    if (!w.trace_done) HIPCHK(c, hipEventCreateWithFlags(&w.trace_done, hipEventDisableTiming));
     if (w.cap >= n && (!path || w.betaA)) return RT_OK;
     free_workspace(w);
     // path mode: queue arrays hold 2 ping-pong queues x RT_NBINS bins of n entries each
@@ -935,6 +938,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     }
     const size_t qs = RT_NBINS * nmax;  // one queue = RT_NBINS bins of nmax
     int last_film = -1;                 // lane of the most recent film launch
+    int last_trace = -1;                // lane of the most recent closest-hit launch (RTMI_PAIR)
     for (int g0 = ib; g0 < ie; g0 += B * lanes) {
         int nIdx[kLanes] = {0}, cur[kLanes] = {0};
         for (int l = 0; l < lanes; ++l) {
@@ -986,9 +990,12 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 if (!fused) {
                     TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, w.hitB, w.hitPrim,
                                 dyn ? qc_cur + RT_NBINS * kQStride : nullptr};
+                    if (c->pair && last_trace >= 0 && last_trace != l)
+                        HIPCHK(c, hipStreamWaitEvent(s, c->ws[last_trace].trace_done, 0));
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
                     ev_mark(c, s, ST_TRACE, e0);
+                    if (c->pair) { HIPCHK(c, hipEventRecord(w.trace_done, s)); last_trace = l; }
                 }
                 PathIO pio{};
                 pio.fused = fused ? 1 : 0;
@@ -1189,6 +1196,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
     if (const char* e = std::getenv("RTMI_LANES")) c->lanes = std::max(1, std::min(kLanes, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_GRID_DIV")) c->grid_div = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("RTMI_PAIR")) c->pair = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
     c->hs.init();
     if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->ws[0].d_qcount, 2 * kQRegion) != hipSuccess ||
@@ -1233,6 +1241,7 @@ void rt_destroy(rt_ctx* c) {
     for (Work& w : c->ws) {
         if (w.d_qcount) hipFree(w.d_qcount);
         if (w.film_done) hipEventDestroy(w.film_done);
+        if (w.trace_done) hipEventDestroy(w.trace_done);
         if (w.stream) hipStreamDestroy(w.stream);
     }
     void* ptrs[] = {c->d_spec, c->d_ctr, c->d_resolve, c->d_work, c->d_film, c->d_cdf, c->d_sobol_mats,

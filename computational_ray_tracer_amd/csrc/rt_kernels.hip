@@ -702,8 +702,16 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
     return traverse<QCAP, ANYHIT, -1>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
 }
 
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 0     // >0: amdgpu_waves_per_eu floor for the closest-hit kernel (register budget)
+#endif
+#if RT_TRACE_WAVES > 0
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
+#else
+#define RT_TRACE_ATTR
+#endif
 template <int QCAP>
-__global__ void __launch_bounds__(kBlock) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
+__global__ void __launch_bounds__(kBlock) RT_TRACE_ATTR k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
     const QueueCounts qc(io.count, io.n);
     const int n = qc.n;
     unsigned long long nn = 0, nt = 0, nh = 0, nr = 0;
