@@ -3,8 +3,8 @@
 Cornell box, 1920x1080, 256 spp (16x16 stratified, jittered), diffuse + NEE, max depth 5.
 
 One *step* = every GPU renders its pixel tiles (32x32 tiles, tile t -> rank t % N) for `spp_per_step * N`
-sample indices, accumulating into its device-resident film; the N films are then reduced to rank 0 with
-one RCCL reduce over xGMI.  Per-GPU work per step is fixed (weak scaling): W*H*spp_per_step samples.
+sample indices, accumulating into its device-resident film; when a step completes the frame (256 indices) the
+N films are reduced to rank 0 with one RCCL reduce over xGMI and the accumulation restarts.  Per-GPU work per step is fixed (weak scaling): W*H*spp_per_step samples.
 
 Prints ONE JSON line on rank 0 (contract in the task statement): metric/value/unit, roofline of the dominant
 kernel (by HIP-event time; algorithmic bytes per SURVEY.md §8(d) / its average launch time),
@@ -25,7 +25,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 from computational_ray_tracer_amd import scene  # noqa: E402
-from computational_ray_tracer_amd.distributed import reduce_film  # noqa: E402
+from computational_ray_tracer_amd.distributed import FrameLoop  # noqa: E402
 from computational_ray_tracer_amd.renderer import Renderer  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -162,17 +162,11 @@ def main():
     r.set_shard(32, world, rank)
     film = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream()
-    per_step = a.spp_per_step * world
-    cursor = [0]
+    # progressive frames: `spp_per_step * world` indices per step, one RCCL reduce per completed frame
+    loop = FrameLoop(spp, a.spp_per_step * world, film, dst=0)
 
     def step():
-        i0 = cursor[0]
-        i1 = min(spp, i0 + per_step)
-        r.render_pass_device(i0, i1, film.data_ptr(), stream.cuda_stream)
-        cursor[0] = 0 if i1 >= spp else i1
-        if world > 1:
-            reduce_film(film, dst=0)  # RCCL over xGMI (each pixel owned by one rank: exact sum)
-        return (i1 - i0)
+        return loop.step(lambda i0, i1, f: r.render_pass_device(i0, i1, f.data_ptr(), stream.cuda_stream))
 
     for _ in range(a.warmup):
         step()

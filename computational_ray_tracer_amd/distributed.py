@@ -29,6 +29,39 @@ def shard_pixels(res, tile, n_shards, shard_id):
     return np.concatenate(out).astype(np.int32) if out else np.zeros(0, np.int32)
 
 
+class FrameLoop:
+    """Progressive rendering of whole frames in steps of `per_step` sample indices (RayTracerTestApp.h:347-452
+    renders one index per pass over all pixels and resolves the film after each pass).
+
+    Each rank accumulates its own pixels into `film` (device-resident).  When a step completes the frame
+    (index `spp` reached) the per-rank films are reduced onto `dst` ONCE — the frame's only collective — the
+    completed frame is kept in `frame` on `dst`, and `film` is zeroed so the next frame starts from nothing.
+    Reducing only at frame end keeps the collective off the per-step path and never re-adds a rank's
+    earlier contributions (an in-place reduce per step would count the root's already-reduced pixels again).
+    """
+
+    def __init__(self, spp, per_step, film, dst=0):
+        self.spp, self.per_step, self.film, self.dst = int(spp), int(per_step), film, dst
+        self.cursor = 0
+        self.frame = None      # last completed (reduced) frame, on dst
+        self.frames_done = 0
+
+    def step(self, render):
+        """render(i0, i1, film) accumulates indices [i0, i1) of this rank's pixels; returns i1 - i0."""
+        i0 = self.cursor
+        i1 = min(self.spp, i0 + self.per_step)
+        render(i0, i1, self.film)
+        if i1 >= self.spp:
+            reduce_film(self.film, dst=self.dst)
+            self.frame = self.film.clone()
+            self.film.zero_()
+            self.frames_done += 1
+            self.cursor = 0
+        else:
+            self.cursor = i1
+        return i1 - i0
+
+
 def reduce_film(film, dst=0):
     """Sum the per-rank films onto `dst` (torch.distributed; backend nccl = RCCL on ROCm, or gloo)."""
     import torch.distributed as dist
