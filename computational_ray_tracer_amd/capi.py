@@ -25,7 +25,8 @@ RT_SENSOR_XYZ, RT_SENSOR_CANON_EOS_100D, RT_SENSOR_COUNT = 0, 1, 18
 RT_OCTREE_BUILD_DEVICE, RT_OCTREE_BUILD_HOST = 0, 1
 RT_ILLUM_D65, RT_ILLUM_A, RT_ILLUM_D50, RT_ILLUM_F1, RT_ILLUM_ACES_D60, RT_ILLUM_COUNT = 0, 1, 2, 3, 15, 16
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
+RT_MAX_DEVICES = 16
 
 F16 = C.c_float * 16
 F9 = C.c_float * 9
@@ -35,7 +36,8 @@ F8 = C.c_float * 8
 
 
 class rt_options(C.Structure):
-    _fields_ = [("device", C.c_int), ("octree_build", C.c_int), ("reserved", C.c_int * 6)]
+    _fields_ = [("device", C.c_int), ("octree_build", C.c_int), ("n_devices", C.c_int),
+                ("devices", C.c_int * RT_MAX_DEVICES), ("reserved", C.c_int * 5)]
 
 
 class rt_pixel(C.Structure):

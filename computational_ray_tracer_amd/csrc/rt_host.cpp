@@ -16,6 +16,7 @@
 #include <limits>
 #include <queue>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -503,6 +504,20 @@ struct rt_ctx {
     struct Ev { hipEvent_t a, b; int stage; };
     std::vector<Ev> pending;
     std::vector<hipEvent_t> pool;
+    int work_epoch = 0;        // bumped whenever build_work rebuilds d_work
+    // multi-device context (rt_options.n_devices > 1): this context renders on devices[0] and
+    // peers[j] on devices[j + 1]; tile t of the caller's shard goes to device (t / n_shards) mod n_devices
+    std::vector<rt_ctx*> peers;
+    struct PeerLink {          // on devices[0]: peer j's owned pixel ids and its compact exchange buffer
+        int* work0 = nullptr;
+        float4* xfer0 = nullptr;
+        size_t cap = 0;
+        int n = 0, epoch = -1;
+    };
+    std::vector<PeerLink> links;
+    hipEvent_t gathered = nullptr;   // devices[0]: peers' pixels packed (multi-device) / peer: pass done
+    float4* xfer = nullptr;          // on a peer: its compact exchange buffer
+    size_t xfer_cap = 0;
 };
 
 namespace {
@@ -664,6 +679,7 @@ int build_work(rt_ctx* c) {
     HIPCHK(c, hipMemcpy(c->d_work, px.data(), px.size() * sizeof(int), hipMemcpyHostToDevice));
     c->n_work = (int)px.size();
     c->work_dirty = false;
+    ++c->work_epoch;
     return RT_OK;
 }
 
@@ -1169,6 +1185,100 @@ int setup_sensor(rt_ctx* c, const rt_film_desc& d) {
     return RT_OK;
 }
 
+
+// ---- multi-device pass (rt_options.n_devices > 1).  Device 0 packs each peer's owned pixels of the
+// caller's film into that peer's exchange buffer; the peer copies them over xGMI, scatters them into its own film,
+// renders its tiles (the same kernels, the same per-pixel index order), packs them and copies them back; device 0
+// scatters them into the caller's film.  Pure copies: the film is bit-identical to a one-device render.
+int peer_prepare(rt_ctx* c, size_t j) {
+    rt_ctx* p = c->peers[j];
+    rt_ctx::PeerLink& L = c->links[j];
+    hipSetDevice(p->device);
+    int rc = build_work(p);
+    if (rc) return fail(c, rc, "device " + std::to_string(p->device) + ": " + p->err);
+    size_t n = (size_t)p->film.res_x * p->film.res_y;
+    if (p->film_cap < n) {
+        if (p->d_film) hipFree(p->d_film);
+        p->d_film = nullptr;
+        HIPCHK(c, dalloc(&p->d_film, n));
+        p->film_cap = n;
+    }
+    if (p->xfer_cap < (size_t)p->n_work) {
+        if (p->xfer) hipFree(p->xfer);
+        p->xfer = nullptr;
+        HIPCHK(c, dalloc(&p->xfer, (size_t)p->n_work));
+        p->xfer_cap = p->n_work;
+    }
+    hipSetDevice(c->device);
+    if (L.epoch != p->work_epoch) {
+        if (L.cap < (size_t)p->n_work) {
+            if (L.work0) hipFree(L.work0);
+            if (L.xfer0) hipFree(L.xfer0);
+            L.work0 = nullptr;
+            L.xfer0 = nullptr;
+            HIPCHK(c, dalloc(&L.work0, (size_t)p->n_work));
+            HIPCHK(c, dalloc(&L.xfer0, (size_t)p->n_work));
+            L.cap = p->n_work;
+        }
+        HIPCHK(c, hipMemcpyPeer(L.work0, c->device, p->d_work, p->device, sizeof(int) * p->n_work));
+        L.n = p->n_work;
+        L.epoch = p->work_epoch;
+    }
+    return RT_OK;
+}
+
+// the peer's half of a pass, on its own stream (runs in its own host thread: multi-level octrees sort with a
+// host round trip per bounce, which must not serialise the devices)
+int peer_pass(rt_ctx* c, size_t j, int ib, int ie) {
+    rt_ctx* p = c->peers[j];
+    const rt_ctx::PeerLink& L = c->links[j];
+    hipSetDevice(p->device);
+    hipStream_t ps = p->stream;
+    const size_t bytes = sizeof(float4) * L.n;
+    HIPCHK(p, hipStreamWaitEvent(ps, c->gathered, 0));
+    if (L.n) {
+        HIPCHK(p, hipMemcpyPeerAsync(p->xfer, p->device, L.xfer0, c->device, bytes, ps));
+        HIPCHK(p, launch_film_scatter(ps, L.n, p->d_work, p->xfer, p->d_film));
+    }
+    int rc = render_device(p, ib, ie, p->d_film, ps);
+    if (rc) return rc;
+    if (L.n) {
+        HIPCHK(p, launch_film_gather(ps, L.n, p->d_work, p->d_film, p->xfer));
+        HIPCHK(p, hipMemcpyPeerAsync(L.xfer0, c->device, p->xfer, p->device, bytes, ps));
+    }
+    HIPCHK(p, hipEventRecord(p->gathered, ps));
+    return RT_OK;
+}
+
+int render_multi(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
+    if (c->peers.empty()) return render_device(c, ib, ie, film, st);
+    int rc = check_ready(c);
+    if (rc) return rc;
+    if (ib < 0 || ie < ib) return fail(c, RT_E_ARG, "invalid index range");
+    for (size_t j = 0; j < c->peers.size(); ++j)
+        if ((rc = peer_prepare(c, j))) return rc;
+    hipSetDevice(c->device);
+    for (const rt_ctx::PeerLink& L : c->links)
+        if (L.n) HIPCHK(c, launch_film_gather(st, L.n, L.work0, film, L.xfer0));
+    HIPCHK(c, hipEventRecord(c->gathered, st));
+    std::vector<int> prc(c->peers.size(), RT_OK);
+    std::vector<std::thread> th;
+    th.reserve(c->peers.size());
+    for (size_t j = 0; j < c->peers.size(); ++j) th.emplace_back([&, j] { prc[j] = peer_pass(c, j, ib, ie); });
+    rc = render_device(c, ib, ie, film, st);
+    for (std::thread& t : th) t.join();
+    hipSetDevice(c->device);
+    if (rc) return rc;
+    for (size_t j = 0; j < c->peers.size(); ++j)
+        if (prc[j]) return fail(c, prc[j], "device " + std::to_string(c->peers[j]->device) + ": " + c->peers[j]->err);
+    for (size_t j = 0; j < c->peers.size(); ++j) {
+        const rt_ctx::PeerLink& L = c->links[j];
+        HIPCHK(c, hipStreamWaitEvent(st, c->peers[j]->gathered, 0));
+        if (L.n) HIPCHK(c, launch_film_scatter(st, L.n, L.work0, L.xfer0, film));
+    }
+    return RT_OK;
+}
+
 }  // namespace
 
 // =========================================================================================== C-ABI
@@ -1176,7 +1286,9 @@ extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
-int rt_create(const rt_options* opt, rt_ctx** out) {
+static void destroy_one(rt_ctx* c);
+
+static int create_one(const rt_options* opt, rt_ctx** out) {
     if (!out) return RT_E_ARG;
     *out = nullptr;
     int ndev = 0;
@@ -1201,7 +1313,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     c->hs.init();
     if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->ws[0].d_qcount, 2 * kQRegion) != hipSuccess ||
         dalloc(&c->d_ctr, (size_t)C_NCOUNTERS) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
-        rt_destroy(c);
+        destroy_one(c);
         return RT_E_OOM;
     }
     DevSpectra ds{};
@@ -1220,7 +1332,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     {
         rt_film_desc fd{};  // XYZ sensor under D65 until rt_film_set says otherwise
         if (setup_sensor(c, fd) != RT_OK) {
-            rt_destroy(c);
+            destroy_one(c);
             return RT_E_HIP;
         }
     }
@@ -1228,7 +1340,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     return RT_OK;
 }
 
-void rt_destroy(rt_ctx* c) {
+static void destroy_one(rt_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
@@ -1254,7 +1366,7 @@ void rt_destroy(rt_ctx* c) {
 
 const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
-int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
+static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     if (!c || !s) return RT_E_ARG;
     if (s->n_triangles <= 0 || s->n_vertices <= 0 || !s->positions || !s->indices)
         return fail(c, RT_E_ARG, "scene needs positions and indices");
@@ -1632,7 +1744,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
     return RT_OK;
 }
 
-int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
+static int camera_set_one(rt_ctx* c, const rt_camera_desc* d) {
     if (!c || !d) return RT_E_ARG;
     if (d->type < RT_CAMERA_PERSPECTIVE || d->type > RT_CAMERA_THINLENS) return fail(c, RT_E_ARG, "unknown camera type");
     c->cam = *d;
@@ -1640,7 +1752,7 @@ int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
     return RT_OK;
 }
 
-int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
+static int sampler_set_one(rt_ctx* c, const rt_sampler_desc* d) {
     if (!c || !d) return RT_E_ARG;
     if (d->kind < RT_SAMPLER_INDEPENDENT || d->kind > RT_SAMPLER_SOBOL) return fail(c, RT_E_ARG, "unknown sampler");
     if (d->kind == RT_SAMPLER_SOBOL && (d->randomize < RT_SOBOL_NONE || d->randomize > RT_SOBOL_OWEN))
@@ -1652,7 +1764,7 @@ int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
     return RT_OK;
 }
 
-int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
+static int film_set_one(rt_ctx* c, const rt_film_desc* d) {
     if (!c || !d) return RT_E_ARG;
     if (d->res_x <= 0 || d->res_y <= 0 || d->filter < RT_FILTER_BOX || d->filter > RT_FILTER_LANCZOS)
         return fail(c, RT_E_ARG, "invalid film");
@@ -1693,7 +1805,7 @@ int rt_film_matrices(rt_ctx* c, float* xyz_from_sensor9, float* rgb_from_xyz9) {
     return RT_OK;
 }
 
-int rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
+static int integrator_set_one(rt_ctx* c, const rt_integrator_desc* d) {
     if (!c || !d) return RT_E_ARG;
     if (d->kind != RT_INTEGRATOR_REFERENCE && d->kind != RT_INTEGRATOR_PATH && d->kind != RT_INTEGRATOR_PATH_MIS)
         return fail(c, RT_E_ARG, "unknown integrator");
@@ -1708,7 +1820,7 @@ int rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
     return RT_OK;
 }
 
-int rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
+static int set_shard_one(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
     if (!c || tile_size <= 0 || tile_size % 8 || n_shards <= 0 || shard_id < 0 || shard_id >= n_shards)
         return c ? fail(c, RT_E_ARG, "invalid shard (tile_size must be a positive multiple of 8)") : RT_E_ARG;
     c->tile = tile_size;
@@ -1722,7 +1834,7 @@ int rt_render_pass_device(rt_ctx* c, int ib, int ie, void* d_film, void* stream)
     if (!c || !d_film) return RT_E_ARG;
     hipSetDevice(c->device);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    return render_device(c, ib, ie, (float4*)d_film, st);
+    return render_multi(c, ib, ie, (float4*)d_film, st);
 }
 
 int rt_render_pass(rt_ctx* c, int ib, int ie, rt_pixel* film) {
@@ -1738,7 +1850,7 @@ int rt_render_pass(rt_ctx* c, int ib, int ie, rt_pixel* film) {
         c->film_cap = n;
     }
     HIPCHK(c, hipMemcpyAsync(c->d_film, film, n * 16, hipMemcpyHostToDevice, c->stream));
-    if ((rc = render_device(c, ib, ie, c->d_film, c->stream))) return rc;
+    if ((rc = render_multi(c, ib, ie, c->d_film, c->stream))) return rc;
     HIPCHK(c, hipMemcpyAsync(film, c->d_film, n * 16, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return RT_OK;
@@ -1769,7 +1881,7 @@ int film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out, int srgb) {
 int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 0); }
 int rt_film_resolve_srgb(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 1); }
 
-int rt_get_stats(rt_ctx* c, rt_stats* out) {
+static int get_stats_one(rt_ctx* c, rt_stats* out) {
     if (!c || !out) return RT_E_ARG;
     hipSetDevice(c->device);
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1790,7 +1902,7 @@ int rt_get_stats(rt_ctx* c, rt_stats* out) {
     return RT_OK;
 }
 
-int rt_reset_stats(rt_ctx* c) {
+static int reset_stats_one(rt_ctx* c) {
     if (!c) return RT_E_ARG;
     hipSetDevice(c->device);
     HIPCHK(c, hipDeviceSynchronize());
@@ -1913,6 +2025,133 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
             rc = fail(c, RT_E_HIP, std::string("debug samples: ") + hipGetErrorString(hipGetLastError()));
     }
     hipFree(dp); hipFree(di); hipFree(dout);
+    return rc;
+}
+
+// ---- multi-device wrappers: configuration goes to every device of the context -------------------------------
+extern "C++" template <class F>
+static int on_all(rt_ctx* c, F f) {
+    int rc = f(c);
+    for (size_t j = 0; !rc && j < c->peers.size(); ++j) {
+        rt_ctx* p = c->peers[j];
+        hipSetDevice(p->device);
+        if ((rc = f(p))) fail(c, rc, "device " + std::to_string(p->device) + ": " + p->err);
+    }
+    hipSetDevice(c->device);
+    return rc;
+}
+
+int rt_create(const rt_options* opt, rt_ctx** out) {
+    if (!out) return RT_E_ARG;
+    *out = nullptr;
+    int nd = opt ? opt->n_devices : 0;
+    if (nd <= 1) return create_one(opt, out);
+    if (nd > RT_MAX_DEVICES) return RT_E_ARG;
+    rt_options o = *opt;
+    o.n_devices = 0;
+    o.device = opt->devices[0];
+    rt_ctx* c = nullptr;
+    int rc = create_one(&o, &c);
+    if (rc) return rc;
+    for (int j = 1; j < nd; ++j) {
+        rt_ctx* p = nullptr;
+        o.device = opt->devices[j];
+        if ((rc = create_one(&o, &p))) { rt_destroy(c); return rc; }
+        c->peers.push_back(p);
+        c->links.emplace_back();
+        if (p->device != c->device) {  // direct xGMI peer copies both ways where the platform allows them
+            int ok = 0;
+            if (hipDeviceCanAccessPeer(&ok, c->device, p->device) == hipSuccess && ok) {
+                hipSetDevice(c->device);
+                if (hipDeviceEnablePeerAccess(p->device, 0) != hipSuccess) (void)hipGetLastError();
+                hipSetDevice(p->device);
+                if (hipDeviceEnablePeerAccess(c->device, 0) != hipSuccess) (void)hipGetLastError();
+            }
+        }
+        hipSetDevice(p->device);
+        if (hipEventCreateWithFlags(&p->gathered, hipEventDisableTiming) != hipSuccess) { rt_destroy(c); return RT_E_HIP; }
+    }
+    hipSetDevice(c->device);
+    if (hipEventCreateWithFlags(&c->gathered, hipEventDisableTiming) != hipSuccess) { rt_destroy(c); return RT_E_HIP; }
+    if ((rc = rt_set_shard(c, 32, 1, 0))) { rt_destroy(c); return rc; }
+    *out = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* c) {
+    if (!c) return;
+    for (size_t j = 0; j < c->peers.size(); ++j) {
+        rt_ctx* p = c->peers[j];
+        hipSetDevice(p->device);
+        if (p->stream) hipStreamSynchronize(p->stream);
+        if (p->xfer) hipFree(p->xfer);
+        if (p->gathered) hipEventDestroy(p->gathered);
+        destroy_one(p);
+    }
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (rt_ctx::PeerLink& L : c->links) {
+        if (L.work0) hipFree(L.work0);
+        if (L.xfer0) hipFree(L.xfer0);
+    }
+    if (c->gathered) hipEventDestroy(c->gathered);
+    destroy_one(c);
+}
+
+int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
+    if (!c) return RT_E_ARG;
+    return on_all(c, [&](rt_ctx* x) { return scene_upload_one(x, s); });
+}
+int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
+    if (!c) return RT_E_ARG;
+    return on_all(c, [&](rt_ctx* x) { return camera_set_one(x, d); });
+}
+int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
+    if (!c) return RT_E_ARG;
+    return on_all(c, [&](rt_ctx* x) { return sampler_set_one(x, d); });
+}
+int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
+    if (!c) return RT_E_ARG;
+    return on_all(c, [&](rt_ctx* x) { return film_set_one(x, d); });
+}
+int rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
+    if (!c) return RT_E_ARG;
+    return on_all(c, [&](rt_ctx* x) { return integrator_set_one(x, d); });
+}
+int rt_reset_stats(rt_ctx* c) {
+    if (!c) return RT_E_ARG;
+    return on_all(c, [&](rt_ctx* x) { return reset_stats_one(x); });
+}
+// the caller's shard (tile t, t % n_shards == shard_id) is split over the context's D devices: device k takes the
+// tiles with (t / n_shards) % D == k, i.e. shard (n_shards·D, shard_id + n_shards·k) of the frame
+// counters and kernel times summed over the context's devices
+int rt_get_stats(rt_ctx* c, rt_stats* out) {
+    if (!c || !out) return RT_E_ARG;
+    rt_stats sum{};
+    int rc = on_all(c, [&](rt_ctx* x) -> int {
+        rt_stats s{};
+        int r = get_stats_one(x, &s);
+        if (r) return r;
+        sum.samples += s.samples; sum.rays += s.rays; sum.shadow_rays += s.shadow_rays;
+        sum.nodes_tested += s.nodes_tested; sum.tris_tested += s.tris_tested; sum.hits += s.hits;
+        sum.shadow_nodes_tested += s.shadow_nodes_tested; sum.shadow_tris_tested += s.shadow_tris_tested;
+        sum.ms_generate += s.ms_generate; sum.ms_trace += s.ms_trace; sum.ms_shade += s.ms_shade;
+        sum.ms_shadow += s.ms_shadow; sum.ms_film += s.ms_film;
+        sum.launches_trace += s.launches_trace; sum.launches_shade += s.launches_shade;
+        return RT_OK;
+    });
+    if (!rc) *out = sum;
+    return rc;
+}
+
+int rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
+    if (!c || n_shards <= 0 || shard_id < 0 || shard_id >= n_shards)
+        return c ? fail(c, RT_E_ARG, "invalid shard") : RT_E_ARG;
+    const int D = 1 + (int)c->peers.size();
+    int rc = set_shard_one(c, tile_size, n_shards * D, shard_id);
+    for (size_t j = 0; !rc && j < c->peers.size(); ++j)
+        if ((rc = set_shard_one(c->peers[j], tile_size, n_shards * D, shard_id + n_shards * (int)(j + 1))))
+            fail(c, rc, c->peers[j]->err);
     return rc;
 }
 

@@ -228,5 +228,7 @@ hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, cons
                             unsigned long long* ctr);
 hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* m_xyz_from_sensor,
                           const float* m_rgb_from_xyz, unsigned char* out, int srgb);
+hipError_t launch_film_gather(hipStream_t st, int n, const int* work, const float4* film, float4* out);
+hipError_t launch_film_scatter(hipStream_t st, int n, const int* work, const float4* in, float4* film);
 
 }  // namespace rtmi

@@ -1403,6 +1403,19 @@ __global__ void k_resolve(int n, const float4* film, const float* __restrict__ A
     }
 }
 
+// ========================================================== multi-device film exchange
+// Owned-pixel gather / scatter between a film and a compact buffer in the shard's work order: the only data a
+// device of a multi-GPU context sends or receives per pass.  Pure copies (no arithmetic), so the exchanged film is
+// bit-identical to a one-device render.
+__global__ void __launch_bounds__(kBlock) k_film_gather(int n, const int* __restrict__ work, const float4* __restrict__ film,
+                                                        float4* __restrict__ out) {
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) out[k] = film[work[k]];
+}
+__global__ void __launch_bounds__(kBlock) k_film_scatter(int n, const int* __restrict__ work, const float4* __restrict__ in,
+                                                         float4* __restrict__ film) {
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) film[work[k]] = in[k];
+}
+
 // ============================================================================== launch wrappers
 static inline int grid_for(int n, int grid) {
     int g = (n + kBlock - 1) / kBlock;
@@ -1523,6 +1536,16 @@ hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, cons
 hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* a, const float* b, unsigned char* out,
                           int srgb) {
     hipLaunchKernelGGL(k_resolve, dim3(grid_for(n, 0)), dim3(kBlock), 0, st, n, film, a, b, out, srgb);
+    return hipGetLastError();
+}
+
+hipError_t launch_film_gather(hipStream_t st, int n, const int* work, const float4* film, float4* out) {
+    hipLaunchKernelGGL(k_film_gather, dim3(grid_for(n, 2048)), dim3(kBlock), 0, st, n, work, film, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_film_scatter(hipStream_t st, int n, const int* work, const float4* in, float4* film) {
+    hipLaunchKernelGGL(k_film_scatter, dim3(grid_for(n, 2048)), dim3(kBlock), 0, st, n, work, in, film);
     return hipGetLastError();
 }
 

@@ -9,12 +9,20 @@ from . import capi
 
 
 class Renderer:
-    """One rt_ctx bound to one GPU.  Configured from a scene.Config (or the individual descriptors)."""
+    """One rt_ctx.  `device` is one HIP ordinal or a list of them (rt_options.devices: every pass renders on
+    all of them at once, pixel tiles interleaved, the film bit-identical to one device).  Configured from a
+    scene.Config (or the individual descriptors)."""
 
     def __init__(self, cfg=None, device=0, octree_build=capi.RT_OCTREE_BUILD_DEVICE):
         self.lib = capi.load_library()
         opt = capi.rt_options()
-        opt.device = device
+        devs = list(device) if isinstance(device, (list, tuple)) else [int(device)]
+        if not 1 <= len(devs) <= capi.RT_MAX_DEVICES:
+            raise ValueError(f"1..{capi.RT_MAX_DEVICES} devices")
+        opt.device = devs[0]
+        opt.n_devices = len(devs)
+        for i, d in enumerate(devs):
+            opt.devices[i] = d
         opt.octree_build = octree_build
         h = C.c_void_p()
         rc = self.lib.rt_create(C.byref(opt), C.byref(h))

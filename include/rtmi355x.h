@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 typedef enum {
     RT_OK = 0,
@@ -37,10 +37,17 @@ typedef enum {
 
 typedef struct rt_ctx rt_ctx;
 
+#define RT_MAX_DEVICES 16
+/* rt_create ("device list"): n_devices <= 1 renders on `device`; n_devices > 1 renders every pass
+ * on devices[0..n_devices) at once — pixel tiles interleaved over the devices (tile t -> device t mod n), the
+ * caller's film on devices[0] (rt_render_pass_device) or on the host, owned pixels exchanged with peer copies
+ * over xGMI.  The film is bit-identical to a one-device render.  A device may be listed more than once (tests). */
 typedef struct {
-    int device;        /* HIP device ordinal                                              */
+    int device;        /* HIP device ordinal (n_devices <= 1)                             */
     int octree_build;  /* RT_OCTREE_BUILD_DEVICE (default) or RT_OCTREE_BUILD_HOST         */
-    int reserved[6];
+    int n_devices;     /* 0 or 1: one device; 2..RT_MAX_DEVICES: devices[]                 */
+    int devices[RT_MAX_DEVICES];
+    int reserved[5];
 } rt_options;
 /* Where rt_scene_upload builds the octree (Octtree_Model.h:33-63): both give the reference's tree bit for bit. */
 enum { RT_OCTREE_BUILD_DEVICE = 0, RT_OCTREE_BUILD_HOST = 1 };
@@ -201,7 +208,7 @@ typedef struct {
                                         stays 0: shadow rays are traced inside the path shade kernel */
     int64_t launches_trace;          /* closest-hit trace launches (per-launch averages) */
     int64_t launches_shade;          /* shade launches (path mode: includes the inline shadow rays) */
-} rt_stats;
+} rt_stats;   /* multi-device contexts: every field summed over the devices */
 
 /* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */
 typedef struct {

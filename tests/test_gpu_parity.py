@@ -446,3 +446,45 @@ def test_device_octree_build_cfg3_matches_host(cfg3_pair):
     for k in ("bounds", "child", "leaf_count", "refs"):
         assert np.array_equal(bits(a[k]) if k == "bounds" else a[k], bits(b[k]) if k == "bounds" else b[k])
     print(f"\nCFG3 scene upload: host build {t_host * 1e3:.0f} ms, device build {t_dev * 1e3:.0f} ms")
+
+
+@pytest.mark.parametrize("kind,ndev", [("cornell", 2), ("cornell", 3), ("mesh", 2), ("reference", 3)])
+def test_multi_device_context_film_bitexact(oracle_lib, kind, ndev):
+    """rt_options.devices (SURVEY §8b device list): one context rendering on several devices, pixel tiles
+    interleaved, owned pixels exchanged by peer copies.  On the 1-GPU test box device 0 is listed `ndev` times
+    (separate contexts, streams and buffers on one GPU): the same code path as distinct GPUs.  The film —
+    accumulated over two passes, so the exchange must carry the caller's earlier values — is bit-identical to
+    the oracle (tolerance 0)."""
+    if kind == "cornell":
+        cfg = scene.cfg_cornell(res=(72, 40), spp_side=2)
+    elif kind == "mesh":
+        cfg = scene.cfg3_blob(res=(64, 40), spp_side=2, max_depth=3, frequency=20)
+    else:
+        cfg = scene.cfg0_reference(res=(64, 64), frequency=8, n_index=4)
+    g = Renderer(cfg, device=[0] * ndev)
+    f = g.new_film()
+    g.render_pass(0, 1, f)
+    g.render_pass(1, 4, f)
+    fo = oracle_lib.OracleScene(cfg).render(0, 4)
+    bad = np.any(bits(f) != bits(fo), axis=1)
+    assert bad.sum() == 0, f"{bad.sum()} pixels differ"
+    st = g.stats()
+    assert st["samples"] == 4 * cfg.film.res[0] * cfg.film.res[1]   # summed over the devices
+
+
+def test_multi_device_device_film_and_shard(oracle_lib):
+    """Device-resident film (rt_render_pass_device) on a 2-device context, and a process-level shard split
+    over the context's devices: equals the single-device render of the same shard."""
+    import torch
+    cfg = scene.cfg_cornell(res=(80, 48), spp_side=2)
+    one = Renderer(cfg)
+    one.set_shard(16, 2, 1)
+    ref = one.render_pass(0, 4)
+    g = Renderer(cfg, device=[0, 0])
+    g.set_shard(16, 2, 1)
+    film = torch.zeros((80 * 48, 4), dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    g.render_pass_device(0, 2, film.data_ptr(), s.cuda_stream)
+    g.render_pass_device(2, 4, film.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(film.cpu().numpy()), bits(ref))
