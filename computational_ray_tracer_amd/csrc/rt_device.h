@@ -516,6 +516,21 @@ RT_DEV bool box_hit(float4 a, float4 b, V3 o, V3 inv, float tMax) {
     return !(mn > mx);
 }
 
+// Conservative box test for the single-leaf culling clusters only — never an octree node, whose test keeps
+// Bounds3::IntersectP's exact operations above.  Same slab distances and tFar factor as box_hit, reduced with
+// v_min/v_max (IEEE minNum/maxNum) instead of compare-and-select chains.  The one behavioural difference: a plane
+// distance that is NaN (d_axis == 0 with the origin exactly on that plane) makes the other plane of the axis decide
+// the slab; such a ray lies in the box's face plane, at least the cluster pad away from every triangle of the
+// cluster (rt_host.cpp upload), so no candidate test of the cluster can pass and skipping it is exact.
+RT_DEV bool cluster_hit(float4 a, float4 b, V3 o, V3 inv, float tMax) {
+    const float g = 1 + 2 * gamma_n(3);
+    const float x0 = (a.x - o.x) * inv.x, x1 = (b.x - o.x) * inv.x;
+    const float y0 = (a.y - o.y) * inv.y, y1 = (b.y - o.y) * inv.y;
+    const float z0 = (a.z - o.z) * inv.z, z1 = (b.z - o.z) * inv.z;
+    const float mn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.f));
+    const float mx = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)) * g;
+    return mn <= fminf(mx, tMax);
+}
 
 // Sampling.h:809-840 Continuous_Inversion_Sampler::Sample: binary search of U in the CDF table, then linear
 // interpolation inside the bin (table built on the host, rt_host.cpp inversion_table).
