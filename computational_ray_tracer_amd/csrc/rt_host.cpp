@@ -1727,6 +1727,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     d.n_shapes = s->n_shapes;
     c->scene_full = full;
     d.qcap = qcap;
+    d.depth = nn < (1 << 24) ? maxd : 1 << 30;  // DFS stack entries hold 24-bit group ids
     if (qcap == 0) {
         int rs = 1;
         while (rs < bound) rs <<= 1;

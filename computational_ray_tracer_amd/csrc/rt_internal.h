@@ -102,6 +102,7 @@ struct DevScene {
     float4 cl_guard;                  // (centre, radius²): rays starting farther out never skip a cluster
     unsigned long long fan_pairs[2];  // single-leaf scenes: bit k (k even) = tiles k, k+1 are a fan pair (a,b,c),(a,c,d)
     int qcap;                       // BFS group FIFO size (compiled variants); 0 = global-memory ring below
+    int depth;                      // octree depth (root = 0): any-hit queries walk depth-first when <= kDfsDepth
     int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
     int ring_mask;
     int ring_threads;               // launches with qcap == 0 are clamped to this many threads

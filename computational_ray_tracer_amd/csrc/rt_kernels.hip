@@ -471,6 +471,94 @@ __device__ __forceinline__ T ldconst(const T* p, int i) {
     return r;
 }
 
+// Any-hit (shadow) query on a multi-level octree, depth first.  With a fixed tMax every node box test and every
+// triangle test has the same outcome whatever the order, the leaves reached through passing boxes are the same set,
+// and the query only asks whether some tested triangle hits (Octtree_Model.h:66-127 with an early exit).  So a
+// depth-first walk returns exactly the BFS's answer, but reaches an occluder after `depth` descents instead of
+// after sweeping every level above it, and needs a stack of `depth` entries instead of a frontier-sized FIFO.
+// Stack entry = (first node of a group << 8) | its children still to visit; LDS, one column per thread.
+#ifndef RT_DFS_ANYHIT
+#define RT_DFS_ANYHIT 0      // exact, but 175 VGPRs in the shade kernel (BFS: 159): occupancy 3 -> 2, CFG3 121 -> 114,
+#endif                       // CFG4 87 -> 66 Msamples/s (A/B): off
+static constexpr int kDfsDepth = 16;
+#if RT_DFS_ANYHIT
+__shared__ unsigned g_dfs[kDfsDepth * kBlock];
+#endif
+template <int KZ>
+__device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, V3 d, float tMax,
+                                             unsigned long long& nn, unsigned long long& nt) {
+#if RT_DFS_ANYHIT
+    const V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
+    const TriRay R = make_triray<KZ>(o, d);
+    const int2* __restrict__ lr = sc.leafRange[set];
+    const float4* __restrict__ tiles = sc.tiles[set];
+    unsigned* stk = g_dfs + threadIdx.x;
+    int sp = 0;
+    int g = 0;          // first node of the current group (the root is a group of one)
+    unsigned pm;        // its children still to visit whose box passes
+    int Ch[8];          // their first children (-1: leaf), kept in registers for the current group
+    int lf = 0, lc = 0; // pending leaf: first tile, triangle count
+    ++nn;
+    {
+        const float4 a = sc.nodeA[0];
+        pm = box_entry(a, sc.nodeB[0], o, inv) <= tMax ? 1u : 0u;
+        Ch[0] = __float_as_int(a.w);
+#pragma unroll
+        for (int k = 1; k < 8; ++k) Ch[k] = -1;
+    }
+    bool done = false;
+    while (true) {
+        // node phase ("while-while", as the BFS): walk until this lane holds a non-empty leaf or runs out
+        while (!done && lc == 0) {
+            if (pm == 0) {
+                if (sp == 0) { done = true; break; }
+                const unsigned e = stk[--sp * kBlock];
+                g = (int)(e >> 8);
+                pm = e & 0xffu;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) Ch[k] = __float_as_int(sc.nodeA[g + k].w);  // independent loads
+                continue;
+            }
+            const int i = __builtin_ctz(pm);
+            pm &= pm - 1;
+            int child = Ch[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) child = i == k ? Ch[k] : child;
+            if (child >= 0) {
+                if (pm) stk[sp++ * kBlock] = ((unsigned)g << 8) | pm;
+                g = child;
+                float4 A8[8], B8[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { A8[k] = sc.nodeA[g + k]; B8[k] = sc.nodeB[g + k]; }
+                nn += 8;
+                pm = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    pm |= (box_entry(A8[k], B8[k], o, inv) <= tMax ? 1u : 0u) << k;
+                    Ch[k] = __float_as_int(A8[k].w);
+                }
+            } else {
+                const int2 r = lr[g + i];
+                lf = r.x;
+                lc = r.y;
+            }
+        }
+        if (lc == 0) return false;
+        const int m = lc < kLeafChunk ? lc : kLeafChunk;
+        for (int k = 0; k < m; ++k) {
+            const float4* tp = tiles + 3 * (lf + k);
+            ++nt;
+            float b0, b1, b2, t;
+            if (tri_intersect<KZ>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax) return true;
+        }
+        lf += m;
+        lc -= m;
+    }
+#else
+    return false;
+#endif
+}
+
 // ===================================================================================== K2 traverse
 // Octtree_Model.h:66-127 — FIFO BFS.  The 8 children of an internal node are contiguous, so the queue
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
@@ -664,6 +752,12 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         }
         return best;
     }
+#if RT_DFS_ANYHIT
+    if constexpr (ANYHIT) {
+        if (sc.depth <= kDfsDepth)  // the upload's octree depth; deeper trees keep the BFS FIFO below
+            return occluded_dfs<KZ>(sc, set, o, d, tMax, nn, nt) ? 0 : -1;  // any-hit: 0 = occluded
+    }
+#endif
     // Group FIFO.  QCAP > 1: a private array (registers) holding the host's exact worst-case bound.
     // QCAP == 0: the first kLdsQ entries of each lane's FIFO live in LDS as 16-bit group ids (first child =
     // 8 g + 1); once a push finds them full the lane spills every later push to its HBM ring (sized by the
