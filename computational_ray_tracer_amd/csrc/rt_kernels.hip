@@ -478,8 +478,9 @@ __device__ __forceinline__ T ldconst(const T* p, int i) {
 // after sweeping every level above it, and needs a stack of `depth` entries instead of a frontier-sized FIFO.
 // Stack entry = (first node of a group << 8) | its children still to visit; LDS, one column per thread.
 #ifndef RT_DFS_ANYHIT
-#define RT_DFS_ANYHIT 0      // exact, but 175 VGPRs in the shade kernel (BFS: 159): occupancy 3 -> 2, CFG3 121 -> 114,
-#endif                       // CFG4 87 -> 66 Msamples/s (A/B): off
+#define RT_DFS_ANYHIT 0      // bit 0: k_path_shade's shadow rays, bit 1: k_path_shade_full / k_occluded.  Exact either
+#endif                       // way; the stack's registers cost occupancy or spills under the 4-wave budgets below:
+                             // CFG3 144 -> 135 (bit 0), CFG4 111 -> 87 (bit 1) Msamples/s (A/B): off
 static constexpr int kDfsDepth = 16;
 #if RT_DFS_ANYHIT
 __shared__ unsigned g_dfs[kDfsDepth * kBlock];
@@ -564,7 +565,7 @@ __device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, 
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
 // reference's node-level FIFO order exactly.  tMax shrinks on every accepted hit ("t < tMax": the first
 // hit found in BFS order wins ties), so hit ids, barycentrics and t are bit-identical to the reference's.
-template <int QCAP, bool ANYHIT, int KZ>
+template <int QCAP, bool ANYHIT, int KZ, bool DFS = false>
 __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0, float& rb1,
                                         float& rb2, float& rt, unsigned long long& nn, unsigned long long& nt) {
     V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -753,7 +754,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         return best;
     }
 #if RT_DFS_ANYHIT
-    if constexpr (ANYHIT) {
+    if constexpr (ANYHIT && DFS) {
         if (sc.depth <= kDfsDepth)  // the upload's octree depth; deeper trees keep the BFS FIFO below
             return occluded_dfs<KZ>(sc, set, o, d, tMax, nn, nt) ? 0 : -1;  // any-hit: 0 = occluded
     }
@@ -867,21 +868,23 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
 
 // When every active lane of the wave has the same dominant ray axis (camera rays, kz-binned queues) the
 // watertight test's coordinate permutation is resolved at compile time; otherwise per lane.
-template <int QCAP, bool ANYHIT>
+template <int QCAP, bool ANYHIT, bool DFS = false>
 __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
                                             float& b2, float& t, unsigned long long& nn, unsigned long long& nt) {
 #if RT_KZ_SPECIALIZE
     int kz = dominant_axis(d);
     uint64_t act = __ballot(true);
-    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
 #endif
-    return traverse<QCAP, ANYHIT, -1>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    return traverse<QCAP, ANYHIT, -1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
 }
 
 #ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 0     // >0: amdgpu_waves_per_eu floor for the closest-hit kernel (register budget)
+#define RT_TRACE_WAVES 4     // >0: amdgpu_waves_per_eu floor for the closest-hit kernel (register budget).  4: the
+                             // multi-level instantiation drops 147 -> 128 VGPRs (48 B/lane spill), 3 -> 4 waves/SIMD:
+                             // CFG3 +10 %; the single-leaf one (107) is unchanged
 #endif
 #if RT_TRACE_WAVES > 0
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
@@ -1033,7 +1036,9 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 // FUSED: the bounce's closest-hit traversal runs here too (the ray is read once, the hit stays in registers), so
 // the VALU-bound traversal and the HBM-bound path-state traffic of different waves overlap on every CU.
 #ifndef RT_SHADE_WAVES
-#define RT_SHADE_WAVES 0     // >0: amdgpu_waves_per_eu floor for the path shade kernel (register budget)
+#define RT_SHADE_WAVES 4     // >0: amdgpu_waves_per_eu floor for the path shade kernel (register budget).  4: the
+                             // multi-level instantiation 159 -> 128 VGPRs (132 B/lane spill), 3 -> 4 waves/SIMD;
+                             // with RT_TRACE_WAVES=4 CFG3 121 -> 144 Msamples/s; single-leaf (125) unchanged
 #endif
 #if RT_SHADE_WAVES > 0
 #define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WAVES)))
@@ -1184,7 +1189,7 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
 #ifdef RT_PROFILE_NO_SHADOW  // timing experiments only: every shadow ray counts as unoccluded
             int hit = -1;
 #else
-            int hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt);
+            int hit = traverse_any<QCAP, true, (RT_DFS_ANYHIT & 1) != 0>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt);
 #endif
             ++nsh;
             if (hit < 0) {
@@ -1241,7 +1246,7 @@ template <int QCAP>
 __device__ __forceinline__ bool scene_occluded(const DevScene& sc, V3 o, V3 d, float tmax, unsigned long long& nn,
                                                unsigned long long& nt) {
     float b0, b1, b2, t;
-    if (traverse_any<QCAP, true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0) return true;
+    if (traverse_any<QCAP, true, (RT_DFS_ANYHIT & 2) != 0>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0) return true;
     for (int si = 0; si < sc.n_shapes; ++si) {
         DevShape sh = ldconst(sc.shapes, si);
         V3 ph;
@@ -1266,8 +1271,18 @@ __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const f
     count_add(ctr, C_SHADOW, ns);
 }
 
+#ifndef RT_SHADE_FULL_WAVES
+#define RT_SHADE_FULL_WAVES 4  // >0: amdgpu_waves_per_eu floor for the mixed-scene shade kernel (register budget).
+                               // 3: 246 -> 168 VGPRs (312 B/lane spill), 2 -> 3 waves/SIMD: CFG4 87 -> 98 Msamples/s;
+                               // 4: 128 VGPRs (464 B/lane spill), 4 waves/SIMD: 111 Msamples/s (A/B)
+#endif
+#if RT_SHADE_FULL_WAVES > 0
+#define RT_SHADE_FULL_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_FULL_WAVES)))
+#else
+#define RT_SHADE_FULL_ATTR
+#endif
 template <int QCAP>
-__global__ void __launch_bounds__(kBlock) k_path_shade_full(DevScene sc, const DevSpectra* sp, DevSampler smp,
+__global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(DevScene sc, const DevSpectra* sp, DevSampler smp,
                                                             DevFilm film, SampleIds ids, PathIO io,
                                                             unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
