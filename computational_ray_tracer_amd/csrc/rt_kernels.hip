@@ -887,7 +887,10 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
                              // CFG3 +10 %; the single-leaf one (107) is unchanged
 #endif
 #if RT_TRACE_WAVES > 0
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
+#ifndef RT_TRACE_WAVES_1
+#define RT_TRACE_WAVES_1 RT_TRACE_WAVES  // single-leaf instantiation (QCAP == 1)
+#endif
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? RT_TRACE_WAVES_1 : RT_TRACE_WAVES)))
 #else
 #define RT_TRACE_ATTR
 #endif
@@ -1041,7 +1044,10 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
                              // with RT_TRACE_WAVES=4 CFG3 121 -> 144 Msamples/s; single-leaf (125) unchanged
 #endif
 #if RT_SHADE_WAVES > 0
-#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WAVES)))
+#ifndef RT_SHADE_WAVES_1
+#define RT_SHADE_WAVES_1 RT_SHADE_WAVES  // single-leaf instantiation (QCAP == 1)
+#endif
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? RT_SHADE_WAVES_1 : RT_SHADE_WAVES)))
 #else
 #define RT_SHADE_ATTR
 #endif

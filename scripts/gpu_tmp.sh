@@ -1,6 +1,9 @@
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
+if [ -n "$WITH_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_tmp.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu_tmp.log; [ $rc -ne 0 ] && exit $rc
+fi
 for c in ${CFGS:-cfg3 cfg4}; do
-  echo "== $c"; BENCH_ARGS="--config $c" BENCH_STEPS=${STEPS_FOR:-1} bash scripts/gpu_ab.sh || exit 1
+  s=1; [ $c = cornell ] && s=4
+  echo "== $c"; BENCH_ARGS="--config $c" BENCH_STEPS=$s bash scripts/gpu_ab.sh || exit 1
 done
