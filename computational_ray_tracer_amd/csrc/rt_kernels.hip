@@ -23,7 +23,7 @@ namespace rtmi {
 
 static constexpr int kBlock = kBlockThreads;
 #ifndef RT_LEAF_CHUNK
-#define RT_LEAF_CHUNK 16
+#define RT_LEAF_CHUNK 32
 #endif
 static constexpr int kLeafChunk = RT_LEAF_CHUNK;  // triangles per leaf phase of the while-while traversal
 static constexpr int kLdsQ = 32;  // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
@@ -763,6 +763,15 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     // QCAP == 0: the first kLdsQ entries of each lane's FIFO live in LDS as 16-bit group ids (first child =
     // 8 g + 1); once a push finds them full the lane spills every later push to its HBM ring (sized by the
     // bound) until the FIFO drains, so pops read LDS for positions below `spill` and HBM from there on.
+#ifndef RT_GROUP_FETCH
+#define RT_GROUP_FETCH 8  // child boxes loaded together per popped group (8, 4 or 2: register pressure vs MLP)
+#endif
+#ifndef RT_LEAF_PREFETCH
+#define RT_LEAF_PREFETCH 1  // software-pipelined leaf loop (next triangle's 48 B in flight during a test): 1 closest-hit only, 2 all
+#endif
+#ifndef RT_CH_RELOAD
+#define RT_CH_RELOAD 0    // 1: re-read a visited child's first-child index instead of keeping 8 in registers
+#endif
     constexpr bool GQ = QCAP == 0;
     int q[GQ ? 1 : QCAP];
     unsigned short* lq = g_lq;
@@ -804,24 +813,35 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 }
                 ++head;
                 if (GQ && head == tail) spill = 0x7fffffff;  // drained: LDS again
-                float4 A8[8], B8[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) { A8[i] = sc.nodeA[gfirst + i]; B8[i] = sc.nodeB[gfirst + i]; }
                 nn += 8;
                 pm = 0;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    E[i] = box_entry(A8[i], B8[i], o, inv);
-                    Ch[i] = __float_as_int(A8[i].w);
-                    pm |= (E[i] <= tMax ? 1u : 0u) << i;
+                for (int h = 0; h < 8; h += RT_GROUP_FETCH) {  // RT_GROUP_FETCH children's boxes in flight at once
+                    float4 A8[RT_GROUP_FETCH], B8[RT_GROUP_FETCH];
+#pragma unroll
+                    for (int i = 0; i < RT_GROUP_FETCH; ++i) {
+                        A8[i] = sc.nodeA[gfirst + h + i];
+                        B8[i] = sc.nodeB[gfirst + h + i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < RT_GROUP_FETCH; ++i) {
+                        E[h + i] = box_entry(A8[i], B8[i], o, inv);
+                        if (!RT_CH_RELOAD) Ch[h + i] = __float_as_int(A8[i].w);
+                        pm |= (E[h + i] <= tMax ? 1u : 0u) << (h + i);
+                    }
                 }
                 continue;
             }
             int i = __builtin_ctz(pm);
             pm &= pm - 1;
-            int child = Ch[0];
+            int child;
+            if (RT_CH_RELOAD) {
+                child = __float_as_int(sc.nodeA[gfirst + i].w);  // cache-resident: the group was just fetched
+            } else {
+                child = Ch[0];
 #pragma unroll
-            for (int k = 1; k < 8; ++k) child = i == k ? Ch[k] : child;
+                for (int k = 1; k < 8; ++k) child = i == k ? Ch[k] : child;
+            }
             if (child >= 0) {
                 if constexpr (GQ) {
                     if (spill == 0x7fffffff && tail - head < kLdsQ) {
@@ -844,9 +864,21 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         // at most kLeafChunk triangles per phase: a lane in a big leaf (the CFG3 octree has leaves of up to 583
         // triangles) keeps the rest pending while the other lanes walk on to their next leaf
         int m = lc < kLeafChunk ? lc : kLeafChunk;
+        constexpr bool PF = RT_LEAF_PREFETCH == 2 || (RT_LEAF_PREFETCH == 1 && !ANYHIT);
+        float4 nA, nB, nC;
+        if constexpr (PF) { nA = tiles[3 * lf]; nB = tiles[3 * lf + 1]; nC = tiles[3 * lf + 2]; }
         for (int k = 0; k < m; ++k) {
-            const float4* tp = tiles + 3 * (lf + k);
-            float4 A = tp[0], B = tp[1], Cc = tp[2];
+            float4 A, B, Cc;
+            if constexpr (PF) {
+                A = nA; B = nB; Cc = nC;  // the next triangle's loads are issued before this one's test
+                if (k + 1 < m) {
+                    const float4* np = tiles + 3 * (lf + k + 1);
+                    nA = np[0]; nB = np[1]; nC = np[2];
+                }
+            } else {
+                const float4* tp = tiles + 3 * (lf + k);
+                A = tp[0]; B = tp[1]; Cc = tp[2];
+            }
             ++nt;
             float b0, b1, b2, t;
             if (tri_intersect<KZ>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
@@ -888,9 +920,9 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 #endif
 #if RT_TRACE_WAVES > 0
 #ifndef RT_TRACE_WAVES_1
-#define RT_TRACE_WAVES_1 RT_TRACE_WAVES  // single-leaf instantiation (QCAP == 1)
+#define RT_TRACE_WAVES_1 0  // single-leaf instantiation (QCAP == 1); 0: no budget
 #endif
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? RT_TRACE_WAVES_1 : RT_TRACE_WAVES)))
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? (RT_TRACE_WAVES_1 > 0 ? RT_TRACE_WAVES_1 : 1) : RT_TRACE_WAVES)))
 #else
 #define RT_TRACE_ATTR
 #endif
@@ -1045,9 +1077,9 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 #endif
 #if RT_SHADE_WAVES > 0
 #ifndef RT_SHADE_WAVES_1
-#define RT_SHADE_WAVES_1 RT_SHADE_WAVES  // single-leaf instantiation (QCAP == 1)
+#define RT_SHADE_WAVES_1 0  // single-leaf instantiation (QCAP == 1); 0: no budget
 #endif
-#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? RT_SHADE_WAVES_1 : RT_SHADE_WAVES)))
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? (RT_SHADE_WAVES_1 > 0 ? RT_SHADE_WAVES_1 : 1) : RT_SHADE_WAVES)))
 #else
 #define RT_SHADE_ATTR
 #endif
