@@ -1070,6 +1070,12 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 // (Get2D, β *= R) appended to the next queue.  Sampler state (PCG state + dimension) lives per path slot.
 // FUSED: the bounce's closest-hit traversal runs here too (the ray is read once, the hit stays in registers), so
 // the VALU-bound traversal and the HBM-bound path-state traffic of different waves overlap on every CU.
+#ifndef RT_APPEND_FIRST
+#define RT_APPEND_FIRST 0    // 1: append the next bounce ray before the inline shadow traversal
+#endif
+#ifndef RT_LD_LDS
+#define RT_LD_LDS 0          // 1: the NEE contribution waits in LDS across the shadow traversal
+#endif
 #ifndef RT_SHADE_WAVES
 #define RT_SHADE_WAVES 4     // >0: amdgpu_waves_per_eu floor for the path shade kernel (register budget).  4: the
                              // multi-level instantiation 159 -> 128 VGPRs (132 B/lane spill), 3 -> 4 waves/SIMD;
@@ -1088,6 +1094,9 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
                                                        SampleIds ids, PathIO io, unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[(RT_NBINS + 6) * (kBlock / 64) + RT_NBINS + 8];
+#if RT_LD_LDS
+    __shared__ float s_ld[8 * kBlock];
+#endif
     const QueueCounts qc(io.count, 0);
     const int n = qc.n;
     unsigned long long snn = 0, snt = 0, nsh = 0, tnn = 0, tnt = 0, tnh = 0, tnr = 0;
@@ -1220,6 +1229,22 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
                 }
             }
         }
+#if RT_APPEND_FIRST  // the next ray leaves before the shadow traversal: its 9 registers are not live across it
+    {
+#if RT_RAY_SORT
+        long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
+#else
+        long pn = queue_append<WAVE>(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
+#endif
+        if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
+    }
+#endif
+#if RT_LD_LDS  // the pending contribution waits in LDS (8 floats per thread) instead of registers
+        if (wantShadow) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s_ld[i * kBlock + threadIdx.x] = Ld[i];
+        }
+#endif
         // NEE shadow ray, traced inline (any hit, fixed tMax) after the bounce state is written, so only the
         // pending contribution Ld stays live across the traversal.  No shadow queue in HBM.
         if (wantShadow) {
@@ -1233,6 +1258,10 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
             if (hit < 0) {
                 float L[8];
                 load8_or_zero(io.LA, io.LB, slot, L, d0);
+#if RT_LD_LDS
+#pragma unroll
+                for (int i = 0; i < 8; ++i) Ld[i] = s_ld[i * kBlock + threadIdx.x];
+#endif
 #pragma unroll
                 for (int i = 0; i < 8; ++i) L[i] += Ld[i];
                 store8(io.LA, io.LB, slot, L);
@@ -1243,12 +1272,14 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
             const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             store8(io.LA, io.LB, slot, z);
         }
+#if !RT_APPEND_FIRST
 #if RT_RAY_SORT
         long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
 #else
         long pn = queue_append<WAVE>(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
 #endif
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
+#endif
     }
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
