@@ -448,11 +448,20 @@ struct Work {
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
     void* sTemp = nullptr;
     size_t sTempBytes = 0, sCap = 0;
+    // shadow queue (multi-level octrees): {o, tMax}, {d, slot}, pending contribution (2 x float4)
+    float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
+    size_t shCap = 0;
     hipStream_t stream = nullptr;  // lanes >= 1: own stream (lane 0 runs on the caller's stream)
     hipEvent_t film_done = nullptr;
     hipEvent_t trace_done = nullptr;  // RTMI_PAIR: the lanes' closest-hit launches take turns
 };
 
+#ifndef RT_SHADOW_QUEUE
+#define RT_SHADOW_QUEUE 0  // multi-level octrees: NEE shadow rays traced by k_path_shadow (RTMI_SHADOW_QUEUE)
+#endif
+#ifndef RT_SHADOW_DFS
+#define RT_SHADOW_DFS 1    // k_path_shadow: depth-first any-hit (RTMI_SHADOW_DFS)
+#endif
 struct rt_ctx {
     // coherence sort of path queues (multi-level octrees): scene quantisation of the sort key
     float4 sort_lo{}, sort_scale{};
@@ -488,6 +497,8 @@ struct rt_ctx {
     Work ws[kLanes];
     int lanes = RT_LANES;  // batches in flight in path mode (RTMI_LANES overrides)
     int grid_div = 1;      // persistent-grid divisor with lanes > 1 (RTMI_GRID_DIV overrides; A/B: 1 beats 2)
+    int shadow_queue = RT_SHADOW_QUEUE;  // multi-level simple path scenes: NEE rays traced by k_path_shadow
+    int shadow_dfs = RT_SHADOW_DFS;      // k_path_shadow walks depth-first (exact any-hit, §6)
     int pair = 0;          // RTMI_PAIR=1: closest-hit launches of the lanes never overlap (trace pairs with shade)
     size_t batch_samples = 0;  // samples in flight per batch (0: 8 Mi path / 16 Mi reference; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
@@ -546,6 +557,23 @@ void free_scene(rt_ctx* c) {
     c->have_scene = false;
 }
 
+void free_shadow_workspace(Work& w) {
+    void* ptrs[] = {w.shO, w.shD, w.shLA, w.shLB};
+    for (void* p : ptrs)
+        if (p) hipFree(p);
+    w.shO = w.shD = w.shLA = w.shLB = nullptr;
+    w.shCap = 0;
+}
+
+int ensure_shadow_workspace(rt_ctx* c, Work& w, size_t n) {
+    if (w.shCap >= n) return RT_OK;
+    free_shadow_workspace(w);
+    HIPCHK(c, dalloc(&w.shO, n)); HIPCHK(c, dalloc(&w.shD, n));
+    HIPCHK(c, dalloc(&w.shLA, n)); HIPCHK(c, dalloc(&w.shLB, n));
+    w.shCap = n;
+    return RT_OK;
+}
+
 void free_sort_workspace(Work& w) {
     void* ptrs[] = {w.sO, w.sD, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sTemp};
     for (void* p : ptrs)
@@ -572,6 +600,7 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
 // batch buffers only (the queue counters, stream and event of a lane live as long as the context)
 void free_workspace(Work& w) {
     free_sort_workspace(w);
+    free_shadow_workspace(w);
     void* ptrs[] = {w.rayO, w.rayD, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.betaA, w.betaB,
                     w.LA, w.LB, w.slot, w.hitPrim, w.dim, w.rng, w.prevPdf};
     for (void* p : ptrs)
@@ -943,6 +972,11 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     const bool dyn = RT_DYN_SCHED == 1 || (RT_DYN_SCHED == 2 && c->dsc.qcap != 1);
     const bool lean = RT_LEAN_GENERATE && !c->dsc.full;  // simple path kernel: no β / L / pdf streams
     const bool fused = RT_FUSED_BOUNCE && !c->dsc.full;  // simple scenes: trace inside the shade kernel
+    // multi-level simple scenes: NEE shadow rays queued and traced by their own kernel (no path state live)
+    const bool shq = c->shadow_queue && c->dsc.qcap != 1 && !c->dsc.full && !fused;
+    if (shq)
+        for (int l = 0; l < lanes; ++l)
+            if ((rc = ensure_shadow_workspace(c, c->ws[l], nmax))) return rc;
     // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
     // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
     // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
@@ -1026,9 +1060,19 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 pio.prevPdf = w.prevPdf;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 pio.ticket = dyn ? qc_cur + (RT_NBINS + 1) * kQStride : nullptr;
+                if (shq) {  // this queue's region holds the shadow-queue length and ticket (zeroed with it)
+                    pio.shO = w.shO; pio.shD = w.shD; pio.shLA = w.shLA; pio.shLB = w.shLB;
+                    pio.shCount = qc_cur + (RT_NBINS + 2) * kQStride;
+                    pio.shTicket = qc_cur + (RT_NBINS + 3) * kQStride;
+                }
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
                 ev_mark(c, s, ST_SHADE, e0);
+                if (shq) {
+                    e0 = ev_start(c, s);
+                    HIPCHK(c, launch_path_shadow(s, grid, c->dsc.qcap, c->shadow_dfs != 0, c->dsc, pio, c->d_ctr));
+                    ev_mark(c, s, ST_SHADOW, e0);
+                }
                 cur[l] = nxt;
             }
         }
@@ -1309,6 +1353,8 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_LANES")) c->lanes = std::max(1, std::min(kLanes, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_GRID_DIV")) c->grid_div = std::max(0, std::atoi(e));
     if (const char* e = std::getenv("RTMI_PAIR")) c->pair = std::atoi(e);
+    if (const char* e = std::getenv("RTMI_SHADOW_QUEUE")) c->shadow_queue = std::atoi(e);
+    if (const char* e = std::getenv("RTMI_SHADOW_DFS")) c->shadow_dfs = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
     c->hs.init();
     if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->ws[0].d_qcount, 2 * kQRegion) != hipSuccess ||

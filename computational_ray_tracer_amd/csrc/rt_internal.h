@@ -142,7 +142,8 @@ static const int kQStride = 64;
 #ifndef RT_NBINS
 #define RT_NBINS 3  // bins of a path-mode ray queue (RT_BIN_MODE in rt_kernels.hip decides a ray's bin)
 #endif
-static const int kQRegion = (RT_NBINS + 2) * kQStride;  // one queue's counters: bin lengths + 2 chunk tickets
+static const int kQRegion = (RT_NBINS + 4) * kQStride;  // one queue's counters: bin lengths + 2 chunk tickets +
+                                                        // shadow-queue length and its chunk ticket
 static const int kBlockThreads = 256;  // threads per block of every kernel
 #ifndef RT_CLUSTER_TRIS
 #define RT_CLUSTER_TRIS 2
@@ -183,6 +184,10 @@ struct PathIO {
     int fused;  // simple scenes: the closest-hit traversal runs inside the shade kernel (no hit records)
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
     int* ticket;  // dynamic chunk counter (zeroed before the launch) or nullptr: static grid-stride
+    // shadow queue (multi-level octrees): the shade kernel appends NEE shadow rays {o, tMax}, {d, slot} and their
+    // pending contribution instead of tracing them inline; k_path_shadow traces them.  shO == nullptr: inline.
+    float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
+    int *shCount = nullptr, *shTicket = nullptr;
 };
 
 struct PathFilmIO {
@@ -222,6 +227,8 @@ hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, c
                                  const ShadeRefIO& io, unsigned long long* ctr);
 hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
                           const ShadeRefIO& sio, const RecordIO& io);
+hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, const DevScene& sc, const PathIO& io,
+                              unsigned long long* ctr);
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
                              unsigned long long* ctr);

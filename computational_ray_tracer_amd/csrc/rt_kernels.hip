@@ -482,13 +482,13 @@ __device__ __forceinline__ T ldconst(const T* p, int i) {
 #endif                       // way; the stack's registers cost occupancy or spills under the 4-wave budgets below:
                              // CFG3 144 -> 135 (bit 0), CFG4 111 -> 87 (bit 1) Msamples/s (A/B): off
 static constexpr int kDfsDepth = 16;
-#if RT_DFS_ANYHIT
+#if 1  // DFS any-hit is compiled in; callers pick it per instantiation (DFS template flag)
 __shared__ unsigned g_dfs[kDfsDepth * kBlock];
 #endif
 template <int KZ>
 __device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, V3 d, float tMax,
                                              unsigned long long& nn, unsigned long long& nt) {
-#if RT_DFS_ANYHIT
+#if 1
     const V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
     const TriRay R = make_triray<KZ>(o, d);
     const int2* __restrict__ lr = sc.leafRange[set];
@@ -753,7 +753,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         }
         return best;
     }
-#if RT_DFS_ANYHIT
+#if 1
     if constexpr (ANYHIT && DFS) {
         if (sc.depth <= kDfsDepth)  // the upload's octree depth; deeper trees keep the BFS FIFO below
             return occluded_dfs<KZ>(sc, set, o, d, tMax, nn, nt) ? 0 : -1;  // any-hit: 0 = occluded
@@ -1245,6 +1245,18 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
             for (int i = 0; i < 8; ++i) s_ld[i * kBlock + threadIdx.x] = Ld[i];
         }
 #endif
+        if constexpr (QCAP != 1) {  // shadow queue: the ray and its pending contribution go to k_path_shadow
+            if (io.shO) {
+                int sp = WAVE ? wave_append(io.shCount, wantShadow) : block_append(io.shCount, wantShadow, lds);
+                if (wantShadow) {
+                    io.shO[sp] = make_float4(so.x, so.y, so.z, stmax);
+                    io.shD[sp] = make_float4(sd.x, sd.y, sd.z, __int_as_float(slot));
+                    io.shLA[sp] = make_float4(Ld[0], Ld[1], Ld[2], Ld[3]);
+                    io.shLB[sp] = make_float4(Ld[4], Ld[5], Ld[6], Ld[7]);
+                    wantShadow = false;  // at depth 0 L is written as zero below; the shadow kernel adds to it
+                }
+            }
+        }
         // NEE shadow ray, traced inline (any hit, fixed tMax) after the bounce state is written, so only the
         // pending contribution Ld stays live across the traversal.  No shadow queue in HBM.
         if (wantShadow) {
@@ -1290,6 +1302,50 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
         count_add(ctr, C_HITS, tnh);
         count_add(ctr, C_RAYS, tnr);
     }
+}
+
+
+// Shadow-queue tracer (multi-level octrees, simple path scenes): the NEE shadow rays k_path_shade appended, traced
+// with no path state live (full occupancy; DFS: depth-first any-hit, exact for a fixed tMax, §6).  An unoccluded
+// ray adds its contribution to L exactly as the inline code would: per slot one shadow ray per bounce, launched
+// between this bounce's shade and the next one's, so every L sees its additions in the same order.
+#ifndef RT_SHADOW_WAVES
+#define RT_SHADOW_WAVES 0  // >0: amdgpu_waves_per_eu floor for k_path_shadow
+#endif
+#if RT_SHADOW_WAVES > 0
+#define RT_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES)))
+#else
+#define RT_SHADOW_ATTR
+#endif
+template <int QCAP, bool DFS>
+__global__ void __launch_bounds__(kBlock) RT_SHADOW_ATTR k_path_shadow(DevScene sc, PathIO io, unsigned long long* ctr) {
+    const int n = *io.shCount;
+    unsigned long long snn = 0, snt = 0, nsh = 0;
+    __shared__ int s_tk;
+    WaveChunks chunks(io.shTicket);
+    for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
+    for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
+        int k = base + chunks.lane;
+        if (k >= n) continue;
+        float4 o4 = io.shO[k], d4 = io.shD[k];
+        float b0, b1, b2, t;
+        int hit = traverse_any<QCAP, true, DFS>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), o4.w, b0, b1, b2,
+                                                t, snn, snt);
+        ++nsh;
+        if (hit < 0) {
+            int slot = __float_as_int(d4.w);
+            float4 la = io.shLA[k], lb = io.shLB[k];
+            const float Ld[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
+            float L[8];
+            load8(io.LA, io.LB, slot, L);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) L[i] += Ld[i];
+            store8(io.LA, io.LB, slot, L);
+        }
+    }
+    count_add(ctr, C_SNODES, snn);
+    count_add(ctr, C_STRIS, snt);
+    count_add(ctr, C_SHADOW, nsh);
 }
 
 // ------------------------------------------------------------------- path mode, general scenes (§8 a21/a22)
@@ -1744,6 +1800,29 @@ hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, c
 hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
                           const ShadeRefIO& sio, const RecordIO& io) {
     hipLaunchKernelGGL(k_records, dim3(grid_for(io.n, 0)), dim3(kBlock), 0, st, sc, sp, film, sio, io);
+    return hipGetLastError();
+}
+
+hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, const DevScene& sc, const PathIO& io,
+                              unsigned long long* ctr) {
+    int gb = grid > 0 ? grid : 1;
+    if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
+    dim3 b(kBlock);
+#define RT_SHADOW_CASE(Q)                                                                                        \
+    case Q:                                                                                                      \
+        if (dfs)                                                                                                 \
+            hipLaunchKernelGGL((k_path_shadow<Q, true>), dim3(resident_grid(k_path_shadow<Q, true>, gb, grid)), b, \
+                               0, st, sc, io, ctr);                                                              \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_path_shadow<Q, false>), dim3(resident_grid(k_path_shadow<Q, false>, gb, grid)), \
+                               b, 0, st, sc, io, ctr);                                                           \
+        break;
+    switch (qcap) {
+        RT_SHADOW_CASE(0)
+        RT_SHADOW_CASE(16)
+        default: return hipErrorInvalidValue;
+    }
+#undef RT_SHADOW_CASE
     return hipGetLastError();
 }
 
