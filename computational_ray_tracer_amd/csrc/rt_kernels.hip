@@ -1396,6 +1396,9 @@ __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const f
     count_add(ctr, C_SHADOW, ns);
 }
 
+#ifndef RT_FULL_NEE_PRE
+#define RT_FULL_NEE_PRE 0    // 1: mixed-scene NEE loop with fewer live registers (reloads beta, λ afterwards)
+#endif
 #ifndef RT_SHADE_FULL_WAVES
 #define RT_SHADE_FULL_WAVES 4  // >0: amdgpu_waves_per_eu floor for the mixed-scene shade kernel (register budget).
                                // 3: 246 -> 168 VGPRs (312 B/lane spill), 2 -> 3 waves/SIMD: CFG4 87 -> 98 Msamples/s;
@@ -1545,6 +1548,14 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(D
                             io.prevPdf[slot] = 0.f;
                         } else {  // Lambert: NEE per light, then a cosine-hemisphere bounce
                             V3 po = vadd(p, vmul(nrm, off));
+#if RT_FULL_NEE_PRE  // the light loop keeps beta·R/π and D65(λ) live instead of beta, R and λ (same products)
+                            float BR[8], D65l[8];
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) {
+                                BR[i] = beta[i] * (R[i] * InvPi);
+                                D65l[i] = dense_query(sp->D65, lam[i]);
+                            }
+#endif
                             for (int li = 0; li < sc.n_lights; ++li) {
                                 const DevLight Lt = ldconst(sc.lights, li);
                                 float u0, u1;
@@ -1599,13 +1610,24 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(D
                                     if (!scene_occluded<QCAP>(sc, po, wi, tmax, snn, snt)) {
 #pragma unroll
                                         for (int i = 0; i < 8; ++i) {
+#if RT_FULL_NEE_PRE
+                                            float Le = sc_le * D65l[i];
+                                            L[i] += (BR[i] * Le) * wgt;
+#else
                                             float Le = sc_le * dense_query(sp->D65, lam[i]);
                                             L[i] += ((beta[i] * (R[i] * InvPi)) * Le) * wgt;
+#endif
                                         }
                                     }
                                 }
                             }
                             store8(io.LA, io.LB, slot, L);
+#if RT_FULL_NEE_PRE  // beta and λ come back from memory, R is recomputed (bit-identical)
+                            load8(io.betaA, io.betaB, slot, beta);
+                            load8(io.lamA, io.lamB, slot, lam);
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.c0, mt.c1, mt.c2, lam[i]);
+#endif
                             // cosine-hemisphere bounce (Sampling.h:449-454), pbrt CoordinateSystem frame
                             float u0, u1, dx, dy;
                             sm.get2d(smp, u0, u1);
