@@ -1060,17 +1060,18 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 pio.prevPdf = w.prevPdf;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 pio.ticket = dyn ? qc_cur + (RT_NBINS + 1) * kQStride : nullptr;
+                ShadowQueueIO sqio{};
                 if (shq) {  // this queue's region holds the shadow-queue length and ticket (zeroed with it)
-                    pio.shO = w.shO; pio.shD = w.shD; pio.shLA = w.shLA; pio.shLB = w.shLB;
-                    pio.shCount = qc_cur + (RT_NBINS + 2) * kQStride;
-                    pio.shTicket = qc_cur + (RT_NBINS + 3) * kQStride;
+                    sqio.shO = w.shO; sqio.shD = w.shD; sqio.shLA = w.shLA; sqio.shLB = w.shLB;
+                    sqio.shCount = qc_cur + (RT_NBINS + 2) * kQStride;
+                    sqio.shTicket = qc_cur + (RT_NBINS + 3) * kQStride;
                 }
                 e0 = ev_start(c, s);
-                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr));
+                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio));
                 ev_mark(c, s, ST_SHADE, e0);
                 if (shq) {
                     e0 = ev_start(c, s);
-                    HIPCHK(c, launch_path_shadow(s, grid, c->dsc.qcap, c->shadow_dfs != 0, c->dsc, pio, c->d_ctr));
+                    HIPCHK(c, launch_path_shadow(s, grid, c->dsc.qcap, c->shadow_dfs != 0, c->dsc, pio, sqio, c->d_ctr));
                     ev_mark(c, s, ST_SHADOW, e0);
                 }
                 cur[l] = nxt;

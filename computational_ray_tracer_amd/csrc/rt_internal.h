@@ -184,8 +184,12 @@ struct PathIO {
     int fused;  // simple scenes: the closest-hit traversal runs inside the shade kernel (no hit records)
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
     int* ticket;  // dynamic chunk counter (zeroed before the launch) or nullptr: static grid-stride
-    // shadow queue (multi-level octrees): the shade kernel appends NEE shadow rays {o, tMax}, {d, slot} and their
-    // pending contribution instead of tracing them inline; k_path_shadow traces them.  shO == nullptr: inline.
+};
+
+// Shadow queue (multi-level octrees): the shade kernel appends NEE shadow rays {o, tMax}, {d, slot} and their
+// pending contribution instead of tracing them inline; k_path_shadow traces them.  shO == nullptr: inline.
+// A separate trailing kernel argument, so PathIO (and the single-leaf kernels' code) is unchanged.
+struct ShadowQueueIO {
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
     int *shCount = nullptr, *shTicket = nullptr;
 };
@@ -228,10 +232,10 @@ hipError_t launch_ref_shade_film(hipStream_t st, int grid, const DevScene& sc, c
 hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevFilm& film,
                           const ShadeRefIO& sio, const RecordIO& io);
 hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, const DevScene& sc, const PathIO& io,
-                              unsigned long long* ctr);
+                              const ShadowQueueIO& shq, unsigned long long* ctr);
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
-                             unsigned long long* ctr);
+                             unsigned long long* ctr, const ShadowQueueIO& shq = ShadowQueueIO{});
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr);
 hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* m_xyz_from_sensor,

@@ -1091,7 +1091,8 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 #endif
 template <int QCAP, bool FUSED>
 __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
-                                                       SampleIds ids, PathIO io, unsigned long long* ctr) {
+                                                       SampleIds ids, PathIO io, unsigned long long* ctr,
+                                                       ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[(RT_NBINS + 6) * (kBlock / 64) + RT_NBINS + 8];
 #if RT_LD_LDS
@@ -1246,13 +1247,13 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
         }
 #endif
         if constexpr (QCAP != 1) {  // shadow queue: the ray and its pending contribution go to k_path_shadow
-            if (io.shO) {
-                int sp = WAVE ? wave_append(io.shCount, wantShadow) : block_append(io.shCount, wantShadow, lds);
+            if (shq.shO) {
+                int sp = WAVE ? wave_append(shq.shCount, wantShadow) : block_append(shq.shCount, wantShadow, lds);
                 if (wantShadow) {
-                    io.shO[sp] = make_float4(so.x, so.y, so.z, stmax);
-                    io.shD[sp] = make_float4(sd.x, sd.y, sd.z, __int_as_float(slot));
-                    io.shLA[sp] = make_float4(Ld[0], Ld[1], Ld[2], Ld[3]);
-                    io.shLB[sp] = make_float4(Ld[4], Ld[5], Ld[6], Ld[7]);
+                    shq.shO[sp] = make_float4(so.x, so.y, so.z, stmax);
+                    shq.shD[sp] = make_float4(sd.x, sd.y, sd.z, __int_as_float(slot));
+                    shq.shLA[sp] = make_float4(Ld[0], Ld[1], Ld[2], Ld[3]);
+                    shq.shLB[sp] = make_float4(Ld[4], Ld[5], Ld[6], Ld[7]);
                     wantShadow = false;  // at depth 0 L is written as zero below; the shadow kernel adds to it
                 }
             }
@@ -1318,23 +1319,23 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
 #define RT_SHADOW_ATTR
 #endif
 template <int QCAP, bool DFS>
-__global__ void __launch_bounds__(kBlock) RT_SHADOW_ATTR k_path_shadow(DevScene sc, PathIO io, unsigned long long* ctr) {
-    const int n = *io.shCount;
+__global__ void __launch_bounds__(kBlock) RT_SHADOW_ATTR k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
+    const int n = *shq.shCount;
     unsigned long long snn = 0, snt = 0, nsh = 0;
     __shared__ int s_tk;
-    WaveChunks chunks(io.shTicket);
+    WaveChunks chunks(shq.shTicket);
     for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
     for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
         int k = base + chunks.lane;
         if (k >= n) continue;
-        float4 o4 = io.shO[k], d4 = io.shD[k];
+        float4 o4 = shq.shO[k], d4 = shq.shD[k];
         float b0, b1, b2, t;
         int hit = traverse_any<QCAP, true, DFS>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), o4.w, b0, b1, b2,
                                                 t, snn, snt);
         ++nsh;
         if (hit < 0) {
             int slot = __float_as_int(d4.w);
-            float4 la = io.shLA[k], lb = io.shLB[k];
+            float4 la = shq.shLA[k], lb = shq.shLB[k];
             const float Ld[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
             float L[8];
             load8(io.LA, io.LB, slot, L);
@@ -1826,7 +1827,7 @@ hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* 
 }
 
 hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, const DevScene& sc, const PathIO& io,
-                              unsigned long long* ctr) {
+                              const ShadowQueueIO& shq, unsigned long long* ctr) {
     int gb = grid > 0 ? grid : 1;
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
@@ -1834,10 +1835,10 @@ hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, cons
     case Q:                                                                                                      \
         if (dfs)                                                                                                 \
             hipLaunchKernelGGL((k_path_shadow<Q, true>), dim3(resident_grid(k_path_shadow<Q, true>, gb, grid)), b, \
-                               0, st, sc, io, ctr);                                                              \
+                               0, st, sc, io, shq, ctr);                                                              \
         else                                                                                                     \
             hipLaunchKernelGGL((k_path_shadow<Q, false>), dim3(resident_grid(k_path_shadow<Q, false>, gb, grid)), \
-                               b, 0, st, sc, io, ctr);                                                           \
+                               b, 0, st, sc, io, shq, ctr);                                                           \
         break;
     switch (qcap) {
         RT_SHADOW_CASE(0)
@@ -1850,7 +1851,7 @@ hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, cons
 
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
-                             unsigned long long* ctr) {
+                             unsigned long long* ctr, const ShadowQueueIO& shq) {
     int gb = grid > 0 ? grid : 1;
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
@@ -1861,10 +1862,10 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
                                sc, sp, smp, film, ids, io, ctr);                                                 \
         else if (io.fused)                                                                                       \
             hipLaunchKernelGGL((k_path_shade<Q, true>), dim3(resident_grid(k_path_shade<Q, true>, gb, grid)), b, 0, \
-                               st, sc, sp, smp, film, ids, io, ctr);                                             \
+                               st, sc, sp, smp, film, ids, io, ctr, shq);                                        \
         else                                                                                                     \
             hipLaunchKernelGGL((k_path_shade<Q, false>), dim3(resident_grid(k_path_shade<Q, false>, gb, grid)), b, \
-                               0, st, sc, sp, smp, film, ids, io, ctr);                                          \
+                               0, st, sc, sp, smp, film, ids, io, ctr, shq);                                     \
         break;
     switch (qcap) {
         RT_SHADE_CASE(0)

@@ -1,8 +1,8 @@
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
-TAG=r01h bash scripts/gpu_prof.sh || exit 1
+TAG=r01i CONFIGS="cfg3 cfg4 cfg5" bash scripts/gpu_round.sh || exit 1
 for c in cfg3 cfg4; do
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_${c}_r01h -o kt --output-format csv -- \
-    python3 bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/kt_${c}_r01h.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_${c}_r01i -o kt --output-format csv -- \
+    python3 bench.py --config $c --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/kt_${c}_r01i.log 2>&1
   rc=$?; echo "kt $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
-CFG=cfg3 bash scripts/gpu_pmc_cfg.sh > gpurun_out/pmc_cfg3_summary_r01h.txt 2>&1; rc=$?; echo "pmc cfg3 rc=$rc"; exit $rc
+exit 0
