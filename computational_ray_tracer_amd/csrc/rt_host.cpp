@@ -894,6 +894,10 @@ int check_ready(rt_ctx* c) {
 #define RT_CLUSTER_PAD_REL 1e-5f  // cluster-box inflation per unit of scene extent (see upload)
 #endif
 #ifndef RT_SORT_RAYS
+#ifndef RT_SORT_NOSYNC
+#define RT_SORT_NOSYNC 0  // 1: the sort reads the queue length on the device and sorts the whole capacity (no
+                          // per-bounce host sync); bit-exact, but CFG3 150.6 -> 149.6 (A/B): off
+#endif
 #define RT_SORT_RAYS 1  // multi-level octrees: coherence-sort each bounce's rays (rt_sort.hip)
 #endif
 #ifndef RT_SORT_SINGLE_LEAF
@@ -1028,10 +1032,15 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 // multi-level octrees: bounce rays regrouped by (octant, origin Morton code) before the trace
                 if (sort_rays && depth > 0) {
                     int nq = 0;
-                    HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, s));
-                    HIPCHK(c, hipStreamSynchronize(s));
                     SortRaysIO so{cO, cD, cS, w.sO, w.sD, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt,
                                   w.sTemp, w.sTempBytes, c->sort_lo, c->sort_scale};
+                    if (RT_SORT_NOSYNC) {  // no host round trip: sort the whole capacity, the device count pads
+                        nq = (int)nmax;
+                        so.count = qc_cur;
+                    } else {
+                        HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, s));
+                        HIPCHK(c, hipStreamSynchronize(s));
+                    }
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, nq, so));
                     ev_mark(c, s, ST_TRACE, e0);

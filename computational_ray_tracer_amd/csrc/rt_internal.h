@@ -220,6 +220,7 @@ struct SortRaysIO {
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp; size_t temp_bytes;
     float4 lo, scale;                                     // origin quantisation: (p - lo) * scale in [0, 512)
+    const int* count = nullptr;  // device queue length: sort all n slots, entries >= *count get the largest key
 };
 size_t sort_rays_temp_bytes(int nmax);
 hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io);

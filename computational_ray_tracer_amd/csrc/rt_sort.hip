@@ -33,8 +33,15 @@ __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every th
 
 __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const float4* __restrict__ o,
                                                               const float4* __restrict__ d, float4 lo, float4 scale,
-                                                              unsigned* __restrict__ keys, int* __restrict__ vals) {
+                                                              unsigned* __restrict__ keys, int* __restrict__ vals,
+                                                              const int* __restrict__ count) {
+    const int nv = count ? *count : n;  // slots past the device count sort last (largest key, stable)
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        if (k >= nv) {
+            keys[k] = 0xffffffffu;
+            vals[k] = k;
+            continue;
+        }
         float4 p = o[k], v = d[k];
         auto q = [](float x) {
             x = x < 0.f ? 0.f : (x > 511.f ? 511.f : x);
@@ -66,8 +73,10 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int*
                                                                 const float4* __restrict__ o,
                                                                 const float4* __restrict__ d,
                                                                 const int* __restrict__ slot, float4* __restrict__ so,
-                                                                float4* __restrict__ sd, int* __restrict__ ss) {
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+                                                                float4* __restrict__ sd, int* __restrict__ ss,
+                                                                const int* __restrict__ count) {
+    const int nv = count ? *count : n;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nv; k += gridDim.x * blockDim.x) {
         int j = perm[k];
         so[k] = o[j];
         sd[k] = d[j];
@@ -89,13 +98,13 @@ hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
     int g = (n + kBlockThreads - 1) / kBlockThreads;
     g = g < 8192 ? g : 8192;
     hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.o, io.d, io.lo, io.scale, io.keys,
-                       io.vals);
+                       io.vals, io.count);
     size_t bytes = io.temp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
                                                       kKeyBits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.o, io.d, io.slot, io.so,
-                       io.sd, io.ss);
+                       io.sd, io.ss, io.count);
     return hipGetLastError();
 }
 
