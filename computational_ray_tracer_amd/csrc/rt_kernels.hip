@@ -565,7 +565,7 @@ __device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, 
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
 // reference's node-level FIFO order exactly.  tMax shrinks on every accepted hit ("t < tMax": the first
 // hit found in BFS order wins ties), so hit ids, barycentrics and t are bit-identical to the reference's.
-template <int QCAP, bool ANYHIT, int KZ, bool DFS = false>
+template <int QCAP, bool ANYHIT, int KZ, bool DFS = false, bool PFA = false>
 __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0, float& rb1,
                                         float& rb2, float& rt, unsigned long long& nn, unsigned long long& nt) {
     V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -766,6 +766,9 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
 #ifndef RT_GROUP_FETCH
 #define RT_GROUP_FETCH 8  // child boxes loaded together per popped group (8, 4 or 2: register pressure vs MLP)
 #endif
+#ifndef RT_FULL_ANYHIT_PREFETCH
+#define RT_FULL_ANYHIT_PREFETCH 0  // 1: the mixed-scene shadow rays use the pipelined leaf loop too
+#endif
 #ifndef RT_LEAF_PREFETCH
 #define RT_LEAF_PREFETCH 1  // software-pipelined leaf loop (next triangle's 48 B in flight during a test): 1 closest-hit only, 2 all
 #endif
@@ -864,7 +867,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         // at most kLeafChunk triangles per phase: a lane in a big leaf (the CFG3 octree has leaves of up to 583
         // triangles) keeps the rest pending while the other lanes walk on to their next leaf
         int m = lc < kLeafChunk ? lc : kLeafChunk;
-        constexpr bool PF = RT_LEAF_PREFETCH == 2 || (RT_LEAF_PREFETCH == 1 && !ANYHIT);
+        constexpr bool PF = RT_LEAF_PREFETCH == 2 || (RT_LEAF_PREFETCH == 1 && (!ANYHIT || PFA));
         float4 nA, nB, nC;
         if constexpr (PF) { nA = tiles[3 * lf]; nB = tiles[3 * lf + 1]; nC = tiles[3 * lf + 2]; }
         for (int k = 0; k < m; ++k) {
@@ -900,17 +903,17 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
 
 // When every active lane of the wave has the same dominant ray axis (camera rays, kz-binned queues) the
 // watertight test's coordinate permutation is resolved at compile time; otherwise per lane.
-template <int QCAP, bool ANYHIT, bool DFS = false>
+template <int QCAP, bool ANYHIT, bool DFS = false, bool PFA = false>
 __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
                                             float& b2, float& t, unsigned long long& nn, unsigned long long& nt) {
 #if RT_KZ_SPECIALIZE
     int kz = dominant_axis(d);
     uint64_t act = __ballot(true);
-    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
 #endif
-    return traverse<QCAP, ANYHIT, -1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    return traverse<QCAP, ANYHIT, -1, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
 }
 
 #ifndef RT_TRACE_WAVES
@@ -1372,7 +1375,8 @@ template <int QCAP>
 __device__ __forceinline__ bool scene_occluded(const DevScene& sc, V3 o, V3 d, float tmax, unsigned long long& nn,
                                                unsigned long long& nt) {
     float b0, b1, b2, t;
-    if (traverse_any<QCAP, true, (RT_DFS_ANYHIT & 2) != 0>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0) return true;
+    if (traverse_any<QCAP, true, (RT_DFS_ANYHIT & 2) != 0, RT_FULL_ANYHIT_PREFETCH != 0>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0)
+        return true;
     for (int si = 0; si < sc.n_shapes; ++si) {
         DevShape sh = ldconst(sc.shapes, si);
         V3 ph;
