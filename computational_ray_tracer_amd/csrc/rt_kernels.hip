@@ -26,7 +26,10 @@ static constexpr int kBlock = kBlockThreads;
 #define RT_LEAF_CHUNK 32
 #endif
 static constexpr int kLeafChunk = RT_LEAF_CHUNK;  // triangles per leaf phase of the while-while traversal
-static constexpr int kLdsQ = 32;  // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
+#ifndef RT_LDS_FIFO
+#define RT_LDS_FIFO 32
+#endif
+static constexpr int kLdsQ = RT_LDS_FIFO;  // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
 __shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by every traversal call site
 
 #ifndef RT_COMPACT
