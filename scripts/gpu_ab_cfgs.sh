@@ -1,4 +1,7 @@
+#!/bin/bash
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
+# A/B of the kernel variants in computational_ray_tracer_amd/lib/variants/*.so over bench configs:
+#   CFGS="cornell cfg3 cfg4" [WITH_TESTS=1] bash scripts/gpu_ab_cfgs.sh
 if [ -n "$WITH_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_tmp.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu_tmp.log; [ $rc -ne 0 ] && exit $rc
