@@ -60,13 +60,6 @@ def kernel_rooflines(st, traffic):
         "k_path_shade": (st["ms_shade"], st["launches_shade"], 312 * st["rays"] + 32 * st["shadow_rays"],
                          32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"]),
     }
-    if st["launches_trace"] == 0 and st["rays"] > 0:
-        # fused bounce (simple scenes): k_path_shade also casts the bounce's closest-hit rays, so it carries
-        # both units of §8(d) work: 40 B per ray cast + 312 B per shaded bounce + 32 B per shadow ray
-        del ks["k_trace_closest"]
-        ks["k_path_shade"] = (st["ms_shade"], st["launches_shade"], (40 + 312) * st["rays"] + 32 * st["shadow_rays"],
-                              32 * (st["nodes_tested"] + st["shadow_nodes_tested"])
-                              + 40 * (st["tris_tested"] + st["shadow_tris_tested"]))
     res = {}
     for name, (ms, launches, stream_b, scene_b) in ks.items():
         launches = max(1, launches)
@@ -84,10 +77,13 @@ def kernel_rooflines(st, traffic):
 
 
 def cpu_baseline(cfg, seconds):
-    """Oracle (C++ restatement, `port`) on host threads, bounded sample: a horizontal band of full rows of
-    the same 1080p Cornell frame, 1 sample index, sized to ~`seconds` of CPU work."""
-    from oracle.oracle import OracleScene
-    threads = min(16, os.cpu_count() or 1)
+    """Oracle (C++ restatement, `port`) on every host thread (hardware_concurrency, as RayTracerTestApp.h:372-397
+    spawns), built -O3 -march=native on this host; bounded sample: a horizontal band of full rows of
+    the same frame, 1 sample index, sized to ~`seconds` of CPU work."""
+    from oracle import oracle
+    oracle.use_native()
+    OracleScene = oracle.OracleScene
+    threads = min(os.cpu_count() or 1, 512)  # the pool's per-box task limit is 1024
     o = OracleScene(cfg)
     W, H = cfg.film.res
     spp = cfg.sampler.spp()
@@ -121,11 +117,17 @@ def cpu_baseline(cfg, seconds):
                 break
     except OSError:
         pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {"value": round(ms, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "affinity_cpus": affinity,
             "single_thread": round(len(p1) * nidx / dt1 / 1e6, 4), "cpu_model": model,
+            "build": "g++ -O3 -march=native -ffp-contract=off (built on this host)",
             "sample": f"oracle C++ restatement (same octree BFS, watertight test, path integrator), {n} samples = "
-                      f"{rows} full rows of the {W}x{H} Cornell frame x sample indices 0..{nidx - 1}, "
-                      f"{threads} threads, {dt:.1f} s"}
+                      f"{rows} full rows of the {W}x{H} frame x sample indices 0..{nidx - 1}, "
+                      f"{threads} threads (os.cpu_count), {dt:.1f} s"}
 
 
 def main():

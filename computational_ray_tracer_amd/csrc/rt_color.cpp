@@ -9,6 +9,7 @@
 #include <cstring>
 #include <utility>
 
+#include "rt_guard.h"
 #include "../../include/rtmi355x.h"
 #include "../data/spectra_data.h"
 
@@ -139,7 +140,7 @@ void gauss_newton(const double* rgb, double* c) {
 
 extern "C" {
 
-int rt_rgb_to_sigmoid(const float* rgb, float* coeffs) {
+static int impl_rt_rgb_to_sigmoid(const float* rgb, float* coeffs) {
     if (!rgb || !coeffs) return RT_E_ARG;
     for (int k = 0; k < 3; ++k)
         if (!(rgb[k] >= 0.f && rgb[k] <= 1.f)) return RT_E_ARG;
@@ -165,6 +166,15 @@ int rt_rgb_to_sigmoid(const float* rgb, float* coeffs) {
     double A = c[0] * s * s, B = c[1] * s - 2 * c[0] * kLmin * s * s, C = c[2] - c[1] * kLmin * s + c[0] * kLmin * kLmin * s * s;
     coeffs[0] = (float)A; coeffs[1] = (float)B; coeffs[2] = (float)C;
     return RT_OK;
+}
+
+}  // extern "C"
+
+// ---- the exception firewall around every entry point (rt_guard.h)
+using rtmi::guarded;
+extern "C" {
+int rt_rgb_to_sigmoid(const float* rgb, float* coeffs) {
+    return guarded([&] { return impl_rt_rgb_to_sigmoid(rgb, coeffs); }, [](const std::string&) {});
 }
 
 }  // extern "C"

@@ -30,20 +30,9 @@ RT_DEV void sincos_det(float x, float& s, float& c) {
     s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
     c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
 }
-#ifdef RT_PROFILE_FLOAT_WARPS  // timing experiments only: float atanh/cosh (results differ from the oracle)
-RT_DEV float f_atanh(float x) { return atanhf(x); }
-RT_DEV float f_cosh(float x) { return coshf(x); }
-#else
 // (float)atanh((double)x) / (float)cosh((double)x) as the oracle computes them: the fast double evaluation of
 // rt_mathf.h, and the full-precision library call only when that result is within 2^-46 of a float rounding midpoint
 // (about 1 input in 3.4e7; tools/verify_warps.cpp checks every input float of the warps against glibc)
-#ifndef RT_FAST_WARPS
-#define RT_FAST_WARPS 1
-#endif
-#if !RT_FAST_WARPS
-RT_DEV float f_atanh(float x) { return (float)atanh((double)x); }
-RT_DEV float f_cosh(float x) { return (float)cosh((double)x); }
-#else
 RT_DEV float f_atanh(float x) {
     double r = rtm::atanh_fast(x);
     float f = (float)r;
@@ -56,8 +45,6 @@ RT_DEV float f_cosh(float x) {
     if (rtm::near_midpoint(r, f)) f = (float)cosh((double)x);
     return f;
 }
-#endif
-#endif
 
 // helpers.h:50-54
 RT_DEV float gamma_n(int n) {

@@ -23,12 +23,7 @@
 #include "../../include/rtmi355x.h"
 #include "../data/spectra_data.h"
 #include "../data/sensor_data.h"
-#ifndef RT_LANES
-#define RT_LANES 2  // path-mode batches in flight on separate streams (4 lanes with 4 Mi-sample batches: 1150)
-#endif
-#ifndef RT_DYN_SCHED
-#define RT_DYN_SCHED 2  // path-mode trace / shade launches take chunks from a ticket counter (BlockChunks):
-#endif                  // 0 never, 1 always, 2 multi-level octrees only (single-leaf scenes: equal per-ray cost)
+#include "rt_guard.h"
 #include "rt_internal.h"
 
 using namespace rtmi;
@@ -37,6 +32,9 @@ namespace {
 
 constexpr int kRingMax = 1 << 16;  // largest BFS group FIFO (HBM ring per resident thread, 4 B per entry)
 constexpr int kMaxLights = 64;
+constexpr int kDefaultLanes = 2;   // path-mode batches in flight on separate streams (RTMI_LANES overrides; 1 lane:
+                                   // Cornell 1217, 2 lanes 1500, 3-4 lanes with 4 Mi-sample batches ~1150 Msamples/s)
+constexpr float kClusterPadRel = 1e-5f;  // cluster-box inflation per unit of scene extent (see scene upload)
 
 // ------------------------------------------------------------------------------ host float math
 // glm operation order, float, -ffp-contract=off (same contract as the device code)
@@ -440,8 +438,7 @@ struct Work {
     int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
     float* prevPdf = nullptr;
     uint4* rng = nullptr;
-    int* d_qcount = nullptr;   // queue q: bin b length at [q * kQRegion + b * kQStride], trace / shade chunk tickets
-                               // at [q * kQRegion + (RT_NBINS, RT_NBINS + 1) * kQStride] (separate cache lines)
+    int* d_qcount = nullptr;   // queue q's counters at [q * kQRegion + kQLen / kQTraceTicket / ...] (rt_internal.h)
     // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers
     float4 *sO = nullptr, *sD = nullptr;
     int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;
@@ -451,17 +448,14 @@ struct Work {
     // shadow queue (multi-level octrees): {o, tMax}, {d, slot}, pending contribution (2 x float4)
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
     size_t shCap = 0;
+    // BFS FIFO overflow ring of the multi-level traversal (qcap 0): one per lane, because the lanes' kernels run
+    // concurrently and index the ring by their own global thread id
+    int* ring = nullptr;
+    size_t ring_cap = 0;   // ints
     hipStream_t stream = nullptr;  // lanes >= 1: own stream (lane 0 runs on the caller's stream)
     hipEvent_t film_done = nullptr;
-    hipEvent_t trace_done = nullptr;  // RTMI_PAIR: the lanes' closest-hit launches take turns
 };
 
-#ifndef RT_SHADOW_QUEUE
-#define RT_SHADOW_QUEUE 0  // multi-level octrees: NEE shadow rays traced by k_path_shadow (RTMI_SHADOW_QUEUE)
-#endif
-#ifndef RT_SHADOW_DFS
-#define RT_SHADOW_DFS 1    // k_path_shadow: depth-first any-hit (RTMI_SHADOW_DFS)
-#endif
 struct rt_ctx {
     // coherence sort of path queues (multi-level octrees): scene quantisation of the sort key
     float4 sort_lo{}, sort_scale{};
@@ -495,11 +489,12 @@ struct rt_ctx {
     int* d_work = nullptr;
     // batch workspaces, one per lane (path mode runs kLanes batches concurrently on separate streams)
     Work ws[kLanes];
-    int lanes = RT_LANES;  // batches in flight in path mode (RTMI_LANES overrides)
-    int grid_div = 1;      // persistent-grid divisor with lanes > 1 (RTMI_GRID_DIV overrides; A/B: 1 beats 2)
-    int shadow_queue = RT_SHADOW_QUEUE;  // multi-level simple path scenes: NEE rays traced by k_path_shadow
-    int shadow_dfs = RT_SHADOW_DFS;      // k_path_shadow walks depth-first (exact any-hit, §6)
-    int pair = 0;          // RTMI_PAIR=1: closest-hit launches of the lanes never overlap (trace pairs with shade)
+    int lanes = kDefaultLanes;  // batches in flight in path mode (RTMI_LANES overrides)
+    // multi-level simple path scenes: NEE rays traced by k_path_shadow (RTMI_SHADOW_QUEUE=1; measured slower than
+    // the inline any-hit, kept as a parity-tested option), depth first (RTMI_SHADOW_DFS, exact any-hit, §6)
+    int shadow_queue = 0;
+    int shadow_dfs = 1;
+    hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
     size_t batch_samples = 0;  // samples in flight per batch (0: 8 Mi path / 16 Mi reference; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
@@ -533,6 +528,9 @@ struct rt_ctx {
 
 namespace {
 
+void set_error(rt_ctx* c, const std::string& msg) {
+    if (c) c->err = msg;
+}
 int fail(rt_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
     return code;
@@ -612,11 +610,38 @@ void free_workspace(Work& w) {
     w.prevPdf = nullptr;
     w.cap = 0;
 }
+void free_ring(Work& w) {
+    if (w.ring) hipFree(w.ring);
+    w.ring = nullptr;
+    w.ring_cap = 0;
+}
 void free_workspace(rt_ctx* c) {
-    for (Work& w : c->ws) free_workspace(w);
+    for (Work& w : c->ws) {
+        free_workspace(w);
+        free_ring(w);
+    }
+}
+
+// this lane's BFS overflow ring (multi-level octrees whose FIFO bound exceeds the register variants)
+int ensure_ring(rt_ctx* c, Work& w) {
+    if (c->dsc.qcap != 0) return RT_OK;
+    const size_t need = (size_t)c->dsc.ring_threads * (size_t)(c->dsc.ring_mask + 1);
+    if (w.ring_cap < need) {
+        free_ring(w);
+        HIPCHK(c, dalloc(&w.ring, need));
+        w.ring_cap = need;
+    }
+    return RT_OK;
+}
+// the scene as a lane's kernels see it: its own overflow ring
+DevScene lane_scene(const rt_ctx* c, const Work& w) {
+    DevScene d = c->dsc;
+    d.ring = w.ring;
+    return d;
 }
 
 int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
+    int rc;
     if (!w.d_qcount) HIPCHK(c, dalloc(&w.d_qcount, 2 * kQRegion));
     if (&w != &c->ws[0]) {
         if (!w.stream) HIPCHK(c, hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
@@ -624,11 +649,11 @@ int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
     } else if (!w.film_done) {
         HIPCHK(c, hipEventCreateWithFlags(&w.film_done, hipEventDisableTiming));
     }
-    if (!w.trace_done) HIPCHK(c, hipEventCreateWithFlags(&w.trace_done, hipEventDisableTiming));
+    if ((rc = ensure_ring(c, w))) return rc;
     if (w.cap >= n && (!path || w.betaA)) return RT_OK;
     free_workspace(w);
-    // path mode: queue arrays hold 2 ping-pong queues x RT_NBINS bins of n entries each
-    size_t nq = path ? 2 * RT_NBINS * n : n;
+    // path mode: queue arrays hold 2 ping-pong queues of n entries each
+    size_t nq = path ? 2 * n : n;
     HIPCHK(c, dalloc(&w.rayO, nq)); HIPCHK(c, dalloc(&w.rayD, nq)); HIPCHK(c, dalloc(&w.slot, nq));
     HIPCHK(c, dalloc(&w.lamA, n)); HIPCHK(c, dalloc(&w.lamB, n));
     HIPCHK(c, dalloc(&w.pdfA, n)); HIPCHK(c, dalloc(&w.pdfB, n));
@@ -890,33 +915,31 @@ int check_ready(rt_ctx* c) {
     return RT_OK;
 }
 
-#ifndef RT_CLUSTER_PAD_REL
-#define RT_CLUSTER_PAD_REL 1e-5f  // cluster-box inflation per unit of scene extent (see upload)
-#endif
-#ifndef RT_SORT_RAYS
-#ifndef RT_SORT_NOSYNC
-#define RT_SORT_NOSYNC 0  // 1: the sort reads the queue length on the device and sorts the whole capacity (no
-                          // per-bounce host sync); bit-exact, but CFG3 150.6 -> 149.6 (A/B): off
-#endif
-#define RT_SORT_RAYS 1  // multi-level octrees: coherence-sort each bounce's rays (rt_sort.hip)
-#endif
-#ifndef RT_SORT_SINGLE_LEAF
-#define RT_SORT_SINGLE_LEAF 0  // also sort on single-leaf scenes (the Cornell box)
-#endif
-#ifndef RT_KZ_BINS_HOST
-#define RT_KZ_BINS_HOST 0  // must match the kernels' RT_KZ_BINS: the sort reads bin 0 as one contiguous queue
-#endif
-#ifndef RT_LEAN_GENERATE
-#define RT_LEAN_GENERATE 1
-#endif
-#ifndef RT_FUSED_BOUNCE
-#define RT_FUSED_BOUNCE 0
-#endif
+// Calls on a context may use different streams (rt_render_pass on the context's stream, rt_render_pass_device on the
+// caller's, the debug entry points): each waits for the previous call's work, which shares the lane-0 buffers.
+int order_after_previous(rt_ctx* c, hipStream_t st) {
+    if (!c->done) HIPCHK(c, hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+    else HIPCHK(c, hipStreamWaitEvent(st, c->done, 0));
+    return RT_OK;
+}
+int mark_done(rt_ctx* c, hipStream_t st) {
+    HIPCHK(c, hipEventRecord(c->done, st));
+    return RT_OK;
+}
 
+int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st);
 // one render pass over [ib, ie) into the device film
 int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     int rc = check_ready(c);
     if (rc) return rc;
+    if ((rc = order_after_previous(c, st))) return rc;
+    rc = render_device_body(c, ib, ie, film, st);
+    int rc2 = mark_done(c, st);
+    return rc ? rc : rc2;
+}
+
+int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
+    int rc;
     if (ib < 0 || ie < ib) return fail(c, RT_E_ARG, "invalid index range");
     if ((rc = ensure_sobol(c))) return rc;
     DevSampler smp = dev_sampler(c);
@@ -946,9 +969,9 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
             hipEvent_t e0 = ev_start(c, st);
             HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, st, ST_GEN, e0);
-            TraceIO tio{w.rayO, w.rayD, nullptr, nS, 0, c->cull ? 1 : 0, w.hitB, w.hitPrim};
+            TraceIO tio{w.rayO, w.rayD, nullptr, nS, c->cull ? 1 : 0, w.hitB, w.hitPrim};
             e0 = ev_start(c, st);
-            HIPCHK(c, launch_trace_closest(st, 0, c->dsc.qcap, c->dsc, tio, c->d_ctr));
+            HIPCHK(c, launch_trace_closest(st, 0, c->dsc.qcap, lane_scene(c, w), tio, c->d_ctr));
             ev_mark(c, st, ST_TRACE, e0);
             ShadeRefIO sio = shade_ref_io(c);
             sio.work_pixels = c->d_work; sio.n_pixels = c->n_work; sio.n_index = nIdx;
@@ -966,33 +989,33 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
     // after batch k-1's), so every pixel still adds its sample indices in increasing order.
     const int nbatch = (ie - ib + B - 1) / B;
     const int lanes = std::max(1, std::min(std::min(c->lanes, kLanes), nbatch));
-    const bool sort_rays = RT_SORT_RAYS && (c->dsc.qcap != 1 || RT_SORT_SINGLE_LEAF) && !RT_KZ_BINS_HOST;
+    // multi-level octrees: coherence-sort each bounce's rays (rt_sort.hip); on the single-leaf Cornell box the sort
+    // costs more than it saves (1110 -> 720 Msamples/s)
+    const bool sort_rays = c->dsc.qcap != 1;
     for (int l = 0; l < lanes; ++l) {
         if ((rc = ensure_workspace(c, c->ws[l], nmax, true))) return rc;
         if (sort_rays && (rc = ensure_sort_workspace(c, c->ws[l], nmax))) return rc;
     }
     // Cornell-like single-leaf scenes cost the same per ray: static chunks on a resident grid beat tickets there
     // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
-    const bool dyn = RT_DYN_SCHED == 1 || (RT_DYN_SCHED == 2 && c->dsc.qcap != 1);
-    const bool lean = RT_LEAN_GENERATE && !c->dsc.full;  // simple path kernel: no β / L / pdf streams
-    const bool fused = RT_FUSED_BOUNCE && !c->dsc.full;  // simple scenes: trace inside the shade kernel
+    const bool dyn = c->dsc.qcap != 1;
+    const bool lean = !c->dsc.full;  // simple path kernel: no β / L / pdf streams (+4.5 %)
     // multi-level simple scenes: NEE shadow rays queued and traced by their own kernel (no path state live)
-    const bool shq = c->shadow_queue && c->dsc.qcap != 1 && !c->dsc.full && !fused;
+    const bool shq = c->shadow_queue && c->dsc.qcap != 1 && !c->dsc.full;
     if (shq)
         for (int l = 0; l < lanes; ++l)
             if ((rc = ensure_shadow_workspace(c, c->ws[l], nmax))) return rc;
     // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
     // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
     // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
-    const int grid = lanes > 1 ? std::max(8, c->grid / std::max(1, c->grid_div)) : c->grid;
+    const int grid = c->grid;
     auto lstream = [&](int l) { return l == 0 ? st : c->ws[l].stream; };
     if (lanes > 1) {  // lanes 1.. start after the caller's earlier work on st
         HIPCHK(c, hipEventRecord(c->ws[0].film_done, st));
         for (int l = 1; l < lanes; ++l) HIPCHK(c, hipStreamWaitEvent(c->ws[l].stream, c->ws[0].film_done, 0));
     }
-    const size_t qs = RT_NBINS * nmax;  // one queue = RT_NBINS bins of nmax
-    int last_film = -1;                 // lane of the most recent film launch
-    int last_trace = -1;                // lane of the most recent closest-hit launch (RTMI_PAIR)
+    const size_t qs = nmax;  // one queue
+    int last_film = -1;      // lane of the most recent film launch
     for (int g0 = ib; g0 < ie; g0 += B * lanes) {
         int nIdx[kLanes] = {0}, cur[kLanes] = {0};
         for (int l = 0; l < lanes; ++l) {
@@ -1009,7 +1032,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, s, ST_GEN, e0);
-            // camera rays fill bin 0 of queue 0 (flat order); the other bins start empty
+            // camera rays fill queue 0
             HIPCHK(c, hipMemsetAsync(w.d_qcount, 0, 2 * kQRegion * sizeof(int), s));
             HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)w.d_qcount, nS, 1, s));
         }
@@ -1026,7 +1049,7 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                 const int* cS = w.slot + (size_t)cur[l] * qs;
                 int* qc_cur = w.d_qcount + kQRegion * cur[l];
                 int* qc_nxt = w.d_qcount + kQRegion * nxt;
-                // the next queue's bin lengths and the chunk tickets its trace and shade launches will use
+                // the next queue's length and the chunk tickets its trace and shade launches will use
                 HIPCHK(c, hipMemsetAsync(qc_nxt, 0, kQRegion * sizeof(int), s));
                 hipEvent_t e0;
                 // multi-level octrees: bounce rays regrouped by (octant, origin Morton code) before the trace
@@ -1034,53 +1057,42 @@ int render_device(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) {
                     int nq = 0;
                     SortRaysIO so{cO, cD, cS, w.sO, w.sD, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt,
                                   w.sTemp, w.sTempBytes, c->sort_lo, c->sort_scale};
-                    if (RT_SORT_NOSYNC) {  // no host round trip: sort the whole capacity, the device count pads
-                        nq = (int)nmax;
-                        so.count = qc_cur;
-                    } else {
-                        HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, s));
-                        HIPCHK(c, hipStreamSynchronize(s));
-                    }
+                    HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, s));
+                    HIPCHK(c, hipStreamSynchronize(s));
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, nq, so));
                     ev_mark(c, s, ST_TRACE, e0);
                     cO = w.sO; cD = w.sD; cS = w.sS;
                 }
-                if (!fused) {
-                    TraceIO tio{cO, cD, qc_cur, 0, nmax, 0, w.hitB, w.hitPrim,
-                                dyn ? qc_cur + RT_NBINS * kQStride : nullptr};
-                    if (c->pair && last_trace >= 0 && last_trace != l)
-                        HIPCHK(c, hipStreamWaitEvent(s, c->ws[last_trace].trace_done, 0));
-                    e0 = ev_start(c, s);
-                    HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, c->dsc, tio, c->d_ctr));
-                    ev_mark(c, s, ST_TRACE, e0);
-                    if (c->pair) { HIPCHK(c, hipEventRecord(w.trace_done, s)); last_trace = l; }
-                }
+                const DevScene dsl = lane_scene(c, w);
+                TraceIO tio{cO, cD, qc_cur, 0, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr};
+                e0 = ev_start(c, s);
+                HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
+                ev_mark(c, s, ST_TRACE, e0);
                 PathIO pio{};
-                pio.fused = fused ? 1 : 0;
                 pio.lean = lean ? 1 : 0;
                 pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = qc_cur;
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
                 pio.nO = w.rayO + (size_t)nxt * qs; pio.nD = w.rayD + (size_t)nxt * qs;
-                pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt; pio.bstride = nmax;
+                pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt;
                 pio.rng = w.rng; pio.dim = w.dim; pio.betaA = w.betaA; pio.betaB = w.betaB;
                 pio.LA = w.LA; pio.LB = w.LB;
                 pio.lamA = w.lamA; pio.lamB = w.lamB; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.prevPdf = w.prevPdf;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
-                pio.ticket = dyn ? qc_cur + (RT_NBINS + 1) * kQStride : nullptr;
+                pio.ticket = dyn ? qc_cur + kQShadeTicket : nullptr;
                 ShadowQueueIO sqio{};
                 if (shq) {  // this queue's region holds the shadow-queue length and ticket (zeroed with it)
                     sqio.shO = w.shO; sqio.shD = w.shD; sqio.shLA = w.shLA; sqio.shLB = w.shLB;
-                    sqio.shCount = qc_cur + (RT_NBINS + 2) * kQStride;
-                    sqio.shTicket = qc_cur + (RT_NBINS + 3) * kQStride;
+                    sqio.shCount = qc_cur + kQShadowLen;
+                    sqio.shTicket = qc_cur + kQShadowTicket;
                 }
                 e0 = ev_start(c, s);
-                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, c->dsc, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio));
+                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio));
                 ev_mark(c, s, ST_SHADE, e0);
                 if (shq) {
                     e0 = ev_start(c, s);
-                    HIPCHK(c, launch_path_shadow(s, grid, c->dsc.qcap, c->shadow_dfs != 0, c->dsc, pio, sqio, c->d_ctr));
+                    HIPCHK(c, launch_path_shadow(s, grid, c->dsc.qcap, c->shadow_dfs != 0, dsl, pio, sqio, c->d_ctr));
                     ev_mark(c, s, ST_SHADOW, e0);
                 }
                 cur[l] = nxt;
@@ -1361,8 +1373,6 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     }
     c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
     if (const char* e = std::getenv("RTMI_LANES")) c->lanes = std::max(1, std::min(kLanes, std::atoi(e)));
-    if (const char* e = std::getenv("RTMI_GRID_DIV")) c->grid_div = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("RTMI_PAIR")) c->pair = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SHADOW_QUEUE")) c->shadow_queue = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SHADOW_DFS")) c->shadow_dfs = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
@@ -1409,13 +1419,13 @@ static void destroy_one(rt_ctx* c) {
     for (Work& w : c->ws) {
         if (w.d_qcount) hipFree(w.d_qcount);
         if (w.film_done) hipEventDestroy(w.film_done);
-        if (w.trace_done) hipEventDestroy(w.trace_done);
         if (w.stream) hipStreamDestroy(w.stream);
     }
     void* ptrs[] = {c->d_spec, c->d_ctr, c->d_resolve, c->d_work, c->d_film, c->d_cdf, c->d_sobol_mats,
                     c->d_sobol_fwd};
     for (void* p : ptrs)
         if (p) hipFree(p);
+    if (c->done) hipEventDestroy(c->done);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1726,7 +1736,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         const std::vector<float4>* tl[2] = {&tiles0, &tiles1};
         const auto& R = ob.nodes[0];
         float ext = std::max(std::max(R.mx.x - R.mn.x, R.mx.y - R.mn.y), R.mx.z - R.mn.z);
-        float pad = RT_CLUSTER_PAD_REL * ext + 1e-3f;
+        float pad = kClusterPadRel * ext + 1e-3f;
         c->dsc.cl_guard = make_float4(.5f * (R.mn.x + R.mx.x), .5f * (R.mn.y + R.mx.y), .5f * (R.mn.z + R.mx.z),
                                       64.f * ext * ext);
         for (int st = 0; st < 2; ++st) {
@@ -1742,19 +1752,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
                 clus[st].push_back(make_float4(mn[0] - pad, mn[1] - pad, mn[2] - pad, 0.f));
                 clus[st].push_back(make_float4(mx[0] + pad, mx[1] + pad, mx[2] + pad, 0.f));
             }
-            // then the boxes of runs of kSuperClusters clusters (the union of their inflated boxes)
-            int nc = (int)clus[st].size() / 2;
-            for (int s0 = 0; kSuperClusters > 0 && s0 < nc; s0 += kSuperClusters) {
-                float4 a = clus[st][2 * s0], b = clus[st][2 * s0 + 1];
-                for (int k = s0 + 1; k < std::min(nc, s0 + kSuperClusters); ++k) {
-                    const float4 &ka = clus[st][2 * k], &kb = clus[st][2 * k + 1];
-                    a.x = std::min(a.x, ka.x); a.y = std::min(a.y, ka.y); a.z = std::min(a.z, ka.z);
-                    b.x = std::max(b.x, kb.x); b.y = std::max(b.y, kb.y); b.z = std::max(b.z, kb.z);
-                }
-                clus[st].push_back(a);
-                clus[st].push_back(b);
-            }
-            c->dsc.n_clusters[st] = nc;
+            c->dsc.n_clusters[st] = (int)clus[st].size() / 2;
             // fan pairs: tile k+1 = (a, c, d) after tile k = (a, b, c), bit for bit (_quad / OBJ fan triangulation)
             unsigned long long fp = 0;
             for (int k = 0; k + 1 < std::min(nt_leaf, 64); k += 2) {
@@ -1784,16 +1782,11 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     c->scene_full = full;
     d.qcap = qcap;
     d.depth = nn < (1 << 24) ? maxd : 1 << 30;  // DFS stack entries hold 24-bit group ids
-    if (qcap == 0) {
+    if (qcap == 0) {  // each lane allocates its ring of ring_threads x rs ints (ensure_ring)
         int rs = 1;
         while (rs < bound) rs <<= 1;
         d.ring_threads = c->grid * kBlockThreads;
         d.ring_mask = rs - 1;
-        void* pr = nullptr;
-        if (hipMalloc(&pr, (size_t)d.ring_threads * rs * sizeof(int)) != hipSuccess)
-            return fail(c, RT_E_OOM, "BFS ring of " + std::to_string(rs) + " groups per thread");
-        c->scene_allocs.push_back(pr);
-        d.ring = (int*)pr;
     }
     d.n_lights = s->n_lights;
     if (s->n_lights >= 1) d.light0 = lights[0];
@@ -1855,7 +1848,7 @@ const char* rt_sensor_name(int sensor) {
     return rtdata::camera_names[sensor - 1];
 }
 
-int rt_film_matrices(rt_ctx* c, float* xyz_from_sensor9, float* rgb_from_xyz9) {
+static int impl_rt_film_matrices(rt_ctx* c, float* xyz_from_sensor9, float* rgb_from_xyz9) {
     if (!c || !xyz_from_sensor9 || !rgb_from_xyz9) return RT_E_ARG;
     std::memcpy(xyz_from_sensor9, c->resolveA, 36);
     std::memcpy(rgb_from_xyz9, c->resolveB, 36);
@@ -1887,14 +1880,14 @@ static int set_shard_one(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
     return RT_OK;
 }
 
-int rt_render_pass_device(rt_ctx* c, int ib, int ie, void* d_film, void* stream) {
+static int impl_rt_render_pass_device(rt_ctx* c, int ib, int ie, void* d_film, void* stream) {
     if (!c || !d_film) return RT_E_ARG;
     hipSetDevice(c->device);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return render_multi(c, ib, ie, (float4*)d_film, st);
 }
 
-int rt_render_pass(rt_ctx* c, int ib, int ie, rt_pixel* film) {
+static int impl_rt_render_pass(rt_ctx* c, int ib, int ie, rt_pixel* film) {
     if (!c || !film) return RT_E_ARG;
     int rc = check_ready(c);
     if (rc) return rc;
@@ -1935,8 +1928,8 @@ int film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out, int srgb) {
 }
 }  // namespace
 
-int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 0); }
-int rt_film_resolve_srgb(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 1); }
+static int impl_rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 0); }
+static int impl_rt_film_resolve_srgb(rt_ctx* c, const rt_pixel* film, uint8_t* out) { return film_resolve(c, film, out, 1); }
 
 static int get_stats_one(rt_ctx* c, rt_stats* out) {
     if (!c || !out) return RT_E_ARG;
@@ -1969,14 +1962,14 @@ static int reset_stats_one(rt_ctx* c) {
     return RT_OK;
 }
 
-int rt_octree_get_info(rt_ctx* c, rt_octree_info* out) {
+static int impl_rt_octree_get_info(rt_ctx* c, rt_octree_info* out) {
     if (!c || !out) return RT_E_ARG;
     if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
     *out = c->info;
     return RT_OK;
 }
 
-int rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32_t* leaf_first, int32_t* leaf_count, int32_t* refs) {
+static int impl_rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32_t* leaf_first, int32_t* leaf_count, int32_t* refs) {
     if (!c) return RT_E_ARG;
     if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
     if (bounds) std::memcpy(bounds, c->h_bounds.data(), c->h_bounds.size() * 4);
@@ -1987,7 +1980,7 @@ int rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32_t* leaf_fir
     return RT_OK;
 }
 
-int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_cull, int32_t* prim, float* bt) {
+static int impl_rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_cull, int32_t* prim, float* bt) {
     if (!c || n < 0 || (n && (!ro || !rd || !prim || !bt))) return RT_E_ARG;
     if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
     if (n == 0) return RT_OK;
@@ -1999,13 +1992,15 @@ int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_c
     }
     float4 *dO = nullptr, *dD = nullptr, *dH = nullptr;
     int* dP = nullptr;
-    int rc = RT_OK;
-    if (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dH, n) || dalloc(&dP, n)) rc = fail(c, RT_E_OOM, "debug trace buffers");
+    int rc = ensure_ring(c, c->ws[0]);
+    if (!rc) rc = order_after_previous(c, c->stream);
+    if (!rc && (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dH, n) || dalloc(&dP, n)))
+        rc = fail(c, RT_E_OOM, "debug trace buffers");
     if (!rc) {
-        TraceIO io{dO, dD, nullptr, n, 0, (use_cull && c->cull) ? 1 : 0, dH, dP};
+        TraceIO io{dO, dD, nullptr, n, (use_cull && c->cull) ? 1 : 0, dH, dP};
         if (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-            launch_trace_closest(c->stream, 0, c->dsc.qcap, c->dsc, io, c->d_ctr) != hipSuccess ||
+            launch_trace_closest(c->stream, 0, c->dsc.qcap, lane_scene(c, c->ws[0]), io, c->d_ctr) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(prim, dP, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(bt, dH, 16 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(c, RT_E_HIP, std::string("debug trace: ") + hipGetErrorString(hipGetLastError()));
@@ -2017,7 +2012,7 @@ int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_c
     return rc;
 }
 
-int rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float* rd, const float* tmax, int32_t* occluded) {
+static int impl_rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float* rd, const float* tmax, int32_t* occluded) {
     if (!c || n < 0 || (n && (!ro || !rd || !tmax || !occluded))) return RT_E_ARG;
     if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
     if (n == 0) return RT_OK;
@@ -2029,12 +2024,13 @@ int rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float* rd, const 
     }
     float4 *dO = nullptr, *dD = nullptr;
     int* dP = nullptr;
-    int rc = RT_OK;
-    if (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dP, n)) rc = fail(c, RT_E_OOM, "debug occlusion buffers");
+    int rc = ensure_ring(c, c->ws[0]);
+    if (!rc) rc = order_after_previous(c, c->stream);
+    if (!rc && (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dP, n))) rc = fail(c, RT_E_OOM, "debug occlusion buffers");
     if (!rc &&
         (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
          hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-         launch_occluded(c->stream, c->dsc.qcap, c->dsc, n, dO, dD, dP, c->d_ctr) != hipSuccess ||
+         launch_occluded(c->stream, c->dsc.qcap, lane_scene(c, c->ws[0]), n, dO, dD, dP, c->d_ctr) != hipSuccess ||
          hipStreamSynchronize(c->stream) != hipSuccess ||
          hipMemcpy(occluded, dP, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
         rc = fail(c, RT_E_HIP, std::string("debug occlusion: ") + hipGetErrorString(hipGetLastError()));
@@ -2042,7 +2038,7 @@ int rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float* rd, const 
     return rc;
 }
 
-int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out) {
+static int impl_rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out) {
     int rc = check_ready(c);
     if (rc) return rc;
     if (n < 0 || (n && (!pixel_ids || !indices || !out))) return fail(c, RT_E_ARG, "bad arguments");
@@ -2058,6 +2054,7 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
     }
     hipSetDevice(c->device);
     if ((rc = ensure_workspace(c, (size_t)n, false))) return rc;
+    if ((rc = order_after_previous(c, c->stream))) return rc;
     int *dp = nullptr, *di = nullptr;
     float* dout = nullptr;
     static_assert(sizeof(rt_sample_record) == 39 * 4, "record layout");
@@ -2069,13 +2066,13 @@ int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* 
         GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].slot, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA, c->ws[0].pdfB, nullptr, nullptr, nullptr,
                   nullptr, nullptr, nullptr, nullptr};
         DevFilm fd = dev_film(c);
-        TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, nullptr, n, 0, c->cull ? 1 : 0, c->ws[0].hitB, c->ws[0].hitPrim};
+        TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, nullptr, n, c->cull ? 1 : 0, c->ws[0].hitB, c->ws[0].hitPrim};
         ShadeRefIO sio = shade_ref_io(c);
         sio.rayD = c->ws[0].rayD; sio.lamA = c->ws[0].lamA; sio.lamB = c->ws[0].lamB; sio.pdfA = c->ws[0].pdfA; sio.pdfB = c->ws[0].pdfB;
         sio.hitB = c->ws[0].hitB; sio.hitPrim = c->ws[0].hitPrim;
         RecordIO rio{n, c->ws[0].rayO, c->ws[0].rayD, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA, c->ws[0].pdfB, c->ws[0].hitB, c->ws[0].hitPrim, dout, 39};
         if (launch_generate(c->stream, 0, n, ids, dev_camera(c->cam), smp, fd, go) != hipSuccess ||
-            launch_trace_closest(c->stream, 0, c->dsc.qcap, c->dsc, tio, c->d_ctr) != hipSuccess ||
+            launch_trace_closest(c->stream, 0, c->dsc.qcap, lane_scene(c, c->ws[0]), tio, c->d_ctr) != hipSuccess ||
             launch_records(c->stream, c->dsc, c->d_spec, fd, sio, rio) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(out, dout, sizeof(rt_sample_record) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
@@ -2098,7 +2095,7 @@ static int on_all(rt_ctx* c, F f) {
     return rc;
 }
 
-int rt_create(const rt_options* opt, rt_ctx** out) {
+static int impl_rt_create(const rt_options* opt, rt_ctx** out) {
     if (!out) return RT_E_ARG;
     *out = nullptr;
     int nd = opt ? opt->n_devices : 0;
@@ -2135,7 +2132,7 @@ int rt_create(const rt_options* opt, rt_ctx** out) {
     return RT_OK;
 }
 
-void rt_destroy(rt_ctx* c) {
+static void impl_rt_destroy(rt_ctx* c) {
     if (!c) return;
     for (size_t j = 0; j < c->peers.size(); ++j) {
         rt_ctx* p = c->peers[j];
@@ -2155,34 +2152,34 @@ void rt_destroy(rt_ctx* c) {
     destroy_one(c);
 }
 
-int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
+static int impl_rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
     if (!c) return RT_E_ARG;
     return on_all(c, [&](rt_ctx* x) { return scene_upload_one(x, s); });
 }
-int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
+static int impl_rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
     if (!c) return RT_E_ARG;
     return on_all(c, [&](rt_ctx* x) { return camera_set_one(x, d); });
 }
-int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
+static int impl_rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
     if (!c) return RT_E_ARG;
     return on_all(c, [&](rt_ctx* x) { return sampler_set_one(x, d); });
 }
-int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
+static int impl_rt_film_set(rt_ctx* c, const rt_film_desc* d) {
     if (!c) return RT_E_ARG;
     return on_all(c, [&](rt_ctx* x) { return film_set_one(x, d); });
 }
-int rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
+static int impl_rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
     if (!c) return RT_E_ARG;
     return on_all(c, [&](rt_ctx* x) { return integrator_set_one(x, d); });
 }
-int rt_reset_stats(rt_ctx* c) {
+static int impl_rt_reset_stats(rt_ctx* c) {
     if (!c) return RT_E_ARG;
     return on_all(c, [&](rt_ctx* x) { return reset_stats_one(x); });
 }
 // the caller's shard (tile t, t % n_shards == shard_id) is split over the context's D devices: device k takes the
 // tiles with (t / n_shards) % D == k, i.e. shard (n_shards·D, shard_id + n_shards·k) of the frame
 // counters and kernel times summed over the context's devices
-int rt_get_stats(rt_ctx* c, rt_stats* out) {
+static int impl_rt_get_stats(rt_ctx* c, rt_stats* out) {
     if (!c || !out) return RT_E_ARG;
     rt_stats sum{};
     int rc = on_all(c, [&](rt_ctx* x) -> int {
@@ -2201,7 +2198,7 @@ int rt_get_stats(rt_ctx* c, rt_stats* out) {
     return rc;
 }
 
-int rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
+static int impl_rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
     if (!c || n_shards <= 0 || shard_id < 0 || shard_id >= n_shards)
         return c ? fail(c, RT_E_ARG, "invalid shard") : RT_E_ARG;
     const int D = 1 + (int)c->peers.size();
@@ -2210,6 +2207,71 @@ int rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
         if ((rc = set_shard_one(c->peers[j], tile_size, n_shards * D, shard_id + n_shards * (int)(j + 1))))
             fail(c, rc, c->peers[j]->err);
     return rc;
+}
+
+}  // extern "C"
+
+// ---- the exception firewall around every entry point (rt_guard.h)
+extern "C" {
+int rt_film_matrices(rt_ctx* c, float* xyz_from_sensor9, float* rgb_from_xyz9) {
+    return guarded([&] { return impl_rt_film_matrices(c, xyz_from_sensor9, rgb_from_xyz9); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_render_pass_device(rt_ctx* c, int ib, int ie, void* d_film, void* stream) {
+    return guarded([&] { return impl_rt_render_pass_device(c, ib, ie, d_film, stream); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_render_pass(rt_ctx* c, int ib, int ie, rt_pixel* film) {
+    return guarded([&] { return impl_rt_render_pass(c, ib, ie, film); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_film_resolve(rt_ctx* c, const rt_pixel* film, uint8_t* out) {
+    return guarded([&] { return impl_rt_film_resolve(c, film, out); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_film_resolve_srgb(rt_ctx* c, const rt_pixel* film, uint8_t* out) {
+    return guarded([&] { return impl_rt_film_resolve_srgb(c, film, out); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_octree_get_info(rt_ctx* c, rt_octree_info* out) {
+    return guarded([&] { return impl_rt_octree_get_info(c, out); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32_t* leaf_first, int32_t* leaf_count, int32_t* refs) {
+    return guarded([&] { return impl_rt_octree_export(c, bounds, child, leaf_first, leaf_count, refs); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_cull, int32_t* prim, float* bt) {
+    return guarded([&] { return impl_rt_debug_trace(c, n, ro, rd, use_cull, prim, bt); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float* rd, const float* tmax, int32_t* occluded) {
+    return guarded([&] { return impl_rt_debug_occluded(c, n, ro, rd, tmax, occluded); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out) {
+    return guarded([&] { return impl_rt_debug_samples(c, n, pixel_ids, indices, out); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_create(const rt_options* opt, rt_ctx** out) {
+    return guarded([&] { return impl_rt_create(opt, out); }, [&](const std::string& m) { set_error(nullptr, m); });
+}
+int rt_scene_upload(rt_ctx* c, const rt_scene_desc* s) {
+    return guarded([&] { return impl_rt_scene_upload(c, s); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_camera_set(rt_ctx* c, const rt_camera_desc* d) {
+    return guarded([&] { return impl_rt_camera_set(c, d); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_sampler_set(rt_ctx* c, const rt_sampler_desc* d) {
+    return guarded([&] { return impl_rt_sampler_set(c, d); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_film_set(rt_ctx* c, const rt_film_desc* d) {
+    return guarded([&] { return impl_rt_film_set(c, d); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_integrator_set(rt_ctx* c, const rt_integrator_desc* d) {
+    return guarded([&] { return impl_rt_integrator_set(c, d); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_reset_stats(rt_ctx* c) {
+    return guarded([&] { return impl_rt_reset_stats(c); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_get_stats(rt_ctx* c, rt_stats* out) {
+    return guarded([&] { return impl_rt_get_stats(c, out); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
+    return guarded([&] { return impl_rt_set_shard(c, tile_size, n_shards, shard_id); }, [&](const std::string& m) { set_error(c, m); });
+}
+void rt_destroy(rt_ctx* c) {
+    guarded([&] { impl_rt_destroy(c); return 0; }, [](const std::string&) {});
 }
 
 }  // extern "C"

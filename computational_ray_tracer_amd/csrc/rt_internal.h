@@ -135,29 +135,18 @@ struct GenOut {
     int lean;  // simple path kernel: no β = 1 / L = 0 / pdf stores (depth 0 and the film kernel derive them)
 };
 
-// Ray queues.  A path-mode queue is split into 3 bins by the rays' dominant axis (the watertight test's
-// kz, Shapes.h:1145): bin b holds rays at ray[b*bstride + i], i < count[b*cstride].  Entries are addressed by
-// a flat index k over bin 0, then 1, then 2, so every wave but the two at bin seams sees one kz.
+// Queue counters of a path-mode ray queue: one 256-B line each (never two hot atomics in one cache line), in a
+// region of kQRegion ints: the queue length, the chunk tickets of its trace and shade launches, and the shadow-queue
+// length and chunk ticket (multi-level octrees).
 static const int kQStride = 64;
-#ifndef RT_NBINS
-#define RT_NBINS 3  // bins of a path-mode ray queue (RT_BIN_MODE in rt_kernels.hip decides a ray's bin)
-#endif
-static const int kQRegion = (RT_NBINS + 4) * kQStride;  // one queue's counters: bin lengths + 2 chunk tickets +
-                                                        // shadow-queue length and its chunk ticket
+enum { kQLen = 0, kQTraceTicket = 1 * kQStride, kQShadeTicket = 2 * kQStride, kQShadowLen = 3 * kQStride,
+       kQShadowTicket = 4 * kQStride, kQRegion = 5 * kQStride };
 static const int kBlockThreads = 256;  // threads per block of every kernel
-#ifndef RT_CLUSTER_TRIS
-#define RT_CLUSTER_TRIS 2
-#endif
-#ifndef RT_SUPER_CLUSTERS
-#define RT_SUPER_CLUSTERS 0
-#endif
-static const int kSuperClusters = RT_SUPER_CLUSTERS;  // clusters per super-cluster box (0: none)
-static const int kClusterTris = RT_CLUSTER_TRIS;  // leaf tiles per culling cluster (single-leaf scenes)  // ints between queue counters: 256 B apart, never in one cache line
+static const int kClusterTris = 2;     // leaf tiles per culling cluster (single-leaf scenes; 4 or 6: -2 %)
 
 struct TraceIO {
     const float4* rayO; const float4* rayD;
-    const int* count; int n;  // binned queue lengths in device memory (count != nullptr) or one fixed n
-    size_t bstride;           // elements between bins
+    const int* count; int n;  // queue length in device memory (count != nullptr) or a fixed n
     int set;                  // tile set: 0 = all triangles, 1 = back-face culled
     float4* hitB;             // (b0, b1, b2, t) at flat index
     int* hitPrim;
@@ -173,15 +162,13 @@ struct ShadeRefIO {
 };
 
 struct PathIO {
-    const float4* rayO; const float4* rayD; const int* slot; const int* count;  // current binned queue
-    const float4* hitB; const int* hitPrim;                                     // at flat index
-    float4* nO; float4* nD; int* nSlot; int* nCount;                            // next binned queue
-    size_t bstride;
+    const float4* rayO; const float4* rayD; const int* slot; const int* count;  // current queue
+    const float4* hitB; const int* hitPrim;                                     // at queue position
+    float4* nO; float4* nD; int* nSlot; int* nCount;                            // next queue
     uint4* rng; int* dim; float4* betaA; float4* betaB; float4* LA; float4* LB;
     const float4* lamA; const float4* lamB; float4* pdfA; float4* pdfB;  // pdf: TerminateSecondary writes it
     float* prevPdf;                                                       // pdf of the last diffuse bounce
     int depth, max_depth;
-    int fused;  // simple scenes: the closest-hit traversal runs inside the shade kernel (no hit records)
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
     int* ticket;  // dynamic chunk counter (zeroed before the launch) or nullptr: static grid-stride
 };

@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "rt_guard.h"
 #include "../../include/rtmi355x.h"
 
 namespace {
@@ -75,7 +76,8 @@ void chunk(std::vector<unsigned char>& out, const char* type, const std::vector<
 
 extern "C" {
 
-int rt_load_obj(const char* path, rt_mesh** out) {
+static void impl_rt_mesh_free(rt_mesh* m);
+static int impl_rt_load_obj(const char* path, rt_mesh** out) {
     if (!path || !out) return RT_E_ARG;
     *out = nullptr;
     FILE* f = std::fopen(path, "rb");
@@ -118,12 +120,17 @@ int rt_load_obj(const char* path, rt_mesh** out) {
     if (!ok || corners.empty()) return RT_E_ARG;
     size_t nc = corners.size();
     rt_mesh* m = (rt_mesh*)std::calloc(1, sizeof(rt_mesh));
+    if (!m) return RT_E_OOM;
     m->n_vertices = (int)nc;
     m->n_triangles = (int)(nc / 3);
     m->positions = (float*)std::malloc(sizeof(float) * 3 * nc);
     m->normals = (float*)std::malloc(sizeof(float) * 3 * nc);
     m->texcoords = (float*)std::malloc(sizeof(float) * 2 * nc);
     m->indices = (uint32_t*)std::malloc(sizeof(uint32_t) * nc);
+    if (!m->positions || !m->normals || !m->texcoords || !m->indices) {
+        impl_rt_mesh_free(m);
+        return RT_E_OOM;
+    }
     for (size_t t = 0; t < nc / 3; ++t) {
         const V3f& a = v[corners[3 * t].v];
         const V3f& b = v[corners[3 * t + 1].v];
@@ -149,13 +156,13 @@ int rt_load_obj(const char* path, rt_mesh** out) {
     return RT_OK;
 }
 
-void rt_mesh_free(rt_mesh* m) {
+static void impl_rt_mesh_free(rt_mesh* m) {
     if (!m) return;
     std::free(m->positions); std::free(m->normals); std::free(m->texcoords); std::free(m->indices);
     std::free(m);
 }
 
-int rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_y) {
+static int impl_rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_y) {
     if (!path || !rgb || w <= 0 || h <= 0) return RT_E_ARG;
     std::string p(path);
     bool png = p.size() >= 4 && (p.compare(p.size() - 4, 4, ".png") == 0 || p.compare(p.size() - 4, 4, ".PNG") == 0);
@@ -197,6 +204,21 @@ int rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_
     size_t wrote = std::fwrite(out.data(), 1, out.size(), f);
     std::fclose(f);
     return wrote == out.size() ? RT_OK : RT_E_ARG;
+}
+
+}  // extern "C"
+
+// ---- the exception firewall around every entry point (rt_guard.h)
+using rtmi::guarded;
+extern "C" {
+int rt_load_obj(const char* path, rt_mesh** out) {
+    return guarded([&] { return impl_rt_load_obj(path, out); }, [](const std::string&) {});
+}
+int rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_y) {
+    return guarded([&] { return impl_rt_image_write(path, w, h, rgb, flip_y); }, [](const std::string&) {});
+}
+void rt_mesh_free(rt_mesh* m) {
+    guarded([&] { impl_rt_mesh_free(m); return 0; }, [](const std::string&) {});
 }
 
 }  // extern "C"

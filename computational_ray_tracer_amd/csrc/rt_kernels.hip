@@ -22,38 +22,21 @@
 namespace rtmi {
 
 static constexpr int kBlock = kBlockThreads;
-#ifndef RT_LEAF_CHUNK
-#define RT_LEAF_CHUNK 32
-#endif
-static constexpr int kLeafChunk = RT_LEAF_CHUNK;  // triangles per leaf phase of the while-while traversal
-#ifndef RT_LDS_FIFO
-#define RT_LDS_FIFO 32
-#endif
-static constexpr int kLdsQ = RT_LDS_FIFO;  // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
+// Tuning constants (A/B measurements of the alternatives: DESIGN.md §4 levers table)
+static constexpr int kLeafChunk = 32;  // triangles per leaf phase of the while-while traversal (16: -5 %, 64: +-0)
+static constexpr int kLdsQ = 32;       // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
+static constexpr int kTriUnroll = 4;   // triangles per scalar-cache batch in single-leaf traversal
 __shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by every traversal call site
 
-#ifndef RT_COMPACT
-#define RT_COMPACT 5         // single-leaf scenes: pass 1 on a compacted list of (ray, cluster) pairs whose box test
-#endif                       // passes (wave ballot + prefix into LDS), instead of every cluster for every lane.
-                             // 1: every ray; 2: waves without a shared dominant axis; 3: as 2 plus every shadow ray;
-                             // 4: closest-hit rays only; 5: closest-hit waves without a shared dominant axis
-#ifndef RT_FAST_CLUSTER
-#define RT_FAST_CLUSTER 1    // cluster culling boxes use cluster_hit (v_min/v_max slab reduction) instead of box_hit
-#endif
-#if RT_FAST_CLUSTER
-#define CL_HIT cluster_hit
-#else
-#define CL_HIT box_hit
-#endif
+// Single-leaf scenes, closest-hit waves without a shared dominant axis (bounce rays): pass 1 runs on a compacted list
+// of (ray, cluster) pairs whose box test passes (wave ballot + prefix into LDS) instead of every cluster for every lane.
 static constexpr int kCompactMaxClusters = 24;  // clusters of a compacted single leaf (Cornell: 18)
 struct CompactWave {
     float4 ra[64], rb[64];                     // staged TriRay per lane: (Sx, Sy, Sz, ox), (oy, oz, kz, -)
     unsigned long long cand[64];               // pass-1 candidate mask per lane (leaf order bit k = tile k)
     unsigned short pair[64 * kCompactMaxClusters];  // lane | cluster << 6
 };
-#if RT_COMPACT
 __shared__ CompactWave g_cmp[kBlock / 64];  // one per wave, shared by every single-leaf traversal call site
-#endif
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -63,34 +46,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-#ifndef RT_TRI_UNROLL
-#define RT_TRI_UNROLL 4      // triangles per scalar-cache batch in single-leaf traversal
-#endif
-#ifndef RT_TWO_PASS
-#define RT_TWO_PASS 1        // single-leaf scenes: cheap candidate pass over all triangles, full test on survivors
-#endif
-#ifndef RT_CLUSTER
-#define RT_CLUSTER 3         // single-leaf scenes: skip triangle runs whose conservative box no lane of a wave
-#endif                       // reaches.  1: shadow rays only; 2: every ray; 3: shadow rays and closest-hit waves
-                             // whose rays share a dominant axis (camera rays)
-#ifndef RT_FAN_PAIRS
-#define RT_FAN_PAIRS 1       // single-leaf scenes: fan-triangulated quads transform their 4 vertices once per ray
-#endif
-#ifndef RT_TRACE_KZSORT
-#define RT_TRACE_KZSORT 0    // closest-hit launches regroup each block's rays by dominant axis in LDS
-#endif
-#ifndef RT_RAY_SORT
-#define RT_RAY_SORT 0        // path queues: each block writes its rays ordered by major direction (6 keys)
-#endif
-#ifndef RT_KZ_BINS
-#define RT_KZ_BINS 0         // 1: path-mode ray queues split into dominant-axis bins (Cornell A/B: trace -7%, shade +23%)
-#endif
-#ifndef RT_BIN_MODE
-#define RT_BIN_MODE (RT_KZ_BINS ? 1 : 0)  // next-queue bin of a bounce ray: 0 one bin, 1 dominant axis,
-#endif                                    // 2 origin triangle pair (prim >> 1, mod RT_NBINS)
-#ifndef RT_KZ_SPECIALIZE
-#define RT_KZ_SPECIALIZE 1   // compile-time watertight permutation for dominant-axis-uniform waves
-#endif
 
 // -------------------------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -129,127 +84,16 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     return pred ? base + rank : -1;
 }
 
-// Block-aggregated append into an RT_NBINS-bin queue (bin -1 = nothing to append): one atomicAdd per non-empty bin
-// per block.  Returns the element position (bin region + index) or -1.
-__device__ __forceinline__ long block_append_bin(int* counters, int bin, size_t bstride, int* lds) {
-    constexpr int NW = kBlock / 64;
-    int wave = threadIdx.x >> 6;
-    int rank = 0;
-#pragma unroll
-    for (int b = 0; b < RT_NBINS; ++b) {
-        uint64_t mask = __ballot(bin == b);
-        if (bin == b)
-            rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        if (lane_id() == 0) lds[b * NW + wave] = __popcll(mask);
-    }
-    __syncthreads();
-    for (int b = threadIdx.x; b < RT_NBINS; b += kBlock) {
-        int tot = 0;
-        for (int w = 0; w < NW; ++w) { int cw = lds[b * NW + w]; lds[b * NW + w] = tot; tot += cw; }
-        lds[RT_NBINS * NW + b] = tot ? atomicAdd(counters + b * kQStride, tot) : 0;
-    }
-    __syncthreads();
-    long pos = -1;
-    if (bin >= 0) pos = (long)bin * (long)bstride + lds[RT_NBINS * NW + bin] + lds[bin * NW + wave] + rank;
-    __syncthreads();
-    return pos;
-}
-// Block-aggregated append into one contiguous chunk ordered by key (0..K-1; -1 = nothing to append), one atomicAdd
-// per block: the block's rays leave grouped by key, so the next launch's waves are direction-coherent.
-template <int K>
-__device__ __forceinline__ long block_append_sorted(int* counter, int key, int* lds) {
-    constexpr int NW = kBlock / 64;
-    int wave = threadIdx.x >> 6;
-    int rank = 0;
-#pragma unroll
-    for (int b = 0; b < K; ++b) {
-        uint64_t mask = __ballot(key == b);
-        if (key == b)
-            rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        if (lane_id() == 0) lds[b * NW + wave] = __popcll(mask);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int i = 0; i < K * NW; ++i) { int cw = lds[i]; lds[i] = tot; tot += cw; }
-        lds[K * NW] = tot ? atomicAdd(counter, tot) : 0;
-    }
-    __syncthreads();
-    long pos = key >= 0 ? (long)lds[K * NW] + lds[key * NW + wave] + rank : -1;
-    __syncthreads();
-    return pos;
-}
-// Position of this thread's item when the block's items are ordered by key (0..K-1), stable within a key.
-// Every thread of the block must call it.
-template <int K>
-__device__ __forceinline__ int block_rank(int key, int* lds) {
-    constexpr int NW = kBlock / 64;
-    int wave = threadIdx.x >> 6;
-    int rank = 0;
-#pragma unroll
-    for (int b = 0; b < K; ++b) {
-        uint64_t mask = __ballot(key == b);
-        if (key == b)
-            rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-        if (lane_id() == 0) lds[b * NW + wave] = __popcll(mask);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int i = 0; i < K * NW; ++i) { int cw = lds[i]; lds[i] = tot; tot += cw; }
-    }
-    __syncthreads();
-    int pos = lds[key * NW + wave] + rank;
-    __syncthreads();
-    return pos;
-}
-// major direction of a ray: dominant axis and its sign (6 keys)
-__device__ __forceinline__ int major_dir(V3 d) {
-    int k = dominant_axis(d);
-    float c = k == 0 ? d.x : (k == 1 ? d.y : d.z);
-    return 2 * k + (c < 0 ? 1 : 0);
-}
-// Lengths of the RT_NBINS bins of a queue (device counters, kQStride apart) and flat index -> element position
-// (bin b occupies [b * bstride, b * bstride + c[b])).
-struct QueueCounts {
-    int c[RT_NBINS];
-    int n;
-    __device__ __forceinline__ QueueCounts(const int* count, int fixed_n) {
-#pragma unroll
-        for (int b = 0; b < RT_NBINS; ++b) c[b] = count ? count[b * kQStride] : (b == 0 ? fixed_n : 0);
-        n = 0;
-#pragma unroll
-        for (int b = 0; b < RT_NBINS; ++b) n += c[b];
-    }
-    __device__ __forceinline__ size_t pos(int k, size_t bstride) const {
-        size_t off = 0;
-#pragma unroll
-        for (int b = 0; b < RT_NBINS - 1; ++b) {
-            bool later = k >= c[b];
-            k = later ? k - c[b] : k;
-            off = later ? off + bstride : off;
-            if (!later) return off + (size_t)k;
-        }
-        return off + (size_t)k;
-    }
-};
-
 // Work distribution of the persistent queue kernels.  With a ticket counter (zeroed before the launch) a block takes
-// the next chunk of RT_DYN_ITEMS x kBlock items whenever it finishes one, so blocks whose rays are expensive
-// (incoherent bounces, big leaves) do not hold back the launch; the next ticket is requested while the current chunk
-// runs.  Without one, block b takes chunks b, b + grid, ... of RT_STATIC_ITEMS x kBlock items.  Every thread of the
-// block must call next().
-#ifndef RT_DYN_ITEMS
-#define RT_DYN_ITEMS 1     // items per thread per ticket (dynamic chunks)
-#endif
-#ifndef RT_STATIC_ITEMS
-#define RT_STATIC_ITEMS 2  // items per thread per chunk without a ticket
-#endif
+// the next chunk of kBlock items whenever it finishes one, so blocks whose rays are expensive (incoherent bounces,
+// big leaves) do not hold back the launch; the next ticket is requested while the current chunk runs.  Without one,
+// block b takes chunks b, b + grid, ... of kStaticItems x kBlock items.  Every thread of the block must call next().
+static constexpr int kStaticItems = 2;  // items per thread per chunk without a ticket (single-leaf scenes)
 struct BlockChunks {
     int* ticket;
     int pref, it, size, lane, step;
     __device__ __forceinline__ explicit BlockChunks(int* t)
-        : ticket(t), pref(0), it(0), size((t ? RT_DYN_ITEMS : RT_STATIC_ITEMS) * kBlock), lane(threadIdx.x),
+        : ticket(t), pref(0), it(0), size((t ? 1 : kStaticItems) * kBlock), lane(threadIdx.x),
           step(kBlock) {
         if (ticket && threadIdx.x == 0) pref = atomicAdd(ticket, 1);
     }
@@ -264,23 +108,17 @@ struct BlockChunks {
     }
 };
 
-// The same for kernels without block-level synchronisation: with a ticket each wave takes RT_WAVE_ITEMS x 64 items
-// per ticket; without one the block-static mapping of BlockChunks.
-#ifndef RT_SHADE_WAVE
-#define RT_SHADE_WAVE 1    // multi-level octrees: shade kernels take per-wave tickets and append per wave
-#endif
-#ifndef RT_WAVE_ITEMS
-#define RT_WAVE_ITEMS 1
-#endif
+// The same for kernels without block-level synchronisation: with a ticket each wave takes 64 items per ticket
+// (128: CFG3 -5 %); without one the block-static mapping of BlockChunks.
 struct WaveChunks {
     int* ticket;
     int pref, it, size, lane, step;
     __device__ __forceinline__ explicit WaveChunks(int* t) : ticket(t), pref(0), it(0) {
         if (ticket) {
-            size = RT_WAVE_ITEMS * 64; lane = lane_id(); step = 64;
+            size = 64; lane = lane_id(); step = 64;
             if (lane == 0) pref = atomicAdd(ticket, 1);
         } else {
-            size = RT_STATIC_ITEMS * kBlock; lane = threadIdx.x; step = kBlock;
+            size = kStaticItems * kBlock; lane = threadIdx.x; step = kBlock;
         }
     }
     __device__ __forceinline__ int next() {
@@ -291,42 +129,18 @@ struct WaveChunks {
     }
     __device__ __forceinline__ int next(int*) { return next(); }
 };
-// Append to the next binned queue: per wave (one atomic per bin per wave; WaveChunks kernels, no block-level
-// synchronisation) or per block (block_append_bin).
+// Append to the next queue: per wave (WaveChunks kernels, no block-level synchronisation) or per block.
 template <bool WAVE>
-__device__ __forceinline__ long queue_append(int* counters, int bin, size_t bstride, int* lds) {
-    if constexpr (!WAVE) {
-        return block_append_bin(counters, bin, bstride, lds);
-    } else {
-        long pos = -1;
-#pragma unroll
-        for (int b = 0; b < RT_NBINS; ++b) {
-            int p = wave_append(counters + b * kQStride, bin == b);
-            if (bin == b) pos = (long)b * (long)bstride + p;
-        }
-        return pos;
-    }
-}
-
-__device__ __forceinline__ int ray_bin(int prim, V3 wi) {
-    if constexpr (RT_BIN_MODE == 1) return dominant_axis(wi);
-    else if constexpr (RT_BIN_MODE == 2) return (prim >> 1) % RT_NBINS;
-    else return 0;
+__device__ __forceinline__ int queue_append(int* counter, bool pred, int* lds) {
+    if constexpr (WAVE) return wave_append(counter, pred);
+    else return block_append(counter, pred, lds);
 }
 
 // the PCG increment of a path never changes after generation: only the 8-byte state half is written back
 __device__ __forceinline__ void store_rng_state(uint4* rng, int slot, uint64_t state) {
     reinterpret_cast<uint2*>(rng)[2 * slot] = make_uint2((uint32_t)state, (uint32_t)(state >> 32));
 }
-#ifndef RT_CTR32
-#define RT_CTR32 0  // 1: per-lane traversal counters in 32 bits (a persistent lane counts < 2^32 tests per launch;
-#endif              // wave reduction and totals stay 64-bit): spills 48 -> 32 B (trace), 132 -> 124 B (shade);
-                    // CFG3 +0.4 %, CFG4 +0.6 %, Cornell -0.6 % (A/B, within noise): off
-#if RT_CTR32
-typedef unsigned ctr_t;
-#else
 typedef unsigned long long ctr_t;
-#endif
 __device__ __forceinline__ void count_add(unsigned long long* ctr, int slot, unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -489,18 +303,13 @@ __device__ __forceinline__ T ldconst(const T* p, int i) {
 // depth-first walk returns exactly the BFS's answer, but reaches an occluder after `depth` descents instead of
 // after sweeping every level above it, and needs a stack of `depth` entries instead of a frontier-sized FIFO.
 // Stack entry = (first node of a group << 8) | its children still to visit; LDS, one column per thread.
-#ifndef RT_DFS_ANYHIT
-#define RT_DFS_ANYHIT 0      // bit 0: k_path_shade's shadow rays, bit 1: k_path_shade_full / k_occluded.  Exact either
-#endif                       // way; the stack's registers cost occupancy or spills under the 4-wave budgets below:
-                             // CFG3 144 -> 135 (bit 0), CFG4 111 -> 87 (bit 1) Msamples/s (A/B): off
+// Used by the shadow-queue kernel (k_path_shadow); inline callers keep the BFS, whose registers the shade kernels can
+// spare (DFS inline: CFG3 144 -> 135, CFG4 111 -> 87 Msamples/s under the 4-wave budgets).
 static constexpr int kDfsDepth = 16;
-#if 1  // DFS any-hit is compiled in; callers pick it per instantiation (DFS template flag)
 __shared__ unsigned g_dfs[kDfsDepth * kBlock];
-#endif
 template <int KZ>
 __device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, V3 d, float tMax,
                                              ctr_t& nn, ctr_t& nt) {
-#if 1
     const V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
     const TriRay R = make_triray<KZ>(o, d);
     const int2* __restrict__ lr = sc.leafRange[set];
@@ -567,9 +376,6 @@ __device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, 
         lf += m;
         lc -= m;
     }
-#else
-    return false;
-#endif
 }
 
 // ===================================================================================== K2 traverse
@@ -577,7 +383,7 @@ __device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, 
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
 // reference's node-level FIFO order exactly.  tMax shrinks on every accepted hit ("t < tMax": the first
 // hit found in BFS order wins ties), so hit ids, barycentrics and t are bit-identical to the reference's.
-template <int QCAP, bool ANYHIT, int KZ, bool DFS = false, bool PFA = false>
+template <int QCAP, bool ANYHIT, int KZ, bool DFS = false>
 __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0, float& rb1,
                                         float& rb2, float& rt, ctr_t& nn, ctr_t& nt) {
     V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
@@ -604,9 +410,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 }
                 return false;
             };
-            constexpr int U = RT_TRI_UNROLL;
+            constexpr int U = kTriUnroll;
             static_assert(U % 2 == 0, "pass 1 walks fan pairs");
-#if RT_TWO_PASS
             if (r.y <= 64) {
                 // pass 1: every triangle's tMax-independent rejections (scalar-cache batches); pass 2: the full
                 // test, in leaf order with the running tMax, on the survivors only — so the division and the
@@ -614,20 +419,18 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 uint64_t cand = 0;
                 int k = 0;
                 const uint64_t fp = sc.fan_pairs[set];  // bit k: leaf tiles k, k+1 share vertices (a,b,c),(a,c,d)
-#if RT_CLUSTER
                 // conservative cluster boxes first: a cluster no lane of the wave reaches is skipped whole
-                // (closest hit: the box over [0, inf); any hit: over [0, tMax], exact for a fixed tMax)
+                // (closest hit: the box over [0, inf); any hit: over [0, tMax], exact for a fixed tMax).  Shadow rays
+                // and coherent closest-hit waves (shared dominant axis: camera rays) cull by wave ballot; incoherent
+                // closest-hit waves compact the passing (ray, cluster) pairs (culling every cluster: -2 %).
                 const float4* cl = sc.clusters[set];
                 const int ncl = sc.n_clusters[set];
-                constexpr bool kCompact = RT_COMPACT == 1 || (RT_COMPACT == 2 && KZ < 0) ||
-                                           (RT_COMPACT == 3 && (KZ < 0 || ANYHIT)) || (RT_COMPACT == 4 && !ANYHIT) ||
-                                           (RT_COMPACT == 5 && !ANYHIT && KZ < 0);
-                constexpr bool kCull = ANYHIT || RT_CLUSTER == 2 || (RT_CLUSTER == 3 && KZ >= 0) || kCompact;
+                constexpr bool kCompact = !ANYHIT && KZ < 0;
+                constexpr bool kCull = ANYHIT || KZ >= 0 || kCompact;
                 if (kCull && ncl * kClusterTris >= r.y) {
                     const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
                     const float gx = o.x - sc.cl_guard.x, gy = o.y - sc.cl_guard.y, gz = o.z - sc.cl_guard.z;
                     const bool far = gx * gx + gy * gy + gz * gz > sc.cl_guard.w;  // pad not sized for it
-#if RT_COMPACT
                     if (kCompact && kClusterTris == 2 && ncl <= kCompactMaxClusters) {
                         // Each lane box-tests every cluster against its own ray; the passing (lane, cluster) pairs
                         // are appended to the wave's LDS list in cluster order (ballot + mbcnt), and the active
@@ -644,7 +447,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         cw.cand[ln] = 0;
                         int np = 0;
                         for (int c = 0; c < ncl; ++c) {
-                            bool hb = far || CL_HIT(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t);
+                            bool hb = far || cluster_hit(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t);
                             uint64_t m = __ballot(hb);
                             if (hb) cw.pair[np + mbcnt64(m)] = (unsigned short)(ln | (c << 6));
                             np += __popcll(m);
@@ -662,7 +465,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                             Q.ky = Q.kx + 1; if (Q.ky == 3) Q.ky = 0;
                             const float4* tp = tiles + 3 * (r.x + 2 * c);
                             unsigned bits;
-                            if (RT_FAN_PAIRS && ((fp >> (2 * c)) & 1)) {
+                            if ((fp >> (2 * c)) & 1) {
                                 bits = tri_candidate_pair<KZ>(Q, tp[0], tp[1], tp[2], tp[4], tp[5]);
                             } else {
                                 bits = tri_candidate<KZ>(Q, tp[0], tp[1], tp[2]) ? 1u : 0u;
@@ -673,22 +476,11 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         wave_lds_sync();
                         cand = cw.cand[ln];
                         k = r.y;
-                    } else
-#endif
-                    {
-                    bool hs = true;
+                    } else {
                     for (int c = 0; c < ncl; ++c) {
-                        if constexpr (kSuperClusters > 0) {
-                            constexpr int S = kSuperClusters > 0 ? kSuperClusters : 1;
-                            if (c % S == 0) {
-                                const int sb = 2 * (ncl + c / S);
-                                hs = far || CL_HIT(ldc4(cl, sb), ldc4(cl, sb + 1), o, inv, cl_t);
-                                if (__ballot(hs) == 0) { c += S - 1; continue; }
-                            }
-                        }
-                        bool hb = far || (hs && CL_HIT(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t));
+                        bool hb = far || cluster_hit(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t);
                         if (__ballot(hb) == 0) continue;
-                        if (RT_FAN_PAIRS && kClusterTris == 2 && ((fp >> (2 * c)) & 1)) {
+                        if (kClusterTris == 2 && ((fp >> (2 * c)) & 1)) {
                             int e = 3 * (r.x + 2 * c);
                             if (hb)
                                 cand |= (uint64_t)tri_candidate_pair<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1),
@@ -708,7 +500,6 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     k = r.y;
                     }
                 }
-#endif
                 for (; k + U <= r.y; k += U) {
                     int e = 3 * (r.x + k);
                     float4 T[3 * U];
@@ -716,7 +507,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     for (int j = 0; j < 3 * U; ++j) T[j] = ldc4(tiles, e + j);
 #pragma unroll
                     for (int u = 0; u < U; u += 2) {
-                        if (RT_FAN_PAIRS && ((fp >> (k + u)) & 1)) {  // wave-uniform: a scalar branch
+                        if ((fp >> (k + u)) & 1) {  // wave-uniform: a scalar branch
                             cand |= (uint64_t)tri_candidate_pair<KZ>(R, T[3 * u], T[3 * u + 1], T[3 * u + 2],
                                                                      T[3 * u + 4], T[3 * u + 5]) << (k + u);
                         } else {
@@ -731,9 +522,6 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     if (tri_candidate<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2))) cand |= 1ull << k;
                 }
                 nt += r.y;
-#ifdef RT_PROFILE_NO_PASS2  // timing experiments only: results are wrong
-                cand = 0;
-#endif
                 while (cand) {
                     int j = __builtin_ctzll(cand);
                     cand &= cand - 1;
@@ -747,7 +535,6 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 }
                 return best;
             }
-#endif
             int k = 0;
             for (; k + U <= r.y; k += U) {
                 int e = 3 * (r.x + k);
@@ -765,28 +552,14 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         }
         return best;
     }
-#if 1
     if constexpr (ANYHIT && DFS) {
         if (sc.depth <= kDfsDepth)  // the upload's octree depth; deeper trees keep the BFS FIFO below
             return occluded_dfs<KZ>(sc, set, o, d, tMax, nn, nt) ? 0 : -1;  // any-hit: 0 = occluded
     }
-#endif
     // Group FIFO.  QCAP > 1: a private array (registers) holding the host's exact worst-case bound.
     // QCAP == 0: the first kLdsQ entries of each lane's FIFO live in LDS as 16-bit group ids (first child =
     // 8 g + 1); once a push finds them full the lane spills every later push to its HBM ring (sized by the
     // bound) until the FIFO drains, so pops read LDS for positions below `spill` and HBM from there on.
-#ifndef RT_GROUP_FETCH
-#define RT_GROUP_FETCH 8  // child boxes loaded together per popped group (8, 4 or 2: register pressure vs MLP)
-#endif
-#ifndef RT_FULL_ANYHIT_PREFETCH
-#define RT_FULL_ANYHIT_PREFETCH 0  // 1: the mixed-scene shadow rays use the pipelined leaf loop too
-#endif
-#ifndef RT_LEAF_PREFETCH
-#define RT_LEAF_PREFETCH 1  // software-pipelined leaf loop (next triangle's 48 B in flight during a test): 1 closest-hit only, 2 all
-#endif
-#ifndef RT_CH_RELOAD
-#define RT_CH_RELOAD 0    // 1: re-read a visited child's first-child index instead of keeping 8 in registers
-#endif
     constexpr bool GQ = QCAP == 0;
     int q[GQ ? 1 : QCAP];
     unsigned short* lq = g_lq;
@@ -830,33 +603,27 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 if (GQ && head == tail) spill = 0x7fffffff;  // drained: LDS again
                 nn += 8;
                 pm = 0;
+                {  // the 8 children's boxes in flight at once (4 or 2 at a time: fewer spills, CFG3 -4 %)
+                    float4 A8[8], B8[8];
 #pragma unroll
-                for (int h = 0; h < 8; h += RT_GROUP_FETCH) {  // RT_GROUP_FETCH children's boxes in flight at once
-                    float4 A8[RT_GROUP_FETCH], B8[RT_GROUP_FETCH];
-#pragma unroll
-                    for (int i = 0; i < RT_GROUP_FETCH; ++i) {
-                        A8[i] = sc.nodeA[gfirst + h + i];
-                        B8[i] = sc.nodeB[gfirst + h + i];
+                    for (int i = 0; i < 8; ++i) {
+                        A8[i] = sc.nodeA[gfirst + i];
+                        B8[i] = sc.nodeB[gfirst + i];
                     }
 #pragma unroll
-                    for (int i = 0; i < RT_GROUP_FETCH; ++i) {
-                        E[h + i] = box_entry(A8[i], B8[i], o, inv);
-                        if (!RT_CH_RELOAD) Ch[h + i] = __float_as_int(A8[i].w);
-                        pm |= (E[h + i] <= tMax ? 1u : 0u) << (h + i);
+                    for (int i = 0; i < 8; ++i) {
+                        E[i] = box_entry(A8[i], B8[i], o, inv);
+                        Ch[i] = __float_as_int(A8[i].w);
+                        pm |= (E[i] <= tMax ? 1u : 0u) << i;
                     }
                 }
                 continue;
             }
             int i = __builtin_ctz(pm);
             pm &= pm - 1;
-            int child;
-            if (RT_CH_RELOAD) {
-                child = __float_as_int(sc.nodeA[gfirst + i].w);  // cache-resident: the group was just fetched
-            } else {
-                child = Ch[0];
+            int child = Ch[0];
 #pragma unroll
-                for (int k = 1; k < 8; ++k) child = i == k ? Ch[k] : child;
-            }
+            for (int k = 1; k < 8; ++k) child = i == k ? Ch[k] : child;
             if (child >= 0) {
                 if constexpr (GQ) {
                     if (spill == 0x7fffffff && tail - head < kLdsQ) {
@@ -879,7 +646,9 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
         // at most kLeafChunk triangles per phase: a lane in a big leaf (the CFG3 octree has leaves of up to 583
         // triangles) keeps the rest pending while the other lanes walk on to their next leaf
         int m = lc < kLeafChunk ? lc : kLeafChunk;
-        constexpr bool PF = RT_LEAF_PREFETCH == 2 || (RT_LEAF_PREFETCH == 1 && (!ANYHIT || PFA));
+        // closest hit: software-pipelined leaf loop (the next triangle's 48 B in flight during a test; any-hit
+        // callers keep the plain loop, whose registers the shade kernels cannot spare)
+        constexpr bool PF = !ANYHIT;
         float4 nA, nB, nC;
         if constexpr (PF) { nA = tiles[3 * lf]; nB = tiles[3 * lf + 1]; nC = tiles[3 * lf + 2]; }
         for (int k = 0; k < m; ++k) {
@@ -913,70 +682,33 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     return best;
 }
 
-// When every active lane of the wave has the same dominant ray axis (camera rays, kz-binned queues) the
-// watertight test's coordinate permutation is resolved at compile time; otherwise per lane.
-template <int QCAP, bool ANYHIT, bool DFS = false, bool PFA = false>
+// When every active lane of the wave has the same dominant ray axis (camera rays) the watertight test's coordinate
+// permutation is resolved at compile time; otherwise per lane.
+template <int QCAP, bool ANYHIT, bool DFS = false>
 __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
                                             float& b2, float& t, ctr_t& nn, ctr_t& nt) {
-#if RT_KZ_SPECIALIZE
     int kz = dominant_axis(d);
     uint64_t act = __ballot(true);
-    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-#endif
-    return traverse<QCAP, ANYHIT, -1, DFS, PFA>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    return traverse<QCAP, ANYHIT, -1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
 }
 
-#ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 4     // >0: amdgpu_waves_per_eu floor for the closest-hit kernel (register budget).  4: the
-                             // multi-level instantiation drops 147 -> 128 VGPRs (48 B/lane spill), 3 -> 4 waves/SIMD:
-                             // CFG3 +10 %; the single-leaf one (107) is unchanged
-#endif
-#if RT_TRACE_WAVES > 0
-#ifndef RT_TRACE_WAVES_1
-#define RT_TRACE_WAVES_1 0  // single-leaf instantiation (QCAP == 1); 0: no budget
-#endif
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? (RT_TRACE_WAVES_1 > 0 ? RT_TRACE_WAVES_1 : 1) : RT_TRACE_WAVES)))
-#else
-#define RT_TRACE_ATTR
-#endif
+// Register budgets (amdgpu_waves_per_eu) of the multi-level instantiations: 4 waves/SIMD (128 VGPRs) on the trace,
+// path shade and mixed-scene shade kernels (CFG3 121 -> 144, CFG4 87 -> 111 Msamples/s; 5 waves spill too much).
+// The single-leaf instantiations (107 / 125 VGPRs) are unbudgeted.
+#define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : 4)))
+
 template <int QCAP>
-__global__ void __launch_bounds__(kBlock) RT_TRACE_ATTR k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
-    const QueueCounts qc(io.count, io.n);
-    const int n = qc.n;
+__global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
+    const int n = io.count ? *io.count : io.n;
     ctr_t nn = 0, nt = 0, nh = 0, nr = 0;
-#if RT_TRACE_KZSORT
-    // The block's rays are regrouped by dominant axis through LDS before traversal, so most waves take the
-    // compile-time-permuted watertight test; hits are written back at the rays' own queue positions.
-    __shared__ float4 s_o[kBlock], s_d[kBlock];
-    __shared__ int s_k[kBlock], s_lds[4 * (kBlock / 64)];
-    for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-        {
-            int kk = base + threadIdx.x;
-            float4 oo = make_float4(0, 0, 0, 0), dd = oo;
-            int key = 3;
-            if (kk < n) {
-                size_t q = qc.pos(kk, io.bstride);
-                oo = io.rayO[q]; dd = io.rayD[q];
-                key = dominant_axis(v3(dd.x, dd.y, dd.z));
-            }
-            int p = block_rank<4>(key, s_lds);
-            s_o[p] = oo; s_d[p] = dd; s_k[p] = kk;
-            __syncthreads();
-        }
-        int k = s_k[threadIdx.x];
-        float4 o4 = s_o[threadIdx.x], d4 = s_d[threadIdx.x];
-        __syncthreads();
-        if (k >= n) continue;
-#else
     // no block-level synchronisation here: each wave takes its own tickets (WaveChunks)
     WaveChunks chunks(io.ticket);
     for (int cb = chunks.next(); cb < n; cb = chunks.next())
     for (int k = cb + chunks.lane; k < cb + chunks.size && k < n; k += chunks.step) {
-        size_t q = qc.pos(k, io.bstride);
-        float4 o4 = io.rayO[q], d4 = io.rayD[q];
-#endif
+        float4 o4 = io.rayO[k], d4 = io.rayD[k];
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
         int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
                                              b0, b1, b2, t, nn, nt);
@@ -1079,47 +811,52 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 }
 
 // ============================================================================ path mode (build-defined)
-// One bounce of the diffuse path integrator (DESIGN.md §Path mode; pbrt-v4 SimplePathIntegrator semantics):
-// emitter hit → Le at depth 0 only (one-sided), then terminate; otherwise NEE on the quad light (Get2D,
-// shadow ray traced inline, pending contribution added on a miss) and a cosine-hemisphere bounce
-// (Get2D, β *= R) appended to the next queue.  Sampler state (PCG state + dimension) lives per path slot.
-// FUSED: the bounce's closest-hit traversal runs here too (the ray is read once, the hit stays in registers), so
-// the VALU-bound traversal and the HBM-bound path-state traffic of different waves overlap on every CU.
-#ifndef RT_APPEND_FIRST
-#define RT_APPEND_FIRST 0    // 1: append the next bounce ray before the inline shadow traversal
-#endif
-#ifndef RT_LD_LDS
-#define RT_LD_LDS 0          // 1: the NEE contribution waits in LDS across the shadow traversal
-#endif
-#ifndef RT_SHADE_WAVES
-#define RT_SHADE_WAVES 4     // >0: amdgpu_waves_per_eu floor for the path shade kernel (register budget).  4: the
-                             // multi-level instantiation 159 -> 128 VGPRs (132 B/lane spill), 3 -> 4 waves/SIMD;
-                             // with RT_TRACE_WAVES=4 CFG3 121 -> 144 Msamples/s; single-leaf (125) unchanged
-#endif
-#if RT_SHADE_WAVES > 0
-#ifndef RT_SHADE_WAVES_1
-#define RT_SHADE_WAVES_1 0  // single-leaf instantiation (QCAP == 1); 0: no budget
-#endif
-#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? (RT_SHADE_WAVES_1 > 0 ? RT_SHADE_WAVES_1 : 1) : RT_SHADE_WAVES)))
-#else
-#define RT_SHADE_ATTR
-#endif
-template <int QCAP, bool FUSED>
-__global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp, DevFilm film,
-                                                       SampleIds ids, PathIO io, unsigned long long* ctr,
-                                                       ShadowQueueIO shq) {
+// One bounce of the diffuse path integrator (pbrt-v4 SimplePathIntegrator semantics): emitter hit →
+// Le at depth 0 only (one-sided), then terminate; otherwise NEE on the quad light (Get2D, shadow ray traced inline,
+// pending contribution added on a miss) and a cosine-hemisphere bounce (Get2D, β *= R) appended to the next queue.
+// Sampler state (PCG state + dimension) lives per path slot.
+__device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevFilm& film, const PathIO& io, int slot,
+                                                Smp& sm) {
+    int pixel, index, x, y;
+    sample_of(ids, slot, pixel, index);
+    pixel_xy(film, pixel, x, y);
+    const uint4 rs = io.rng[slot];
+    sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
+    sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
+    sm.px = x; sm.py = y; sm.index = index; sm.dim = io.dim[slot];
+}
+__device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm) {
+    store_rng_state(io.rng, slot, sm.rng.state);
+    io.dim[slot] = sm.dim;
+}
+// cosine-hemisphere direction (Sampling.h:449-454) in the pbrt CoordinateSystem frame of nrm; false when z == 0
+__device__ __forceinline__ bool cosine_bounce(float u0, float u1, V3 nrm, V3& wi, float& z) {
+    float dx, dy;
+    disk_concentric(u0, u1, dx, dy);
+    z = 1 - dx * dx - dy * dy;
+    z = sqrtf(z > 0.f ? z : 0.f);  // SafeSqrt: std::max(0.f, x)
+    if (z == 0) return false;
+    float sign = copysignf(1.0f, nrm.z);
+    float a = -1 / (sign + nrm.z);
+    float b = nrm.x * nrm.y * a;
+    V3 ss = v3(1 + sign * (nrm.x * nrm.x) * a, sign * b, -sign * nrm.x);
+    V3 tt = v3(b, sign + (nrm.y * nrm.y) * a, -nrm.y);
+    wi = vadd(vadd(vmul(ss, dx), vmul(tt, dy)), vmul(nrm, z));
+    return true;
+}
+
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp,
+                                                                         DevFilm film, SampleIds ids, PathIO io,
+                                                                         unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
-    __shared__ int lds[(RT_NBINS + 6) * (kBlock / 64) + RT_NBINS + 8];
-#if RT_LD_LDS
-    __shared__ float s_ld[8 * kBlock];
-#endif
-    const QueueCounts qc(io.count, 0);
-    const int n = qc.n;
-    ctr_t snn = 0, snt = 0, nsh = 0, tnn = 0, tnt = 0, tnh = 0, tnr = 0;
+    __shared__ int lds[kBlock / 64 + 1];
+    const int n = *io.count;
+    ctr_t snn = 0, snt = 0, nsh = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
-    constexpr bool WAVE = RT_SHADE_WAVE && QCAP != 1;
+    constexpr bool WAVE = QCAP != 1;
     __shared__ int s_tk;
     std::conditional_t<WAVE, WaveChunks, BlockChunks> chunks(io.ticket);
     for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
@@ -1127,28 +864,13 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
         int k = base + chunks.lane;
         bool wantShadow = false, wantNext = false, storedL = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
-        int nbin = -1;
         V3 so = v3(0, 0, 0), sd = so;
         float stmax = 0.f;
         float Ld[8];
         int slot = -1;
-        size_t q = 0;
         if (k < n) {
-            q = qc.pos(k, io.bstride);
-            slot = io.slot[q];
-            int prim;
-            float4 d4, hb;
-            if constexpr (FUSED) {
-                float4 o4 = io.rayO[q];
-                d4 = io.rayD[q];
-                hb = make_float4(0, 0, 0, 0);
-                prim = traverse_any<QCAP, false>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
-                                                 hb.x, hb.y, hb.z, hb.w, tnn, tnt);
-                tnh += prim >= 0;
-                tnr += 1;
-            } else {
-                prim = io.hitPrim[k];
-            }
+            slot = io.slot[k];
+            const int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
                 load8(io.lamA, io.lamB, slot, lam);
@@ -1161,7 +883,7 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
                 float4 P0 = sc.triWorld[3 * prim], P1 = sc.triWorld[3 * prim + 1], P2 = sc.triWorld[3 * prim + 2];
                 V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
                 V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
-                if constexpr (!FUSED) d4 = io.rayD[q];
+                const float4 d4 = io.rayD[k];
                 V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
                 DevMaterial dm = sc.materials[sc.triMaterial[prim]];
                 float4 mt = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
@@ -1177,22 +899,15 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
                 } else if (io.depth < io.max_depth) {
                     V3 nrm = ng;
                     if (vdot(nrm, rayd) > 0) nrm = v3(-nrm.x, -nrm.y, -nrm.z);
-                    if constexpr (!FUSED) hb = io.hitB[k];
+                    const float4 hb = io.hitB[k];
                     V3 p = vadd(vadd(vmul(p0, hb.x), vmul(p1, hb.y)), vmul(p2, hb.z));
                     float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
                     V3 po = vadd(p, vmul(nrm, off));
                     float R[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.x, mt.y, mt.z, lam[i]);
-                    // restore the sampler of this camera sample
-                    int pixel, index, x, y;
-                    sample_of(ids, slot, pixel, index);
-                    pixel_xy(film, pixel, x, y);
                     Smp sm;
-                    uint4 rs = io.rng[slot];
-                    sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
-                    sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
-                    sm.px = x; sm.py = y; sm.index = index; sm.dim = io.dim[slot];
+                    restore_sampler(ids, film, io, slot, sm);
                     // --- NEE on the quad light
                     float u0, u1;
                     sm.get2d(smp, u0, u1);
@@ -1221,46 +936,20 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
                     }
                     // --- cosine-hemisphere BSDF sample (Sampling.h:449-454), frame = pbrt CoordinateSystem
                     sm.get2d(smp, u0, u1);
-                    float dx, dy;
-                    disk_concentric(u0, u1, dx, dy);
-                    float z = 1 - dx * dx - dy * dy;
-                    z = sqrtf(z > 0.f ? z : 0.f);  // SafeSqrt: std::max(0.f, x)
-                    if (z != 0) {
-                        float sign = copysignf(1.0f, nrm.z);
-                        float a = -1 / (sign + nrm.z);
-                        float b = nrm.x * nrm.y * a;
-                        V3 ss = v3(1 + sign * (nrm.x * nrm.x) * a, sign * b, -sign * nrm.x);
-                        V3 tt = v3(b, sign + (nrm.y * nrm.y) * a, -nrm.y);
-                        V3 wi = vadd(vadd(vmul(ss, dx), vmul(tt, dy)), vmul(nrm, z));
+                    V3 wi;
+                    float z;
+                    if (cosine_bounce(u0, u1, nrm, wi, z)) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) beta[i] *= R[i];
                         store8(io.betaA, io.betaB, slot, beta);
                         wantNext = true;
-                        nbin = ray_bin(prim, wi);
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
                     }
-                    store_rng_state(io.rng, slot, sm.rng.state);
-                    io.dim[slot] = sm.dim;
+                    save_sampler(io, slot, sm);
                 }
             }
         }
-#if RT_APPEND_FIRST  // the next ray leaves before the shadow traversal: its 9 registers are not live across it
-    {
-#if RT_RAY_SORT
-        long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
-#else
-        long pn = queue_append<WAVE>(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
-#endif
-        if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
-    }
-#endif
-#if RT_LD_LDS  // the pending contribution waits in LDS (8 floats per thread) instead of registers
-        if (wantShadow) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) s_ld[i * kBlock + threadIdx.x] = Ld[i];
-        }
-#endif
         if constexpr (QCAP != 1) {  // shadow queue: the ray and its pending contribution go to k_path_shadow
             if (shq.shO) {
                 int sp = WAVE ? wave_append(shq.shCount, wantShadow) : block_append(shq.shCount, wantShadow, lds);
@@ -1277,19 +966,11 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
         // pending contribution Ld stays live across the traversal.  No shadow queue in HBM.
         if (wantShadow) {
             float b0, b1, b2, t;
-#ifdef RT_PROFILE_NO_SHADOW  // timing experiments only: every shadow ray counts as unoccluded
-            int hit = -1;
-#else
-            int hit = traverse_any<QCAP, true, (RT_DFS_ANYHIT & 1) != 0>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt);
-#endif
+            int hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt);
             ++nsh;
             if (hit < 0) {
                 float L[8];
                 load8_or_zero(io.LA, io.LB, slot, L, d0);
-#if RT_LD_LDS
-#pragma unroll
-                for (int i = 0; i < 8; ++i) Ld[i] = s_ld[i * kBlock + threadIdx.x];
-#endif
 #pragma unroll
                 for (int i = 0; i < 8; ++i) L[i] += Ld[i];
                 store8(io.LA, io.LB, slot, L);
@@ -1300,24 +981,12 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
             const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             store8(io.LA, io.LB, slot, z);
         }
-#if !RT_APPEND_FIRST
-#if RT_RAY_SORT
-        long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
-#else
-        long pn = queue_append<WAVE>(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
-#endif
+        const int pn = queue_append<WAVE>(io.nCount, wantNext, lds);
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
-#endif
     }
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
-    if constexpr (FUSED) {
-        count_add(ctr, C_NODES, tnn);
-        count_add(ctr, C_TRIS, tnt);
-        count_add(ctr, C_HITS, tnh);
-        count_add(ctr, C_RAYS, tnr);
-    }
 }
 
 
@@ -1325,21 +994,12 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_ATTR k_path_shade(DevScene sc
 // with no path state live (full occupancy; DFS: depth-first any-hit, exact for a fixed tMax, §6).  An unoccluded
 // ray adds its contribution to L exactly as the inline code would: per slot one shadow ray per bounce, launched
 // between this bounce's shade and the next one's, so every L sees its additions in the same order.
-#ifndef RT_SHADOW_WAVES
-#define RT_SHADOW_WAVES 0  // >0: amdgpu_waves_per_eu floor for k_path_shadow
-#endif
-#if RT_SHADOW_WAVES > 0
-#define RT_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES)))
-#else
-#define RT_SHADOW_ATTR
-#endif
 template <int QCAP, bool DFS>
-__global__ void __launch_bounds__(kBlock) RT_SHADOW_ATTR k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
+__global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
     const int n = *shq.shCount;
     ctr_t snn = 0, snt = 0, nsh = 0;
-    __shared__ int s_tk;
     WaveChunks chunks(shq.shTicket);
-    for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
+    for (int cb = chunks.next(); cb < n; cb = chunks.next())
     for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
         int k = base + chunks.lane;
         if (k >= n) continue;
@@ -1369,26 +1029,11 @@ __global__ void __launch_bounds__(kBlock) RT_SHADOW_ATTR k_path_shadow(DevScene 
 // shapes, mirror and BK7/constant-eta glass (TerminateSecondary rewrites the sample's pdf), point / distant /
 // disk / quad lights (one sample each, shadow rays traced inline in light order), and MIS (power heuristic).
 // Semantics and sample-dimension order: oracle/rtcore.hpp LiPath, DESIGN.md §5.
-__device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevFilm& film, const PathIO& io, int slot,
-                                                Smp& sm, uint4& rs) {
-    int pixel, index, x, y;
-    sample_of(ids, slot, pixel, index);
-    pixel_xy(film, pixel, x, y);
-    rs = io.rng[slot];
-    sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
-    sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
-    sm.px = x; sm.py = y; sm.index = index; sm.dim = io.dim[slot];
-}
-__device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm, uint4 rs) {
-    store_rng_state(io.rng, slot, sm.rng.state);
-    io.dim[slot] = sm.dim;
-}
 template <int QCAP>
 __device__ __forceinline__ bool scene_occluded(const DevScene& sc, V3 o, V3 d, float tmax, ctr_t& nn,
                                                ctr_t& nt) {
     float b0, b1, b2, t;
-    if (traverse_any<QCAP, true, (RT_DFS_ANYHIT & 2) != 0, RT_FULL_ANYHIT_PREFETCH != 0>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0)
-        return true;
+    if (traverse_any<QCAP, true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0) return true;
     for (int si = 0; si < sc.n_shapes; ++si) {
         DevShape sh = ldconst(sc.shapes, si);
         V3 ph;
@@ -1413,30 +1058,17 @@ __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const f
     count_add(ctr, C_SHADOW, ns);
 }
 
-#ifndef RT_FULL_NEE_PRE
-#define RT_FULL_NEE_PRE 0    // 1: mixed-scene NEE loop with fewer live registers (reloads beta, λ afterwards)
-#endif
-#ifndef RT_SHADE_FULL_WAVES
-#define RT_SHADE_FULL_WAVES 4  // >0: amdgpu_waves_per_eu floor for the mixed-scene shade kernel (register budget).
-                               // 3: 246 -> 168 VGPRs (312 B/lane spill), 2 -> 3 waves/SIMD: CFG4 87 -> 98 Msamples/s;
-                               // 4: 128 VGPRs (464 B/lane spill), 4 waves/SIMD: 111 Msamples/s (A/B)
-#endif
-#if RT_SHADE_FULL_WAVES > 0
-#define RT_SHADE_FULL_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_FULL_WAVES)))
-#else
-#define RT_SHADE_FULL_ATTR
-#endif
 template <int QCAP>
-__global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(DevScene sc, const DevSpectra* sp, DevSampler smp,
-                                                            DevFilm film, SampleIds ids, PathIO io,
-                                                            unsigned long long* ctr) {
+__global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(DevScene sc, const DevSpectra* sp,
+                                                                              DevSampler smp, DevFilm film,
+                                                                              SampleIds ids, PathIO io,
+                                                                              unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
-    __shared__ int lds[(RT_NBINS + 6) * (kBlock / 64) + RT_NBINS + 8];
-    const QueueCounts qc(io.count, 0);
-    const int n = qc.n;
+    __shared__ int lds[kBlock / 64 + 1];
+    const int n = *io.count;
     ctr_t snn = 0, snt = 0, nsh = 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
-    constexpr bool WAVE = RT_SHADE_WAVE && QCAP != 1;
+    constexpr bool WAVE = QCAP != 1;
     __shared__ int s_tk;
     std::conditional_t<WAVE, WaveChunks, BlockChunks> chunks(io.ticket);
     for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
@@ -1444,17 +1076,16 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(D
         int k = base + chunks.lane;
         bool wantNext = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
-        int nbin = -1, slot = -1;
+        int slot = -1;
         if (k < n) {
-            size_t q = qc.pos(k, io.bstride);
-            slot = io.slot[q];
+            slot = io.slot[k];
             int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8], L[8];
                 load8(io.lamA, io.lamB, slot, lam);
                 load8(io.betaA, io.betaB, slot, beta);
                 load8(io.LA, io.LB, slot, L);
-                float4 o4 = io.rayO[q], d4 = io.rayD[q];
+                float4 o4 = io.rayO[k], d4 = io.rayD[k];
                 V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
                 V3 rayd = vnorm(rdw);
                 float4 hb = io.hitB[k];
@@ -1522,12 +1153,10 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(D
                         wantNext = true;
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                        nbin = ray_bin(prim, wi);
                         io.prevPdf[slot] = 0.f;
                     } else {
                         Smp sm;
-                        uint4 rs;
-                        restore_sampler(ids, film, io, slot, sm, rs);
+                        restore_sampler(ids, film, io, slot, sm);
                         if (mt.type == 2) {  // smooth dielectric
                             if (mt.eta == 0) {  // dispersive BK7: TerminateSecondary (spectrum.h:302-310)
                                 float pdf[8];
@@ -1561,18 +1190,9 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(D
                             wantNext = true;
                             nO = make_float4(po.x, po.y, po.z, 0.f);
                             nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                            nbin = ray_bin(prim, wi);
                             io.prevPdf[slot] = 0.f;
                         } else {  // Lambert: NEE per light, then a cosine-hemisphere bounce
                             V3 po = vadd(p, vmul(nrm, off));
-#if RT_FULL_NEE_PRE  // the light loop keeps beta·R/π and D65(λ) live instead of beta, R and λ (same products)
-                            float BR[8], D65l[8];
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) {
-                                BR[i] = beta[i] * (R[i] * InvPi);
-                                D65l[i] = dense_query(sp->D65, lam[i]);
-                            }
-#endif
                             for (int li = 0; li < sc.n_lights; ++li) {
                                 const DevLight Lt = ldconst(sc.lights, li);
                                 float u0, u1;
@@ -1627,57 +1247,34 @@ __global__ void __launch_bounds__(kBlock) RT_SHADE_FULL_ATTR k_path_shade_full(D
                                     if (!scene_occluded<QCAP>(sc, po, wi, tmax, snn, snt)) {
 #pragma unroll
                                         for (int i = 0; i < 8; ++i) {
-#if RT_FULL_NEE_PRE
-                                            float Le = sc_le * D65l[i];
-                                            L[i] += (BR[i] * Le) * wgt;
-#else
                                             float Le = sc_le * dense_query(sp->D65, lam[i]);
                                             L[i] += ((beta[i] * (R[i] * InvPi)) * Le) * wgt;
-#endif
                                         }
                                     }
                                 }
                             }
                             store8(io.LA, io.LB, slot, L);
-#if RT_FULL_NEE_PRE  // beta and λ come back from memory, R is recomputed (bit-identical)
-                            load8(io.betaA, io.betaB, slot, beta);
-                            load8(io.lamA, io.lamB, slot, lam);
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.c0, mt.c1, mt.c2, lam[i]);
-#endif
                             // cosine-hemisphere bounce (Sampling.h:449-454), pbrt CoordinateSystem frame
-                            float u0, u1, dx, dy;
+                            float u0, u1;
                             sm.get2d(smp, u0, u1);
-                            disk_concentric(u0, u1, dx, dy);
-                            float z = 1 - dx * dx - dy * dy;
-                            z = sqrtf(z > 0.f ? z : 0.f);
-                            if (z != 0) {
-                                float sign = copysignf(1.0f, nrm.z);
-                                float a = -1 / (sign + nrm.z);
-                                float b = nrm.x * nrm.y * a;
-                                V3 ss = v3(1 + sign * (nrm.x * nrm.x) * a, sign * b, -sign * nrm.x);
-                                V3 tt = v3(b, sign + (nrm.y * nrm.y) * a, -nrm.y);
-                                V3 wi = vadd(vadd(vmul(ss, dx), vmul(tt, dy)), vmul(nrm, z));
+                            V3 wi;
+                            float z;
+                            if (cosine_bounce(u0, u1, nrm, wi, z)) {
 #pragma unroll
                                 for (int i = 0; i < 8; ++i) beta[i] *= R[i];
                                 store8(io.betaA, io.betaB, slot, beta);
                                 wantNext = true;
                                 nO = make_float4(po.x, po.y, po.z, 0.f);
                                 nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                                nbin = ray_bin(prim, wi);
                                 io.prevPdf[slot] = z * InvPi;
                             }
                         }
-                        save_sampler(io, slot, sm, rs);
+                        save_sampler(io, slot, sm);
                     }
                 }
             }
         }
-#if RT_RAY_SORT
-        long pn = block_append_sorted<6>(io.nCount, wantNext ? major_dir(v3(nD.x, nD.y, nD.z)) : -1, lds);
-#else
-        long pn = queue_append<WAVE>(io.nCount, wantNext ? nbin : -1, io.bstride, lds);
-#endif
+        const int pn = queue_append<WAVE>(io.nCount, wantNext, lds);
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1780,15 +1377,11 @@ static inline int grid_for(int n, int grid) {
     return g < 1 ? 1 : g;
 }
 
-#ifndef RT_GRID_OCC
-#define RT_GRID_OCC 1
-#endif
 // Persistent grid-stride kernels: every block gets the same share of the queue, so launching more blocks than can
-// be resident at once (grid = 8 per CU, occupancy 4-5 per CU) runs a second, under-occupied round of blocks.
-// RT_GRID_OCC clamps the grid to exactly the resident block count of the kernel (`grid` is CUs x 8).
+// be resident at once (grid = 8 per CU, occupancy 4-5 per CU) runs a second, under-occupied round of blocks.  The
+// grid is clamped to exactly the resident block count of the kernel (`grid` is CUs x 8; Cornell 1112 -> 1202).
 template <class F>
 static int resident_grid(F kern, int gb, int grid) {
-#if RT_GRID_OCC
     static std::mutex mu;
     static std::unordered_map<const void*, int> cache;
     int per_cu = 0;
@@ -1806,7 +1399,6 @@ static int resident_grid(F kern, int gb, int grid) {
         int res = per_cu * (grid / 8);
         if (res > 0 && gb > res) gb = res;
     }
-#endif
     return gb;
 }
 
@@ -1876,12 +1468,9 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
         if (sc.full)                                                                                             \
             hipLaunchKernelGGL(k_path_shade_full<Q>, dim3(resident_grid(k_path_shade_full<Q>, gb, grid)), b, 0, st, \
                                sc, sp, smp, film, ids, io, ctr);                                                 \
-        else if (io.fused)                                                                                       \
-            hipLaunchKernelGGL((k_path_shade<Q, true>), dim3(resident_grid(k_path_shade<Q, true>, gb, grid)), b, 0, \
-                               st, sc, sp, smp, film, ids, io, ctr, shq);                                        \
         else                                                                                                     \
-            hipLaunchKernelGGL((k_path_shade<Q, false>), dim3(resident_grid(k_path_shade<Q, false>, gb, grid)), b, \
-                               0, st, sc, sp, smp, film, ids, io, ctr, shq);                                     \
+            hipLaunchKernelGGL(k_path_shade<Q>, dim3(resident_grid(k_path_shade<Q>, gb, grid)), b, 0, st, sc, sp,  \
+                               smp, film, ids, io, ctr, shq);                                                    \
         break;
     switch (qcap) {
         RT_SHADE_CASE(0)

@@ -6,20 +6,13 @@
 
 #include "rt_internal.h"
 
-#ifndef RT_SORT_KEY
-#define RT_SORT_KEY 4
-#endif
-#ifndef RT_SORT_DIRB
-#define RT_SORT_DIRB 3       // direction: octant + 2 x DIRB bits of the octahedral position
-#endif
-#ifndef RT_SORT_ORGB
-#define RT_SORT_ORGB 7       // origin: ORGB bits per axis (Morton)
-#endif
-
+// key = direction octant, then the octahedral position of the direction on a 2^kDirB x 2^kDirB grid, then a Morton
+// code of the origin with kOrgB bits per axis (DESIGN.md §6 key table: CFG3 83 / CFG4 55 Msamples/s, best measured)
 namespace rtmi {
 namespace {
 
-constexpr int kKeyBits = RT_SORT_KEY == 4 ? 3 + 2 * RT_SORT_DIRB + 3 * RT_SORT_ORGB : 30;
+constexpr int kDirB = 3, kOrgB = 7;
+constexpr int kKeyBits = 3 + 2 * kDirB + 3 * kOrgB;
 static_assert(kKeyBits <= 32, "sort key wider than 32 bits");
 
 __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every third bit of 27
@@ -47,24 +40,14 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const float4
             x = x < 0.f ? 0.f : (x > 511.f ? 511.f : x);
             return (unsigned)x;
         };
-        unsigned m = spread3(q((p.x - lo.x) * scale.x)) << 2 | spread3(q((p.y - lo.y) * scale.y)) << 1 |
-                     spread3(q((p.z - lo.z) * scale.z));
         unsigned oct = (v.x < 0.f ? 4u : 0u) | (v.y < 0.f ? 2u : 0u) | (v.z < 0.f ? 1u : 0u);
-#if RT_SORT_KEY == 1
-        keys[k] = m << 3 | oct;  // origin-major
-#elif RT_SORT_KEY == 4
-        {  // octant, then the octahedral position on a 2^B x 2^B grid, then an origin Morton code of 3 x ORGB bits
-            constexpr int B = RT_SORT_DIRB, OB = RT_SORT_ORGB;
-            float s = fabsf(v.x) + fabsf(v.y) + fabsf(v.z);
-            const float G = (float)(1 << B);
-            unsigned ux = (unsigned)fminf(fabsf(v.x) / s * G, G - 1), uy = (unsigned)fminf(fabsf(v.y) / s * G, G - 1);
-            unsigned mo = spread3(q((p.x - lo.x) * scale.x) >> (9 - OB)) << 2 |
-                          spread3(q((p.y - lo.y) * scale.y) >> (9 - OB)) << 1 | spread3(q((p.z - lo.z) * scale.z) >> (9 - OB));
-            keys[k] = ((oct << (2 * B) | ux << B | uy) << (3 * OB)) | mo;
-        }
-#else
-        keys[k] = oct << 27 | m;  // direction octant first
-#endif
+        float sum = fabsf(v.x) + fabsf(v.y) + fabsf(v.z);
+        const float G = (float)(1 << kDirB);
+        unsigned ux = (unsigned)fminf(fabsf(v.x) / sum * G, G - 1), uy = (unsigned)fminf(fabsf(v.y) / sum * G, G - 1);
+        unsigned mo = spread3(q((p.x - lo.x) * scale.x) >> (9 - kOrgB)) << 2 |
+                      spread3(q((p.y - lo.y) * scale.y) >> (9 - kOrgB)) << 1 |
+                      spread3(q((p.z - lo.z) * scale.z) >> (9 - kOrgB));
+        keys[k] = ((oct << (2 * kDirB) | ux << kDirB | uy) << (3 * kOrgB)) | mo;
         vals[k] = k;
     }
 }

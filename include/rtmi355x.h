@@ -29,8 +29,8 @@ typedef enum {
     RT_E_ARG = -1,      /* invalid argument / descriptor                                   */
     RT_E_HIP = -2,      /* HIP runtime error (message in rt_last_error)                    */
     RT_E_RCCL = -3,     /* reserved: collectives run in the caller (torch.distributed)     */
-    RT_E_OOM = -4,      /* device allocation failed                                        */
-    RT_E_STATE = -5,    /* call order: scene/camera/sampler/film not set                   */
+    RT_E_OOM = -4,      /* device or host allocation failed (std::bad_alloc is caught)     */
+    RT_E_STATE = -5,    /* call order: scene/camera/sampler/film not set; internal error   */
     RT_E_NODEVICE = -6, /* no gfx950 device visible                                        */
     RT_E_LIMIT = -7     /* scene exceeds a compiled limit (e.g. BFS queue bound)           */
 } rt_status;
@@ -204,8 +204,9 @@ typedef struct {
     int64_t shadow_nodes_tested;     /* node box tests by any-hit (shadow) rays          */
     int64_t shadow_tris_tested;      /* triangle tests by any-hit (shadow) rays          */
     int64_t hits;                    /* closest-hit rays that hit                        */
-    double ms_generate, ms_trace, ms_shade, ms_shadow, ms_film;  /* HIP-event kernel time; ms_shadow
-                                        stays 0: shadow rays are traced inside the path shade kernel */
+    double ms_generate, ms_trace, ms_shade, ms_shadow, ms_film;  /* HIP-event kernel time; ms_shadow is
+                                        the shadow-queue kernel (RTMI_SHADOW_QUEUE=1), else 0: shadow rays
+                                        are traced inside the path shade kernel */
     int64_t launches_trace;          /* closest-hit trace launches (per-launch averages) */
     int64_t launches_shade;          /* shade launches (path mode: includes the inline shadow rays) */
 } rt_stats;   /* multi-device contexts: every field summed over the devices */

@@ -21,6 +21,21 @@ def build(quiet=True):
     return LIB
 
 
+def use_native():
+    """bench.py's cpu_baseline leg: rebuild the restatement with -O3 -march=native for the host it runs on (SURVEY
+    §8d; ~5 s of g++ on the GPU box's own CPU, so the binary matches that CPU) and load it instead of the -O2
+    parity build.  -ffp-contract=off and no fast-math either way, so both builds compute the same bits."""
+    global LIB
+    if _lib is not None:
+        raise RuntimeError("oracle library already loaded")
+    out = ORACLE_DIR / "_build" / "librtcore_native.so"
+    r = subprocess.run(["make", "-C", str(ORACLE_DIR), "native", "-B"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("oracle native build failed:\n" + r.stdout + r.stderr)
+    LIB = out
+    return out
+
+
 _lib = None
 
 
@@ -163,7 +178,7 @@ class OracleScene:
         if film is None:
             film = np.zeros((self.res[0] * self.res[1], 4), np.float32)
         if nthreads is None:
-            nthreads = min(os.cpu_count() or 1, 16)
+            nthreads = min(os.cpu_count() or 1, 16)  # tests; bench.py's baseline passes os.cpu_count()
         cnt = np.zeros(5, np.int64)
         if pixel_ids is not None:
             pixel_ids = np.ascontiguousarray(pixel_ids, np.int32)

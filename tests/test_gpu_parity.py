@@ -243,6 +243,20 @@ def test_cfg3_path_film_bitexact(cfg3_pair):
     assert bad.sum() == 0, f"{bad.sum()} pixels differ"
 
 
+def test_cfg3_lanes_overlap_with_ring_spills(cfg3_pair, oracle_lib, monkeypatch):
+    """Two lanes whose trace / shade kernels run concurrently on a scene whose BFS FIFOs spill to the HBM overflow
+    ring (qcap 0): each lane has its own ring, so the film is bit-exact (tolerance 0).  Small batches (one index
+    each) keep both lanes busy at once across the pass."""
+    cfg, _, o = cfg3_pair
+    monkeypatch.setenv("RTMI_BATCH_SAMPLES", str(96 * 54))
+    monkeypatch.setenv("RTMI_LANES", "2")
+    g = Renderer(cfg)
+    fg = g.render_pass(0, 4)
+    fo = o.render(0, 4)
+    bad = np.any(bits(fg) != bits(fo), axis=1)
+    assert bad.sum() == 0, f"{bad.sum()} pixels differ"
+
+
 @pytest.fixture(scope="module")
 def cfg4_small():
     return scene.cfg4_mixed(res=(96, 54), spp=(2, 2), frequency=16)
