@@ -25,7 +25,7 @@ RT_SENSOR_XYZ, RT_SENSOR_CANON_EOS_100D, RT_SENSOR_COUNT = 0, 1, 18
 RT_OCTREE_BUILD_DEVICE, RT_OCTREE_BUILD_HOST = 0, 1
 RT_ILLUM_D65, RT_ILLUM_A, RT_ILLUM_D50, RT_ILLUM_F1, RT_ILLUM_ACES_D60, RT_ILLUM_COUNT = 0, 1, 2, 3, 15, 16
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 RT_MAX_DEVICES = 16
 
 F16 = C.c_float * 16
@@ -101,7 +101,7 @@ class rt_stats(C.Structure):
                 ("shadow_tris_tested", C.c_int64), ("hits", C.c_int64),
                 ("ms_generate", C.c_double), ("ms_trace", C.c_double), ("ms_shade", C.c_double),
                 ("ms_shadow", C.c_double), ("ms_film", C.c_double), ("launches_trace", C.c_int64),
-                ("launches_shade", C.c_int64)]
+                ("launches_shade", C.c_int64), ("fallback_rays", C.c_int64), ("shadow_fallback_rays", C.c_int64)]
 
 
 class rt_sample_record(C.Structure):
@@ -115,7 +115,8 @@ class rt_mesh(C.Structure):
 
 
 class rt_octree_info(C.Structure):
-    _fields_ = [("n_nodes", C.c_int), ("n_leaf_refs", C.c_int), ("max_queue_groups", C.c_int), ("depth", C.c_int)]
+    _fields_ = [("n_nodes", C.c_int), ("n_leaf_refs", C.c_int), ("max_queue_groups", C.c_int), ("depth", C.c_int),
+                ("bvh_nodes", C.c_int), ("bvh_depth", C.c_int)]
 
 
 # every symbol include/rtmi355x.h declares (checked by tests/test_capi_symbols.py)

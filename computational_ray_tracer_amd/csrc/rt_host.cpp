@@ -1641,6 +1641,29 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
                 return fail(c, RT_E_LIMIT, "octree too large for 16-bit BFS group ids");
         }
     }
+    // multi-level octrees: the fast traversal's BVH per tile set (non-degenerate triangles; set 1 without the
+    // back-facing ones) and the canonical-rule window (rt_bvh.cpp)
+    BvhData bvh[2];
+    float wabs = 0.f;
+    if (qcap != 1) {
+        float mc = 0.f;
+        for (const F3& p : wv) mc = std::max(mc, std::max(std::fabs(p.x), std::max(std::fabs(p.y), std::fabs(p.z))));
+        wabs = mc * 0x1p-20f;  // same value as the oracle's Octree::SetWindow
+        const float pad = mc * 0x1p-18f;
+        for (int st = 0; st < (c->cull ? 2 : 1); ++st) {
+            std::vector<float> t9;
+            std::vector<int> ids;
+            for (int t = 0; t < nt; ++t) {
+                if (degen[t] || (st == 1 && back[t])) continue;
+                for (int k = 0; k < 3; ++k) {
+                    const F3& p = tri3[3 * (size_t)t + k];
+                    t9.push_back(p.x); t9.push_back(p.y); t9.push_back(p.z);
+                }
+                ids.push_back(t);
+            }
+            build_bvh4(t9.data(), ids.data(), (int)ids.size(), pad, bvh[st]);
+        }
+    }
     c->info.n_nodes = nn;
     c->info.n_leaf_refs = (int)c->h_refs.size();
     c->info.max_queue_groups = bound;
@@ -1767,7 +1790,20 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     void *pc0 = nullptr, *pc1 = nullptr;
     if ((rc = up(clus[0].data(), clus[0].size() * 16, &pc0)) || (rc = up(clus[1].data(), clus[1].size() * 16, &pc1)))
         return rc;
+    void* pbv[2] = {nullptr, nullptr};
+    void* pbt[2] = {nullptr, nullptr};
+    for (int st = 0; st < 2; ++st)
+        if (!bvh[st].nodes.empty() && ((rc = up(bvh[st].nodes.data(), bvh[st].nodes.size() * 16, &pbv[st])) ||
+                                        (rc = up(bvh[st].tiles.data(), bvh[st].tiles.size() * 16, &pbt[st]))))
+            return rc;
     DevScene& d = c->dsc;
+    for (int st = 0; st < 2; ++st) {
+        d.bvh[st] = (const float4*)(pbv[st] ? pbv[st] : pbv[0]);
+        d.btiles[st] = (const float4*)(pbt[st] ? pbt[st] : pbt[0]);
+    }
+    d.wabs = wabs;
+    c->info.bvh_nodes = (int)(bvh[0].nodes.size() / 8);
+    c->info.bvh_depth = bvh[0].depth;
     d.clusters[0] = (const float4*)pc0; d.clusters[1] = (const float4*)pc1;
     if (qcap != 1) d.n_clusters[0] = d.n_clusters[1] = 0;
     d.nodeA = (const float4*)pA; d.nodeB = (const float4*)pB;
@@ -1948,6 +1984,8 @@ static int get_stats_one(rt_ctx* c, rt_stats* out) {
     s.shadow_nodes_tested = (int64_t)h[C_SNODES];
     s.shadow_tris_tested = (int64_t)h[C_STRIS];
     s.samples = (int64_t)h[C_SAMPLES];
+    s.fallback_rays = (int64_t)h[C_FALLBACK];
+    s.shadow_fallback_rays = (int64_t)h[C_SFALLBACK];
     *out = s;
     return RT_OK;
 }
@@ -2192,6 +2230,7 @@ static int impl_rt_get_stats(rt_ctx* c, rt_stats* out) {
         sum.ms_generate += s.ms_generate; sum.ms_trace += s.ms_trace; sum.ms_shade += s.ms_shade;
         sum.ms_shadow += s.ms_shadow; sum.ms_film += s.ms_film;
         sum.launches_trace += s.launches_trace; sum.launches_shade += s.launches_shade;
+        sum.fallback_rays += s.fallback_rays; sum.shadow_fallback_rays += s.shadow_fallback_rays;
         return RT_OK;
     });
     if (!rc) *out = sum;

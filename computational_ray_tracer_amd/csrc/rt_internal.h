@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace rtmi {
 
 static const int kSpecN = 471;      // dense spectra 360..830 nm (spectrum.h:17, 380-381)
@@ -106,10 +108,23 @@ struct DevScene {
     int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
     int ring_mask;
     int ring_threads;               // launches with qcap == 0 are clamped to this many threads
+    // multi-level octrees (qcap != 1): the fast traversal's 4-wide BVH per tile set (rt_bvh.cpp: 8 float4 per
+    // node) and its leaf-ordered triangle tiles; rays it finds ambiguous fall back to the octree BFS
+    const float4* bvh[2];
+    const float4* btiles[2];
+    float wabs;                     // canonical-rule window W(t) = t 2^-16 + wabs
 };
 
 // device counter slots (u64)
-enum { C_NODES = 0, C_TRIS, C_HITS, C_RAYS, C_SHADOW, C_SAMPLES, C_SNODES, C_STRIS, C_NCOUNTERS = 16 };
+enum { C_NODES = 0, C_TRIS, C_HITS, C_RAYS, C_SHADOW, C_SAMPLES, C_SNODES, C_STRIS, C_FALLBACK, C_SFALLBACK,
+       C_NCOUNTERS = 16 };
+
+// host: 4-wide BVH build (rt_bvh.cpp)
+struct BvhData {
+    std::vector<float4> nodes, tiles;
+    int depth = 0, max_leaf = 0;
+};
+void build_bvh4(const float* tri9, const int* ids, int n, float pad, BvhData& out);
 
 }  // namespace rtmi
 

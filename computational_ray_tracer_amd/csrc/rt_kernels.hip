@@ -26,7 +26,11 @@ static constexpr int kBlock = kBlockThreads;
 static constexpr int kLeafChunk = 32;  // triangles per leaf phase of the while-while traversal (16: -5 %, 64: +-0)
 static constexpr int kLdsQ = 32;       // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
 static constexpr int kTriUnroll = 4;   // triangles per scalar-cache batch in single-leaf traversal
-__shared__ unsigned short g_lq[kLdsQ * kBlock];  // one per block, shared by every traversal call site
+static constexpr int kBvhStack = 16;   // BVH traversal stack entries per lane (child word, entry distance): 32 KB
+// One per block, shared by every multi-level traversal call site: the BVH stacks, and — for the rare rays the BVH
+// hands to the reference BFS, after the wave's BVH loop has finished — that BFS's LDS-resident group FIFO.
+__shared__ uint2 g_bstk[kBvhStack * kBlock];
+static_assert(sizeof(uint2) * kBvhStack >= 2 * kLdsQ, "the BFS FIFO lives in the BVH stack's LDS");
 
 // Single-leaf scenes, closest-hit waves without a shared dominant axis (bounce rays): pass 1 runs on a compacted list
 // of (ray, cluster) pairs whose box test passes (wave ballot + prefix into LDS) instead of every cluster for every lane.
@@ -562,7 +566,9 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     // bound) until the FIFO drains, so pops read LDS for positions below `spill` and HBM from there on.
     constexpr bool GQ = QCAP == 0;
     int q[GQ ? 1 : QCAP];
-    unsigned short* lq = g_lq;
+    // the FIFO lives in this thread's own column of the BVH stacks (waves of the block may still be walking theirs):
+    // entry j at 16-bit word (j / 4) * 4 kBlock + j % 4 of the column
+    unsigned short* lq = reinterpret_cast<unsigned short*>(g_bstk + threadIdx.x);
     int* gq = GQ ? sc.ring + (blockIdx.x * blockDim.x + threadIdx.x) : nullptr;
     const int qmask = GQ ? sc.ring_mask : QCAP - 1;
     int spill = 0x7fffffff;
@@ -594,7 +600,10 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
             if (pm == 0) {
                 if (head == tail) { done = true; break; }
                 if constexpr (GQ) {
-                    if (head < spill) gfirst = 8 * (int)lq[(head & (kLdsQ - 1)) * kBlock + threadIdx.x] + 1;
+                    if (head < spill) {
+                        const int j = head & (kLdsQ - 1);
+                        gfirst = 8 * (int)lq[(j >> 2) * (4 * kBlock) + (j & 3)] + 1;
+                    }
                     else gfirst = gq[(size_t)(head & qmask) * sc.ring_threads];
                 } else {
                     gfirst = q[head & qmask];
@@ -627,7 +636,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
             if (child >= 0) {
                 if constexpr (GQ) {
                     if (spill == 0x7fffffff && tail - head < kLdsQ) {
-                        lq[(tail & (kLdsQ - 1)) * kBlock + threadIdx.x] = (unsigned short)((child - 1) >> 3);
+                        const int j = tail & (kLdsQ - 1);
+                        lq[(j >> 2) * (4 * kBlock) + (j & 3)] = (unsigned short)((child - 1) >> 3);
                     } else {
                         if (spill == 0x7fffffff) spill = tail;
                         gq[(size_t)(tail & qmask) * sc.ring_threads] = child;
@@ -682,17 +692,213 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     return best;
 }
 
+// ============================================================= fast multi-level traversal
+// The reference's unordered BFS (Octtree_Model.h:66-127) only shrinks tMax when its order happens to reach the
+// near leaf, and its answer depends on that order only through near-ties.  Multi-level scenes therefore walk a
+// 4-wide BVH (rt_bvh.cpp) nearest-child first and apply the canonical rule of oracle/rtcore.hpp
+// (Octree::ClosestCanonical / OccludedCanonical), which tests/test_canonical_traversal.py checks against the BFS
+// on >= 10 M rays:
+//   closest hit: keep the two smallest-t distinct triangles (t1, t2), prune with cut = t1 + 2 W(t1).  If
+//                t2 > t1 + W(t1) the BFS must end on t1's triangle with the same (b, t); otherwise (or on a stack
+//                overflow) the ray is ambiguous;
+//   any hit:     a passing triangle with t < tMax - W(tMax) proves occlusion; hits only inside the window are
+//                ambiguous.
+// Ambiguous rays — rare: coplanar / touching surfaces, near-tMax occluders — run the reference BFS below.
+__device__ __forceinline__ float canon_window(float t, float wabs) { return t * 0x1p-16f + wabs; }
+
+// conservative slab test of one child box: entry distance in [0, tcut] or +inf.  (lo - o)/d is computed as
+// fma(lo, inv, -o inv), i.e. exactly for an origin perturbed by half an ulp; boxes are padded by 2^-18 of the
+// scene's extent at build, which covers that.  inv = 1 / d with |d| clamped to >= 2^-80 (bvh_inv): a zero
+// component then gives huge but finite plane distances of the right sign (no inf - inf), and the clamped ray
+// leaves a slab it starts in only after ~pad / 2^-80, far beyond any distance in a scene.
+__device__ __forceinline__ float child_entry(float lx, float hx, float ly, float hy, float lz, float hz, V3 inv, V3 oi,
+                                             float tcut) {
+    const float x0 = __builtin_fmaf(lx, inv.x, -oi.x), x1 = __builtin_fmaf(hx, inv.x, -oi.x);
+    const float y0 = __builtin_fmaf(ly, inv.y, -oi.y), y1 = __builtin_fmaf(hy, inv.y, -oi.y);
+    const float z0 = __builtin_fmaf(lz, inv.z, -oi.z), z1 = __builtin_fmaf(hz, inv.z, -oi.z);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.f));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tcut)) * 1.00000048f;
+    return tn <= tf ? tn : __builtin_inff();
+}
+__device__ __forceinline__ V3 bvh_inv(V3 d) {
+    const float e = 0x1p-80f;
+    return v3(1 / copysignf(fmaxf(fabsf(d.x), e), d.x), 1 / copysignf(fmaxf(fabsf(d.y), e), d.y),
+              1 / copysignf(fmaxf(fabsf(d.z), e), d.z));
+}
+__device__ __forceinline__ void cswap(float& ea, int& wa, float& eb, int& wb) {
+    const bool s = eb < ea;
+    const float e = s ? eb : ea;
+    const int w = s ? wb : wa;
+    eb = s ? ea : eb; wb = s ? wa : wb;
+    ea = e; wa = w;
+}
+__device__ __forceinline__ void decode_leaf(int w, int& lf, int& lc) {
+    lf = (w >> 4) & 0x7ffffff;
+    lc = (w & 15) + 1;
+}
+
+// closest hit over the BVH: returns the triangle id (or -1) with (b0, b1, b2, t); amb = the BFS must decide
+template <int KZ>
+__device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0,
+                                           float& rb1, float& rb2, float& rt, ctr_t& nn, ctr_t& nt, bool& amb) {
+    const float4* __restrict__ nodes = sc.bvh[set];
+    const float4* __restrict__ tiles = sc.btiles[set];
+    const V3 inv = bvh_inv(d);
+    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+    const TriRay R = make_triray<KZ>(o, d);
+    uint2* stk = g_bstk + threadIdx.x;
+    int sp = 0;
+    float cut = tMaxInit, t2 = __builtin_inff();
+    int best = -1, second = -1;
+    bool overflow = false;
+    int node = 0, lf = 0, lc = 0;
+    while (true) {
+        // node phase ("while-while"): open internal nodes nearest-first until this lane holds a leaf
+        while (lc == 0) {
+            if (node < 0) {
+                if (sp == 0) break;
+                const uint2 e = stk[--sp * kBlock];
+                if (__uint_as_float(e.y) > cut) continue;  // entered beyond the current cut: nothing to find there
+                const int w = (int)e.x;
+                if (w >= 0) node = w;
+                else decode_leaf(w, lf, lc);
+                continue;
+            }
+            const float4* N = nodes + 8 * (size_t)node;
+            const float4 LX = N[0], HX = N[1], LY = N[2], HY = N[3], LZ = N[4], HZ = N[5], CW = N[6];
+            nn += 4;
+            float e0 = child_entry(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, inv, oi, cut);
+            float e1 = child_entry(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, inv, oi, cut);
+            float e2 = child_entry(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, inv, oi, cut);
+            float e3 = child_entry(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, inv, oi, cut);
+            int w0 = __float_as_int(CW.x), w1 = __float_as_int(CW.y), w2 = __float_as_int(CW.z), w3 = __float_as_int(CW.w);
+            e0 = w0 == -1 ? __builtin_inff() : e0;
+            e1 = w1 == -1 ? __builtin_inff() : e1;
+            e2 = w2 == -1 ? __builtin_inff() : e2;
+            e3 = w3 == -1 ? __builtin_inff() : e3;
+            cswap(e0, w0, e1, w1); cswap(e2, w2, e3, w3); cswap(e0, w0, e2, w2); cswap(e1, w1, e3, w3);
+            cswap(e1, w1, e2, w2);
+            node = -1;
+            const float INF = __builtin_inff();
+            if (e3 < INF) { if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)w3, __float_as_uint(e3)); else overflow = true; }
+            if (e2 < INF) { if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)w2, __float_as_uint(e2)); else overflow = true; }
+            if (e1 < INF) { if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)w1, __float_as_uint(e1)); else overflow = true; }
+            if (e0 < INF) {
+                if (w0 >= 0) node = w0;
+                else decode_leaf(w0, lf, lc);
+            }
+        }
+        if (lc == 0) break;
+        for (int k = 0; k < lc; ++k) {
+            const float4* tp = tiles + 3 * (lf + k);
+            const float4 A = tp[0], B = tp[1], Cc = tp[2];
+            ++nt;
+            float b0, b1, b2, t;
+            if (tri_intersect<KZ>(R, cut, A, B, Cc, b0, b1, b2, t) && t < cut) {
+                if (best < 0 || t < rt) {
+                    t2 = best < 0 ? t2 : rt;
+                    second = best;
+                    best = __float_as_int(Cc.y);
+                    rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+                    const float c2 = t + 2.f * canon_window(t, sc.wabs);
+                    cut = c2 < cut ? c2 : cut;
+                } else if (t < t2) {
+                    second = __float_as_int(Cc.y);
+                    t2 = t;
+                }
+            }
+        }
+        lc = 0;
+    }
+    amb = overflow || (second >= 0 && t2 <= rt + canon_window(rt, sc.wabs));
+    return best;
+}
+
+// any hit over the BVH with a fixed tMax: 0 = occluded, -1 = not; amb = only window hits were found
+template <int KZ>
+__device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 d, float tMax, ctr_t& nn, ctr_t& nt,
+                                          bool& amb) {
+    const float4* __restrict__ nodes = sc.bvh[set];
+    const float4* __restrict__ tiles = sc.btiles[set];
+    const V3 inv = bvh_inv(d);
+    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+    const TriRay R = make_triray<KZ>(o, d);
+    const float sure = tMax - canon_window(tMax, sc.wabs);
+    uint2* stk = g_bstk + threadIdx.x;
+    int sp = 0;
+    bool window = false, overflow = false;
+    int node = 0, lf = 0, lc = 0;
+    while (true) {
+        while (lc == 0) {
+            if (node < 0) {
+                if (sp == 0) break;
+                const int w = (int)stk[--sp * kBlock].x;
+                if (w >= 0) node = w;
+                else decode_leaf(w, lf, lc);
+                continue;
+            }
+            const float4* N = nodes + 8 * (size_t)node;
+            const float4 LX = N[0], HX = N[1], LY = N[2], HY = N[3], LZ = N[4], HZ = N[5], CW = N[6];
+            nn += 4;
+            const int w[4] = {__float_as_int(CW.x), __float_as_int(CW.y), __float_as_int(CW.z), __float_as_int(CW.w)};
+            const bool h[4] = {w[0] != -1 && child_entry(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, inv, oi, tMax) < __builtin_inff(),
+                               w[1] != -1 && child_entry(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, inv, oi, tMax) < __builtin_inff(),
+                               w[2] != -1 && child_entry(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, inv, oi, tMax) < __builtin_inff(),
+                               w[3] != -1 && child_entry(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, inv, oi, tMax) < __builtin_inff()};
+            node = -1;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (!h[k]) continue;
+                if (node < 0 && lc == 0) {  // the first passing child is opened next, the others wait
+                    if (w[k] >= 0) node = w[k];
+                    else decode_leaf(w[k], lf, lc);
+                } else if (sp < kBvhStack) {
+                    stk[sp++ * kBlock] = make_uint2((unsigned)w[k], 0u);
+                } else {
+                    overflow = true;
+                }
+            }
+        }
+        if (lc == 0) break;
+        for (int k = 0; k < lc; ++k) {
+            const float4* tp = tiles + 3 * (lf + k);
+            ++nt;
+            float b0, b1, b2, t;
+            if (tri_intersect<KZ>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax) {
+                if (t < sure) { amb = false; return 0; }
+                window = true;
+            }
+        }
+        lc = 0;
+    }
+    amb = window || overflow;
+    return -1;
+}
+
+template <int QCAP, bool ANYHIT, int KZ, bool DFS>
+__device__ __forceinline__ int traverse_kz(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
+                                           float& b2, float& t, ctr_t& nn, ctr_t& nt, ctr_t& nfb) {
+    if constexpr (QCAP != 1) {
+        bool amb = false;
+        const int r = ANYHIT ? bvh_anyhit<KZ>(sc, set, o, d, tMax, nn, nt, amb)
+                             : bvh_closest<KZ>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, amb);
+        if (!amb) return r;
+        ++nfb;  // ambiguous (rare): the reference BFS decides, with the wave's other lanes done with the BVH
+    }
+    return traverse<QCAP, ANYHIT, KZ, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+}
+
 // When every active lane of the wave has the same dominant ray axis (camera rays) the watertight test's coordinate
 // permutation is resolved at compile time; otherwise per lane.
 template <int QCAP, bool ANYHIT, bool DFS = false>
 __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
-                                            float& b2, float& t, ctr_t& nn, ctr_t& nt) {
+                                            float& b2, float& t, ctr_t& nn, ctr_t& nt, ctr_t& nfb) {
     int kz = dominant_axis(d);
     uint64_t act = __ballot(true);
-    if (__ballot(kz == 2) == act) return traverse<QCAP, ANYHIT, 2, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 0) == act) return traverse<QCAP, ANYHIT, 0, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    if (__ballot(kz == 1) == act) return traverse<QCAP, ANYHIT, 1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
-    return traverse<QCAP, ANYHIT, -1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt);
+    if (__ballot(kz == 2) == act) return traverse_kz<QCAP, ANYHIT, 2, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, nfb);
+    if (__ballot(kz == 0) == act) return traverse_kz<QCAP, ANYHIT, 0, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, nfb);
+    if (__ballot(kz == 1) == act) return traverse_kz<QCAP, ANYHIT, 1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, nfb);
+    return traverse_kz<QCAP, ANYHIT, -1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, nfb);
 }
 
 // Register budgets (amdgpu_waves_per_eu) of the multi-level instantiations: 4 waves/SIMD (128 VGPRs) on the trace,
@@ -703,7 +909,7 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
     const int n = io.count ? *io.count : io.n;
-    ctr_t nn = 0, nt = 0, nh = 0, nr = 0;
+    ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
     // no block-level synchronisation here: each wave takes its own tickets (WaveChunks)
     WaveChunks chunks(io.ticket);
     for (int cb = chunks.next(); cb < n; cb = chunks.next())
@@ -711,7 +917,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
         float4 o4 = io.rayO[k], d4 = io.rayD[k];
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
         int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
-                                             b0, b1, b2, t, nn, nt);
+                                             b0, b1, b2, t, nn, nt, nfb);
         if (sc.n_shapes) {  // analytic shapes after the octree, running tMax; hitB = object-space point
             float tm = prim >= 0 ? t : 3.402823466e+38f;
             for (int si = 0; si < sc.n_shapes; ++si) {
@@ -732,6 +938,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
     count_add(ctr, C_TRIS, nt);
     count_add(ctr, C_HITS, nh);
     count_add(ctr, C_RAYS, nr);
+    count_add(ctr, C_FALLBACK, nfb);
 }
 
 // ======================================================================= K3 reference shading + film
@@ -852,7 +1059,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[kBlock / 64 + 1];
     const int n = *io.count;
-    ctr_t snn = 0, snt = 0, nsh = 0;
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
@@ -966,7 +1173,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         // pending contribution Ld stays live across the traversal.  No shadow queue in HBM.
         if (wantShadow) {
             float b0, b1, b2, t;
-            int hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt);
+            int hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt, sfb);
             ++nsh;
             if (hit < 0) {
                 float L[8];
@@ -987,6 +1194,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
+    count_add(ctr, C_SFALLBACK, sfb);
 }
 
 
@@ -997,7 +1205,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
 template <int QCAP, bool DFS>
 __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
     const int n = *shq.shCount;
-    ctr_t snn = 0, snt = 0, nsh = 0;
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     WaveChunks chunks(shq.shTicket);
     for (int cb = chunks.next(); cb < n; cb = chunks.next())
     for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
@@ -1006,7 +1214,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, 
         float4 o4 = shq.shO[k], d4 = shq.shD[k];
         float b0, b1, b2, t;
         int hit = traverse_any<QCAP, true, DFS>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), o4.w, b0, b1, b2,
-                                                t, snn, snt);
+                                                t, snn, snt, sfb);
         ++nsh;
         if (hit < 0) {
             int slot = __float_as_int(d4.w);
@@ -1022,6 +1230,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, 
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
+    count_add(ctr, C_SFALLBACK, sfb);
 }
 
 // ------------------------------------------------------------------- path mode, general scenes (§8 a21/a22)
@@ -1031,9 +1240,9 @@ __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, 
 // Semantics and sample-dimension order: oracle/rtcore.hpp LiPath, DESIGN.md §5.
 template <int QCAP>
 __device__ __forceinline__ bool scene_occluded(const DevScene& sc, V3 o, V3 d, float tmax, ctr_t& nn,
-                                               ctr_t& nt) {
+                                               ctr_t& nt, ctr_t& nfb) {
     float b0, b1, b2, t;
-    if (traverse_any<QCAP, true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt) >= 0) return true;
+    if (traverse_any<QCAP, true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt, nfb) >= 0) return true;
     for (int si = 0; si < sc.n_shapes; ++si) {
         DevShape sh = ldconst(sc.shapes, si);
         V3 ph;
@@ -1047,15 +1256,16 @@ __device__ __forceinline__ bool scene_occluded(const DevScene& sc, V3 o, V3 d, f
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const float4* o, const float4* d, int* out,
                                                      unsigned long long* ctr) {
-    ctr_t nn = 0, nt = 0, ns = 0;
+    ctr_t nn = 0, nt = 0, ns = 0, nfb = 0;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         float4 o4 = o[k], d4 = d[k];
-        out[k] = scene_occluded<QCAP>(sc, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, nn, nt) ? 1 : 0;
+        out[k] = scene_occluded<QCAP>(sc, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, nn, nt, nfb) ? 1 : 0;
         ++ns;
     }
     count_add(ctr, C_SNODES, nn);
     count_add(ctr, C_STRIS, nt);
     count_add(ctr, C_SHADOW, ns);
+    count_add(ctr, C_SFALLBACK, nfb);
 }
 
 template <int QCAP>
@@ -1066,7 +1276,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[kBlock / 64 + 1];
     const int n = *io.count;
-    ctr_t snn = 0, snt = 0, nsh = 0;
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = QCAP != 1;
     __shared__ int s_tk;
@@ -1244,7 +1454,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                 }
                                 if (ok) {
                                     ++nsh;
-                                    if (!scene_occluded<QCAP>(sc, po, wi, tmax, snn, snt)) {
+                                    if (!scene_occluded<QCAP>(sc, po, wi, tmax, snn, snt, sfb)) {
 #pragma unroll
                                         for (int i = 0; i < 8; ++i) {
                                             float Le = sc_le * dense_query(sp->D65, lam[i]);
@@ -1280,6 +1490,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
+    count_add(ctr, C_SFALLBACK, sfb);
 }
 
 // sensor + film for path mode (pixel-owned, index order)

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 typedef enum {
     RT_OK = 0,
@@ -199,8 +199,9 @@ typedef struct {
     int64_t samples;                 /* camera samples evaluated                         */
     int64_t rays;                    /* closest-hit rays traced                          */
     int64_t shadow_rays;             /* any-hit rays traced                              */
-    int64_t nodes_tested;            /* octree node box tests by closest-hit rays        */
-    int64_t tris_tested;             /* triangle tests by closest-hit rays               */
+    int64_t nodes_tested;            /* box tests executed by closest-hit rays (BVH child boxes, plus octree
+                                        nodes of BFS-traced rays)                        */
+    int64_t tris_tested;             /* triangle tests executed by closest-hit rays      */
     int64_t shadow_nodes_tested;     /* node box tests by any-hit (shadow) rays          */
     int64_t shadow_tris_tested;      /* triangle tests by any-hit (shadow) rays          */
     int64_t hits;                    /* closest-hit rays that hit                        */
@@ -209,6 +210,9 @@ typedef struct {
                                         are traced inside the path shade kernel */
     int64_t launches_trace;          /* closest-hit trace launches (per-launch averages) */
     int64_t launches_shade;          /* shade launches (path mode: includes the inline shadow rays) */
+    int64_t fallback_rays;           /* multi-level octrees: closest-hit rays the fast BVH traversal found
+                                        ambiguous (canonical rule), traced by the reference BFS */
+    int64_t shadow_fallback_rays;    /* the same for any-hit (shadow) rays                */
 } rt_stats;   /* multi-device contexts: every field summed over the devices */
 
 /* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */
@@ -228,6 +232,8 @@ typedef struct {
     int n_leaf_refs;
     int max_queue_groups;            /* host-computed bound of the BFS group queue       */
     int depth;
+    int bvh_nodes;                   /* multi-level octrees: 4-wide nodes of the fast traversal's BVH (0: none) */
+    int bvh_depth;
 } rt_octree_info;
 
 /* ---- lifecycle ---------------------------------------------------------------------------------- */

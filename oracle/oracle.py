@@ -87,6 +87,8 @@ def lib():
             "orc_trace": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), C.c_int, P(C.c_int), P(C.c_float), P(C.c_int64)], C.c_int),
             "orc_occluded": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_int)], C.c_int),
             "orc_samples": ([C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(capi.rt_sample_record)], C.c_int),
+            "orc_canonical_check": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int, C.c_int,
+                                     P(C.c_int64)], C.c_int),
             "orc_render": ([C.c_void_p, C.c_int, C.c_int, P(C.c_float), C.c_int, P(C.c_int64), P(C.c_int), C.c_int], C.c_int),
             "orc_resolve": ([C.c_void_p, P(C.c_float), P(C.c_uint8)], None),
             "orc_resolve_srgb": ([C.c_void_p, P(C.c_float), P(C.c_uint8)], None),
@@ -165,6 +167,18 @@ class OracleScene:
         occ = np.zeros(len(ro), np.int32)
         lib().orc_occluded(self.h, len(ro), fptr(ro), fptr(rd), fptr(tmax), iptr(occ))
         return occ
+
+    def canonical_check(self, ro, rd, tmax, use_cull=False, nthreads=None):
+        """Canonical fast-path rule vs the reference BFS on every ray; returns a dict of counts."""
+        ro = np.ascontiguousarray(ro, np.float32)
+        rd = np.ascontiguousarray(rd, np.float32)
+        tmax = np.ascontiguousarray(tmax, np.float32)
+        st = np.zeros(8, np.int64)
+        lib().orc_canonical_check(self.h, len(ro), fptr(ro), fptr(rd), fptr(tmax), int(use_cull),
+                                  nthreads or (os.cpu_count() or 1), st.ctypes.data_as(C.POINTER(C.c_int64)))
+        keys = ["closest_mismatch", "closest_ambiguous", "anyhit_mismatch", "anyhit_ambiguous", "hits", "occluded",
+                "rays", "first_mismatch"]
+        return dict(zip(keys, (int(x) for x in st)))
 
     def samples(self, pixel_ids, indices):
         from computational_ray_tracer_amd import capi

@@ -972,6 +972,79 @@ struct Octree {
         }
         return false;
     }
+
+    // ---- Canonical (order-independent) rule of the GPU's fast traversal.
+    // NOT the reference's algorithm: this restates the rule the GPU applies while walking its own BVH, so a CPU test
+    // can check, over millions of rays, that it always returns what Traverse / Occluded return.
+    //  * closest hit: t1 = the smallest t of any triangle passing the watertight test (any tMax above it), t2 the
+    //    next distinct triangle's; pruning with cut = t1 + 2 W(t1) is conservative (a triangle's hit point lies in
+    //    a leaf whose box the ray enters before that t).  If t2 > t1 + W(t1) the BFS must accept t1's triangle, with
+    //    the same (b, t), and nothing after it (every other hit is > W farther: the scaled tMax test and t < tMax
+    //    decide robustly); otherwise the ray is *ambiguous* and the caller runs the reference BFS.
+    //  * any hit (fixed tMax): a passing triangle with t < tMax - W(tMax) proves the BFS finds an occluder (its hit
+    //    leaf is entered before tMax); passing triangles only inside [tMax - W, tMax) are ambiguous -> BFS.
+    // W(t) = t 2^-16 + wabs, wabs = max |world coordinate| 2^-20: far above the few-ulp rounding of t and of the
+    // box entry distances, far below any real gap between distinct surfaces (Cornell light to ceiling: 0.1).
+    float wabs = 0;
+    static float Window(float t, float wabs) { return t * 0x1p-16f + wabs; }
+    void SetWindow() {
+        float m = 0;
+        for (const vec3& p : model->wpos) m = std::max(m, std::max(std::fabs(p.x), std::max(std::fabs(p.y), std::fabs(p.z))));
+        wabs = m * 0x1p-20f;
+    }
+    struct Canon { int tri = -1; TriIsect isect{}; int tri2 = -1; float t2 = std::numeric_limits<float>::infinity(); bool amb = false; };
+    Canon ClosestCanonical(const Ray& ray, bool use_cull) const {
+        Canon c;
+        float cut = std::numeric_limits<float>::max();
+        std::vector<int> stack{0};
+        while (!stack.empty()) {
+            int cur = stack.back();
+            stack.pop_back();
+            if (!IntersectP(nodes[cur].bounds, ray, cut)) continue;
+            if (!nodes[cur].leaf) {
+                for (int i = 7; i >= 0; --i) stack.push_back(nodes[cur].child[i]);
+                continue;
+            }
+            for (int t : nodes[cur].tris) {
+                if (t == c.tri || t == c.tri2) continue;  // the octree stores a triangle in every leaf it overlaps
+                if (use_cull && model->cull && !model->back_facing.empty() && model->back_facing[t]) continue;
+                TriIsect is;
+                if (!BasicIntersect(model->P(t, 0), model->P(t, 1), model->P(t, 2), ray, cut, &is) || !(is.t < cut)) continue;
+                if (c.tri < 0 || is.t < c.isect.t) {
+                    c.tri2 = c.tri; c.t2 = c.tri < 0 ? c.t2 : c.isect.t;
+                    c.tri = t; c.isect = is;
+                    cut = std::min(cut, is.t + 2 * Window(is.t, wabs));
+                } else if (is.t < c.t2) {
+                    c.tri2 = t; c.t2 = is.t;
+                }
+            }
+        }
+        c.amb = c.tri >= 0 && c.tri2 >= 0 && c.t2 <= c.isect.t + Window(c.isect.t, wabs);
+        return c;
+    }
+    // 1 occluded, 0 not, -1 ambiguous
+    int OccludedCanonical(const Ray& ray, float tMax) const {
+        const float sure = tMax - Window(tMax, wabs);
+        bool amb = false;
+        std::vector<int> stack{0};
+        while (!stack.empty()) {
+            int cur = stack.back();
+            stack.pop_back();
+            if (!IntersectP(nodes[cur].bounds, ray, tMax)) continue;
+            if (!nodes[cur].leaf) {
+                for (int i = 7; i >= 0; --i) stack.push_back(nodes[cur].child[i]);
+                continue;
+            }
+            for (int t : nodes[cur].tris) {
+                TriIsect is;
+                if (BasicIntersect(model->P(t, 0), model->P(t, 1), model->P(t, 2), ray, tMax, &is) && is.t < tMax) {
+                    if (is.t < sure) return 1;
+                    amb = true;
+                }
+            }
+        }
+        return amb ? -1 : 0;
+    }
 };
 
 // ------------------------------------------------------------------------------- camera

@@ -1,6 +1,7 @@
 // ORACLE C entry points — TEST INFRASTRUCTURE ONLY (loaded by tests/, __graft_entry__.smoke() and the
 // cpu_baseline leg of bench.py through ctypes).  Consumes the same POD descriptors as the product ABI
 // (include/rtmi355x.h) so a test can hand identical inputs to both sides.
+#include <array>
 #include <atomic>
 #include <thread>
 
@@ -277,6 +278,7 @@ void* orc_scene_create(const rt_scene_desc* sc, const rt_camera_desc* cam, const
     m.Prepare();
     m.ComputeBackFace({sc->cull_look[0], sc->cull_look[1], sc->cull_look[2]}, sc->cull_backfaces != 0);
     S.octree.Create(m, sc->octree_capacity > 0 ? sc->octree_capacity : Octree::TRIANGLE_CAPACITY_DEFAULT);
+    S.octree.SetWindow();
     S.tri_material.assign(sc->n_triangles, 0);
     if (sc->tri_material) S.tri_material.assign(sc->tri_material, sc->tri_material + sc->n_triangles);
     for (int i = 0; i < sc->n_materials; ++i) {
@@ -411,6 +413,53 @@ int orc_occluded(void* h, int n, const float* ro, const float* rd, const float* 
     for (int i = 0; i < n; ++i) {
         Ray r{{ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]}, {rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]}};
         occluded[i] = SceneOccluded(S, r, tmax[i]) ? 1 : 0;
+    }
+    return 0;
+}
+
+// Canonical-rule check (Octree::ClosestCanonical / OccludedCanonical): for every ray, the canonical
+// closest hit (the BFS only when ambiguous) against Traverse, and the canonical any hit against Occluded with tMax =
+// tmax[i].  stats[8]: closest mismatches, closest ambiguous, any-hit mismatches, any-hit ambiguous, closest hits,
+// occluded, rays, first mismatching ray (or -1).
+int orc_canonical_check(void* h, int n, const float* ro, const float* rd, const float* tmax, int use_cull, int nthreads,
+                        int64_t* stats) {
+    const Octree& T = static_cast<OracleScene*>(h)->S.octree;
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::array<int64_t, 8>> part(nthreads);
+    std::vector<std::thread> pool;
+    for (int th = 0; th < nthreads; ++th)
+        pool.emplace_back([&, th] {
+            std::array<int64_t, 8>& st = part[th];
+            st.fill(0);
+            st[7] = -1;
+            const int i0 = (int)((int64_t)n * th / nthreads), i1 = (int)((int64_t)n * (th + 1) / nthreads);
+            for (int i = i0; i < i1; ++i) {
+                Ray r{{ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]}, {rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]}};
+                Octree::Hit b = T.Traverse(r, use_cull != 0);
+                Octree::Canon c = T.ClosestCanonical(r, use_cull != 0);
+                bool same;
+                if (c.amb) {
+                    ++st[1];
+                    same = true;  // the fast path defers to the BFS
+                } else {
+                    same = c.tri == b.tri && (c.tri < 0 || std::memcmp(&c.isect, &b.isect, sizeof(TriIsect)) == 0);
+                }
+                if (!same) { ++st[0]; if (st[7] < 0) st[7] = i; }
+                st[4] += b.tri >= 0;
+                bool occ = T.Occluded(r, tmax[i]);
+                int oc = T.OccludedCanonical(r, tmax[i]);
+                if (oc < 0) ++st[3];
+                else if ((oc == 1) != occ) { ++st[2]; if (st[7] < 0) st[7] = i; }
+                st[5] += occ;
+                ++st[6];
+            }
+        });
+    for (auto& t : pool) t.join();
+    for (int k = 0; k < 7; ++k) stats[k] = 0;
+    stats[7] = -1;
+    for (auto& st : part) {
+        for (int k = 0; k < 7; ++k) stats[k] += st[k];
+        if (stats[7] < 0 && st[7] >= 0) stats[7] = st[7];
     }
     return 0;
 }
