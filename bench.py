@@ -29,7 +29,10 @@ from computational_ray_tracer_amd.distributed import FrameLoop  # noqa: E402
 from computational_ray_tracer_amd.renderer import Renderer  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-TRAFFIC_FILE = ROOT / "profiles" / "traffic.json"
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2 cycles at 2.4 GHz
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles (32 lanes/cycle x 2)")
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
+COUNTERS_DIR = ROOT / "profiles"
 
 
 def parse():
@@ -46,14 +49,15 @@ def parse():
     return p.parse_args()
 
 
-def kernel_rooflines(st, traffic):
-    """Per-kernel HBM roofline from the HIP-event launch times of the timed region.
+def kernel_rooflines(st, counters):
+    """Per-kernel HBM and VALU rooflines from HIP-event launch times (the single-lane pass: one launch at a time).
 
     Algorithmic bytes follow SURVEY.md §8(d): the per-ray HBM streams are `achieved` (k_trace_closest: 40 B per
-    ray cast; k_path_shade: 312 B per shaded bounce + 32 B per shadow ray); the §8(d) scene terms (32 B per node
-    box test + 40 B per triangle test) are reported beside them as `achieved_incl_scene` — on this 36-triangle
-    scene they are scalar-cache/L2 hits (the whole octree is 1.8 KB), so folding them into an HBM rate would
-    exceed the HBM peak.  `traffic` is the PMC-measured DRAM bytes per launch (profiles/traffic.json)."""
+    ray cast; k_path_shade: 312 B per shaded bounce + 32 B per shadow ray); the §8(d) scene terms (32 B per box
+    test + 40 B per triangle test actually executed) are reported beside them as `achieved_incl_scene` — they are
+    cache hits (the Cornell scene is 1.8 KB, the CFG3 BVH 1.7 MB + 4.7 MB of triangles), so folding them into an
+    HBM rate could exceed the HBM peak.  `traffic` is the PMC-measured DRAM bytes per launch and `valu` the
+    SQ_INSTS_VALU per launch over the same single-lane launch time, both from profiles/counters_<config>.json."""
     ks = {
         "k_trace_closest": (st["ms_trace"], st["launches_trace"], 40 * st["rays"],
                             32 * st["nodes_tested"] + 40 * st["tris_tested"]),
@@ -65,15 +69,62 @@ def kernel_rooflines(st, traffic):
         launches = max(1, launches)
         avg_s = ms / launches * 1e-3
         a = stream_b / launches / avg_s / 1e9
+        kc = (counters or {}).get(name, {})
         res[name] = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(a / HBM_PEAK_GBS, 4),
-                     "traffic": (traffic or {}).get(name, {}).get("dram_bytes_per_launch"),
+                     "traffic": kc.get("dram_bytes_per_launch"),
                      "kernel": name, "launches": launches, "avg_launch_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": int(stream_b / launches),
                      "scene_bytes_per_launch": int(scene_b / launches),
                      "achieved_incl_scene": round((stream_b + scene_b) / launches / avg_s / 1e9, 1),
                      "total_ms": round(ms, 3)}
+        if kc.get("valu_insts_per_launch"):
+            g = kc["valu_insts_per_launch"] / avg_s / 1e9
+            res[name]["valu"] = {"achieved": round(g, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                                 "frac": round(g / VALU_PEAK_GINST, 4),
+                                 "insts_per_launch": int(kc["valu_insts_per_launch"])}
     return res
+
+
+def single_lane_pass(cfg, world, rank, spp_per_step, steps):
+    """Per-kernel launch times with ONE batch in flight (RTMI_LANES=1): with two lanes a launch's HIP-event time
+    also covers the other lane's kernels sharing the CUs, so per-kernel rooflines come from this pass (the rocprof
+    kernel traces under profiles/ are single-lane too).  Untimed for `value`; same workload and step size."""
+    old = os.environ.get("RTMI_LANES")
+    os.environ["RTMI_LANES"] = "1"
+    try:
+        r1 = Renderer(cfg, device=torch.cuda.current_device())
+    finally:
+        if old is None:
+            del os.environ["RTMI_LANES"]
+        else:
+            os.environ["RTMI_LANES"] = old
+    r1.set_shard(32, world, rank)
+    W, H = cfg.film.res
+    film = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    spp = cfg.sampler.spp()
+    n = spp_per_step * world
+    i0 = 0
+
+    def step():
+        nonlocal i0
+        if i0 + n > spp:
+            i0 = 0
+        r1.render_pass_device(i0, i0 + n, film.data_ptr(), stream.cuda_stream)
+        i0 += n
+
+    step()
+    torch.cuda.synchronize()
+    r1.reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = r1.stats()
+    del r1
+    return st, dt
 
 
 def cpu_baseline(cfg, seconds):
@@ -196,26 +247,30 @@ def main():
     else:
         total_samples = float(st["samples"])
     value = total_samples / dt / 1e6
-    # roofline of the dominant kernel (most HIP-event time in the timed region)
-    traffic = None
-    if TRAFFIC_FILE.exists():
-        tj = json.loads(TRAFFIC_FILE.read_text())
-        if tj.get("config", "cornell") == a.config:  # PMC bytes are only valid for the workload they measured
-            traffic = tj.get("kernels")
-    rl = kernel_rooflines(st, traffic)
-    dom = max(rl, key=lambda k: rl[k]["total_ms"])
-    roofline = dict(rl[dom])
-    roofline["limiter"] = "VALU issue (octree box + watertight triangle tests); see DESIGN.md §Roofline"
-    # Two batches run concurrently on two streams (DESIGN.md §4 lanes), so a launch's HIP-event duration includes
-    # time it shares the CUs with the other lane's kernels; the node-level figure divides every kernel's §8(d)
-    # stream bytes (generate 96 B/sample, trace 40 B/ray, shade 312 B/bounce + 32 B/shadow ray, film 128 B/sample)
-    # by the wall time of the timed region.
+    # roofline of the dominant kernel (most HIP-event time), from a single-lane pass (see single_lane_pass)
+    counters = None
+    cf = COUNTERS_DIR / f"counters_{a.config}.json"
+    if cf.exists():  # PMC bytes / VALU instructions are only valid for the workload they measured
+        counters = json.loads(cf.read_text()).get("kernels")
+    roofline = {}
+    if rank == 0:
+        st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
+        rl = kernel_rooflines(st1, counters)
+        dom = max(rl, key=lambda k: rl[k]["total_ms"])
+        roofline = dict(rl[dom])
+        roofline["basis"] = (f"single-lane pass (RTMI_LANES=1, {a.steps} steps, {dt1 / a.steps * 1e3:.3f} ms/step): "
+                             f"{roofline['launches'] / a.steps:g} launches per step x {roofline['avg_launch_ms']} ms")
+        roofline["ms_per_step_single_lane"] = round(dt1 / a.steps * 1e3, 3)
+        roofline["limiter"] = "VALU issue and memory latency (box + watertight triangle tests); see DESIGN.md §4"
+        roofline["other_kernels"] = {k: v for k, v in rl.items() if k != dom}
+    # Two batches run concurrently on two streams in the timed region (DESIGN.md §4 lanes); the node-level figure
+    # divides every kernel's §8(d) stream bytes (generate 96 B/sample, trace 40 B/ray, shade 312 B/bounce + 32 B per
+    # shadow ray, film 128 B/sample) by the wall time of the timed region.
     node_b = 96 * st["samples"] + (40 + 312) * st["rays"] + 32 * st["shadow_rays"] + 128 * st["samples"]
     node_a = node_b / dt / 1e9
     roofline["node"] = {"achieved": round(node_a, 1), "frac": round(node_a / HBM_PEAK_GBS, 4),
                         "bytes_per_step": int(node_b / a.steps), "lanes": int(os.environ.get("RTMI_LANES", "2")),
                         "basis": "all kernels' algorithmic stream bytes / wall time of the timed region"}
-    roofline["other_kernels"] = {k: v for k, v in rl.items() if k != dom}
     out = {
         "metric": "Msamples/s (whole node) at 1920x1080; achieved HBM GB/s vs roofline",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -227,7 +282,8 @@ def main():
         "roofline": roofline,
         "stage_ms": {k: round(st[k], 2) for k in ("ms_generate", "ms_trace", "ms_shade", "ms_shadow", "ms_film")},
         "counters": {k: st[k] for k in ("samples", "rays", "shadow_rays", "nodes_tested", "tris_tested",
-                                        "shadow_nodes_tested", "shadow_tris_tested", "hits")},
+                                        "shadow_nodes_tested", "shadow_tris_tested", "hits", "fallback_rays",
+                                        "shadow_fallback_rays")},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds)

@@ -434,10 +434,8 @@ struct Work {
     size_t cap = 0;
     float4 *rayO = nullptr, *rayD = nullptr, *lamA = nullptr, *lamB = nullptr, *pdfA = nullptr, *pdfB = nullptr;
     float4* hitB = nullptr;
-    float4 *betaA = nullptr, *betaB = nullptr, *LA = nullptr, *LB = nullptr;
-    int *slot = nullptr, *hitPrim = nullptr, *dim = nullptr;
-    float* prevPdf = nullptr;
-    uint4* rng = nullptr;
+    float4* rec = nullptr;     // path mode: one 128-B record per slot (rt_internal.h R_*)
+    int *slot = nullptr, *hitPrim = nullptr;
     int* d_qcount = nullptr;   // queue q's counters at [q * kQRegion + kQLen / kQTraceTicket / ...] (rt_internal.h)
     // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers
     float4 *sO = nullptr, *sD = nullptr;
@@ -494,6 +492,7 @@ struct rt_ctx {
     // the inline any-hit, kept as a parity-tested option), depth first (RTMI_SHADOW_DFS, exact any-hit, §6)
     int shadow_queue = 0;
     int shadow_dfs = 1;
+    int sort_rays = 1;         // RTMI_SORT=0: no coherence sort (A/B)
     hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
     size_t batch_samples = 0;  // samples in flight per batch (0: 8 Mi path / 16 Mi reference; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
@@ -599,15 +598,11 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
 void free_workspace(Work& w) {
     free_sort_workspace(w);
     free_shadow_workspace(w);
-    void* ptrs[] = {w.rayO, w.rayD, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.betaA, w.betaB,
-                    w.LA, w.LB, w.slot, w.hitPrim, w.dim, w.rng, w.prevPdf};
+    void* ptrs[] = {w.rayO, w.rayD, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.rec, w.slot, w.hitPrim};
     for (void* p : ptrs)
         if (p) hipFree(p);
-    w.rayO = w.rayD = w.lamA = w.lamB = w.pdfA = w.pdfB = w.hitB = nullptr;
-    w.betaA = w.betaB = w.LA = w.LB = nullptr;
-    w.slot = w.hitPrim = w.dim = nullptr;
-    w.rng = nullptr;
-    w.prevPdf = nullptr;
+    w.rayO = w.rayD = w.lamA = w.lamB = w.pdfA = w.pdfB = w.hitB = w.rec = nullptr;
+    w.slot = w.hitPrim = nullptr;
     w.cap = 0;
 }
 void free_ring(Work& w) {
@@ -650,18 +645,17 @@ int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
         HIPCHK(c, hipEventCreateWithFlags(&w.film_done, hipEventDisableTiming));
     }
     if ((rc = ensure_ring(c, w))) return rc;
-    if (w.cap >= n && (!path || w.betaA)) return RT_OK;
+    if (w.cap >= n && (path ? w.rec != nullptr : w.lamA != nullptr)) return RT_OK;
     free_workspace(w);
     // path mode: queue arrays hold 2 ping-pong queues of n entries each
     size_t nq = path ? 2 * n : n;
     HIPCHK(c, dalloc(&w.rayO, nq)); HIPCHK(c, dalloc(&w.rayD, nq)); HIPCHK(c, dalloc(&w.slot, nq));
-    HIPCHK(c, dalloc(&w.lamA, n)); HIPCHK(c, dalloc(&w.lamB, n));
     HIPCHK(c, dalloc(&w.pdfA, n)); HIPCHK(c, dalloc(&w.pdfB, n));
     HIPCHK(c, dalloc(&w.hitB, n)); HIPCHK(c, dalloc(&w.hitPrim, n));
     if (path) {
-        HIPCHK(c, dalloc(&w.betaA, n)); HIPCHK(c, dalloc(&w.betaB, n));
-        HIPCHK(c, dalloc(&w.LA, n)); HIPCHK(c, dalloc(&w.LB, n));
-        HIPCHK(c, dalloc(&w.dim, n)); HIPCHK(c, dalloc(&w.rng, n)); HIPCHK(c, dalloc(&w.prevPdf, n));
+        HIPCHK(c, dalloc(&w.rec, (size_t)kRecF4 * n));
+    } else {
+        HIPCHK(c, dalloc(&w.lamA, n)); HIPCHK(c, dalloc(&w.lamB, n));
     }
     w.cap = n;
     return RT_OK;
@@ -963,9 +957,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             int nIdx = std::min(B, ie - b0);
             int nS = nIdx * c->n_work;
             SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
-            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, nullptr, w.dim, nullptr,
-                      w.betaA, w.betaB, w.LA, w.LB};
-            go.lean = 0;
+            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, RecView{nullptr, 0, 0}, 0};
             hipEvent_t e0 = ev_start(c, st);
             HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, st, ST_GEN, e0);
@@ -991,7 +983,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const int lanes = std::max(1, std::min(std::min(c->lanes, kLanes), nbatch));
     // multi-level octrees: coherence-sort each bounce's rays (rt_sort.hip); on the single-leaf Cornell box the sort
     // costs more than it saves (1110 -> 720 Msamples/s)
-    const bool sort_rays = c->dsc.qcap != 1;
+    const bool sort_rays = c->dsc.qcap != 1 && c->sort_rays;
     for (int l = 0; l < lanes; ++l) {
         if ((rc = ensure_workspace(c, c->ws[l], nmax, true))) return rc;
         if (sort_rays && (rc = ensure_sort_workspace(c, c->ws[l], nmax))) return rc;
@@ -1015,6 +1007,11 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
         for (int l = 1; l < lanes; ++l) HIPCHK(c, hipStreamWaitEvent(c->ws[l].stream, c->ws[0].film_done, 0));
     }
     const size_t qs = nmax;  // one queue
+    // slot state layout (rt_internal.h RecView): records for multi-level scenes (sorted, scattered slots), SoA for
+    // single-leaf ones (slots stay in queue order)
+    const bool records = c->dsc.qcap != 1;
+    const size_t rec_fs = records ? 1 : nmax;
+    const unsigned rec_ss = records ? (unsigned)kRecF4 : 1u;
     int last_film = -1;      // lane of the most recent film launch
     for (int g0 = ib; g0 < ie; g0 += B * lanes) {
         int nIdx[kLanes] = {0}, cur[kLanes] = {0};
@@ -1023,12 +1020,11 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             if (b0 >= ie) break;
             Work& w = c->ws[l];
             hipStream_t s = lstream(l);
+            const RecView rv{w.rec, rec_fs, rec_ss};
             nIdx[l] = std::min(B, ie - b0);
             int nS = nIdx[l] * c->n_work;
             SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
-            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, w.rng, w.dim,
-                      c->dsc.full ? w.prevPdf : nullptr, w.betaA, w.betaB, w.LA, w.LB};
-            go.lean = lean ? 1 : 0;
+            GenOut go{w.rayO, w.rayD, w.slot, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0};
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, s, ST_GEN, e0);
@@ -1042,6 +1038,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             for (int l = 0; l < lanes && nIdx[l] > 0; ++l) {
                 Work& w = c->ws[l];
                 hipStream_t s = lstream(l);
+                const RecView rv{w.rec, rec_fs, rec_ss};
                 SampleIds ids{c->d_work, c->n_work, g0 + l * B, nullptr, nullptr};
                 int nxt = cur[l] ^ 1;
                 const float4* cO = w.rayO + (size_t)cur[l] * qs;
@@ -1075,10 +1072,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
                 pio.nO = w.rayO + (size_t)nxt * qs; pio.nD = w.rayD + (size_t)nxt * qs;
                 pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt;
-                pio.rng = w.rng; pio.dim = w.dim; pio.betaA = w.betaA; pio.betaB = w.betaB;
-                pio.LA = w.LA; pio.LB = w.LB;
-                pio.lamA = w.lamA; pio.lamB = w.lamB; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
-                pio.prevPdf = w.prevPdf;
+                pio.rec = RecView{w.rec, rv.fs, rv.ss}; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 pio.ticket = dyn ? qc_cur + kQShadeTicket : nullptr;
                 ShadowQueueIO sqio{};
@@ -1101,8 +1095,9 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
         for (int l = 0; l < lanes && nIdx[l] > 0; ++l) {
             Work& w = c->ws[l];
             hipStream_t s = lstream(l);
+            const RecView rv{w.rec, rec_fs, rec_ss};
             if (last_film >= 0 && last_film != l) HIPCHK(c, hipStreamWaitEvent(s, c->ws[last_film].film_done, 0));
-            PathFilmIO fio{c->d_work, c->n_work, nIdx[l], w.LA, w.LB, w.lamA, w.lamB, w.pdfA, w.pdfB, film};
+            PathFilmIO fio{c->d_work, c->n_work, nIdx[l], RecView{w.rec, rv.fs, rv.ss}, w.pdfA, w.pdfB, film};
             fio.lean = lean ? 1 : 0;
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_path_film(s, 0, c->d_spec, fd, fio, c->d_ctr));
@@ -1375,6 +1370,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_LANES")) c->lanes = std::max(1, std::min(kLanes, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_SHADOW_QUEUE")) c->shadow_queue = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SHADOW_DFS")) c->shadow_dfs = std::atoi(e);
+    if (const char* e = std::getenv("RTMI_SORT")) c->sort_rays = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
     c->hs.init();
     if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->ws[0].d_qcount, 2 * kQRegion) != hipSuccess ||
@@ -2101,8 +2097,8 @@ static int impl_rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, con
         hipMemcpy(dp, pixel_ids, 4 * (size_t)n, hipMemcpyHostToDevice);
         hipMemcpy(di, indices, 4 * (size_t)n, hipMemcpyHostToDevice);
         SampleIds ids{nullptr, 1, 0, dp, di};
-        GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].slot, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA, c->ws[0].pdfB, nullptr, nullptr, nullptr,
-                  nullptr, nullptr, nullptr, nullptr};
+        GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].slot, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA,
+                  c->ws[0].pdfB, RecView{nullptr, 0, 0}, 0};
         DevFilm fd = dev_film(c);
         TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, nullptr, n, c->cull ? 1 : 0, c->ws[0].hitB, c->ws[0].hitPrim};
         ShadeRefIO sio = shade_ref_io(c);

@@ -140,10 +140,7 @@ __device__ __forceinline__ int queue_append(int* counter, bool pred, int* lds) {
     else return block_append(counter, pred, lds);
 }
 
-// the PCG increment of a path never changes after generation: only the 8-byte state half is written back
-__device__ __forceinline__ void store_rng_state(uint4* rng, int slot, uint64_t state) {
-    reinterpret_cast<uint2*>(rng)[2 * slot] = make_uint2((uint32_t)state, (uint32_t)(state >> 32));
-}
+
 typedef unsigned long long ctr_t;
 __device__ __forceinline__ void count_add(unsigned long long* ctr, int slot, unsigned long long v) {
 #pragma unroll
@@ -179,6 +176,26 @@ __device__ __forceinline__ void load8_or_zero(const float4* a, const float4* b, 
 __device__ __forceinline__ void store8(float4* a, float4* b, int s, const float v[8]) {
     a[s] = make_float4(v[0], v[1], v[2], v[3]);
     b[s] = make_float4(v[4], v[5], v[6], v[7]);
+}
+// fields of a slot's path state (rt_internal.h RecView, R_*)
+__device__ __forceinline__ float4* recf(const RecView& r, int slot, int f) {
+    return r.p + (size_t)f * r.fs + (size_t)slot * r.ss;
+}
+__device__ __forceinline__ void rload8(const RecView& r, int slot, int f, float v[8]) {
+    const float4* q = recf(r, slot, f);
+    load8(q, q + r.fs, 0, v);
+}
+__device__ __forceinline__ void rload8_or_zero(const RecView& r, int slot, int f, float v[8], bool zero) {
+    const float4* q = recf(r, slot, f);
+    load8_or_zero(q, q + r.fs, 0, v, zero);
+}
+__device__ __forceinline__ void rstore8(const RecView& r, int slot, int f, const float v[8]) {
+    float4* q = recf(r, slot, f);
+    store8(q, q + r.fs, 0, v);
+}
+__device__ __forceinline__ float rec_prev_pdf(const RecView& r, int slot) { return recf(r, slot, R_MISC)->y; }
+__device__ __forceinline__ void rec_set_prev_pdf(const RecView& r, int slot, float p) {
+    reinterpret_cast<float*>(recf(r, slot, R_MISC))[1] = p;
 }
 
 // ===================================================================================== K1 generate
@@ -261,19 +278,21 @@ __global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevC
         out.rayO[s] = make_float4(wo[0], wo[1], wo[2], 0.f);
         out.rayD[s] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
         out.slot[s] = s;
-        store8(out.lamA, out.lamB, s, lam);
         if (!out.lean) store8(out.pdfA, out.pdfB, s, pdf);
-        if (out.rng) {
-            out.rng[s] = make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
-                                    (uint32_t)(sm.rng.inc >> 32));
-            out.dim[s] = sm.dim;
+        if (out.rec.p) {  // path mode: the slot's state
+            rstore8(out.rec, s, R_LAM, lam);
+            *reinterpret_cast<uint4*>(recf(out.rec, s, R_RNG)) =
+                make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
+                           (uint32_t)(sm.rng.inc >> 32));
+            *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, 0.f);  // (dimension, prevPdf 0)
             if (!out.lean) {
-                out.betaA[s] = make_float4(1.f, 1.f, 1.f, 1.f);
-                out.betaB[s] = make_float4(1.f, 1.f, 1.f, 1.f);
-                out.LA[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-                out.LB[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+                const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                rstore8(out.rec, s, R_BETA, one);
+                rstore8(out.rec, s, R_L, zero);
             }
-            if (out.prevPdf) out.prevPdf[s] = 0.f;
+        } else {
+            store8(out.lamA, out.lamB, s, lam);
         }
     }
 }
@@ -1027,14 +1046,15 @@ __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevF
     int pixel, index, x, y;
     sample_of(ids, slot, pixel, index);
     pixel_xy(film, pixel, x, y);
-    const uint4 rs = io.rng[slot];
+    const uint4 rs = *reinterpret_cast<const uint4*>(recf(io.rec, slot, R_RNG));
     sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
     sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
-    sm.px = x; sm.py = y; sm.index = index; sm.dim = io.dim[slot];
+    sm.px = x; sm.py = y; sm.index = index; sm.dim = __float_as_int(recf(io.rec, slot, R_MISC)->x);
 }
+// the PCG increment of a path never changes after generation: only the 8-byte state half is written back
 __device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm) {
-    store_rng_state(io.rng, slot, sm.rng.state);
-    io.dim[slot] = sm.dim;
+    *reinterpret_cast<uint2*>(recf(io.rec, slot, R_RNG)) = make_uint2((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32));
+    *reinterpret_cast<int*>(recf(io.rec, slot, R_MISC)) = sm.dim;
 }
 // cosine-hemisphere direction (Sampling.h:449-454) in the pbrt CoordinateSystem frame of nrm; false when z == 0
 __device__ __forceinline__ bool cosine_bounce(float u0, float u1, V3 nrm, V3& wi, float& z) {
@@ -1080,12 +1100,12 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
             const int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
-                load8(io.lamA, io.lamB, slot, lam);
+                rload8(io.rec, slot, R_LAM, lam);
                 if (d0) {
 #pragma unroll
                     for (int i = 0; i < 8; ++i) beta[i] = 1.f;
                 } else {
-                    load8(io.betaA, io.betaB, slot, beta);
+                    rload8(io.rec, slot, R_BETA, beta);
                 }
                 float4 P0 = sc.triWorld[3 * prim], P1 = sc.triWorld[3 * prim + 1], P2 = sc.triWorld[3 * prim + 2];
                 V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
@@ -1097,10 +1117,10 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                 if (mt.w > 0) {
                     if (io.depth == 0 && vdot(ng, rayd) < 0) {
                         float L[8];
-                        load8_or_zero(io.LA, io.LB, slot, L, d0);
+                        rload8_or_zero(io.rec, slot, R_L, L, d0);
 #pragma unroll
                         for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.w * dense_query(sp->D65, lam[i]));
-                        store8(io.LA, io.LB, slot, L);
+                        rstore8(io.rec, slot, R_L, L);
                         storedL = true;
                     }
                 } else if (io.depth < io.max_depth) {
@@ -1148,7 +1168,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                     if (cosine_bounce(u0, u1, nrm, wi, z)) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) beta[i] *= R[i];
-                        store8(io.betaA, io.betaB, slot, beta);
+                        rstore8(io.rec, slot, R_BETA, beta);
                         wantNext = true;
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
@@ -1177,16 +1197,16 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
             ++nsh;
             if (hit < 0) {
                 float L[8];
-                load8_or_zero(io.LA, io.LB, slot, L, d0);
+                rload8_or_zero(io.rec, slot, R_L, L, d0);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) L[i] += Ld[i];
-                store8(io.LA, io.LB, slot, L);
+                rstore8(io.rec, slot, R_L, L);
                 storedL = true;
             }
         }
         if (d0 && slot >= 0 && !storedL) {
             const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            store8(io.LA, io.LB, slot, z);
+            rstore8(io.rec, slot, R_L, z);
         }
         const int pn = queue_append<WAVE>(io.nCount, wantNext, lds);
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
@@ -1221,10 +1241,10 @@ __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, 
             float4 la = shq.shLA[k], lb = shq.shLB[k];
             const float Ld[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
             float L[8];
-            load8(io.LA, io.LB, slot, L);
+            rload8(io.rec, slot, R_L, L);
 #pragma unroll
             for (int i = 0; i < 8; ++i) L[i] += Ld[i];
-            store8(io.LA, io.LB, slot, L);
+            rstore8(io.rec, slot, R_L, L);
         }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1292,9 +1312,9 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
             int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8], L[8];
-                load8(io.lamA, io.lamB, slot, lam);
-                load8(io.betaA, io.betaB, slot, beta);
-                load8(io.LA, io.LB, slot, L);
+                rload8(io.rec, slot, R_LAM, lam);
+                rload8(io.rec, slot, R_BETA, beta);
+                rload8(io.rec, slot, R_L, L);
                 float4 o4 = io.rayO[k], d4 = io.rayD[k];
                 V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
                 V3 rayd = vnorm(rdw);
@@ -1330,7 +1350,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                     lidx = s.light;
                 }
                 const DevMaterial mt = sc.materials[mid];
-                float prevPdf = io.prevPdf[slot];
+                float prevPdf = rec_prev_pdf(io.rec, slot);
                 if (mt.emit > 0) {  // one-sided pure emitter, ends the path
                     if (front) {
                         if (prevPdf == 0) {
@@ -1348,7 +1368,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                     L[i] += (beta[i] * (mt.emit * dense_query(sp->D65, lam[i]))) * wb;
                             }
                         }
-                        store8(io.LA, io.LB, slot, L);
+                        rstore8(io.rec, slot, R_L, L);
                     }
                 } else if (io.depth < io.max_depth) {
                     float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
@@ -1358,12 +1378,12 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                     if (mt.type == 1) {  // perfect mirror: no sampler draws
 #pragma unroll
                         for (int i = 0; i < 8; ++i) beta[i] *= R[i];
-                        store8(io.betaA, io.betaB, slot, beta);
+                        rstore8(io.rec, slot, R_BETA, beta);
                         V3 po = vadd(p, vmul(nrm, off)), wi = reflect_dir(rayd, nrm);
                         wantNext = true;
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                        io.prevPdf[slot] = 0.f;
+                        rec_set_prev_pdf(io.rec, slot, 0.f);
                     } else {
                         Smp sm;
                         restore_sampler(ids, film, io, slot, sm);
@@ -1393,14 +1413,14 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                             } else {
 #pragma unroll
                                 for (int i = 0; i < 8; ++i) beta[i] /= (etap * etap);
-                                store8(io.betaA, io.betaB, slot, beta);
+                                rstore8(io.rec, slot, R_BETA, beta);
                                 po = vsub(p, vmul(nrm, off));
                                 wi = wt;
                             }
                             wantNext = true;
                             nO = make_float4(po.x, po.y, po.z, 0.f);
                             nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                            io.prevPdf[slot] = 0.f;
+                            rec_set_prev_pdf(io.rec, slot, 0.f);
                         } else {  // Lambert: NEE per light, then a cosine-hemisphere bounce
                             V3 po = vadd(p, vmul(nrm, off));
                             for (int li = 0; li < sc.n_lights; ++li) {
@@ -1463,7 +1483,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                     }
                                 }
                             }
-                            store8(io.LA, io.LB, slot, L);
+                            rstore8(io.rec, slot, R_L, L);
                             // cosine-hemisphere bounce (Sampling.h:449-454), pbrt CoordinateSystem frame
                             float u0, u1;
                             sm.get2d(smp, u0, u1);
@@ -1472,11 +1492,11 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                             if (cosine_bounce(u0, u1, nrm, wi, z)) {
 #pragma unroll
                                 for (int i = 0; i < 8; ++i) beta[i] *= R[i];
-                                store8(io.betaA, io.betaB, slot, beta);
+                                rstore8(io.rec, slot, R_BETA, beta);
                                 wantNext = true;
                                 nO = make_float4(po.x, po.y, po.z, 0.f);
                                 nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                                io.prevPdf[slot] = z * InvPi;
+                                rec_set_prev_pdf(io.rec, slot, z * InvPi);
                             }
                         }
                         save_sampler(io, slot, sm);
@@ -1503,14 +1523,14 @@ __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevF
         for (int i = 0; i < io.n_index; ++i) {
             int s = i * io.n_pixels + j;
             float lam[8], pdf[8], L[8], rgb[3];
-            load8(io.lamA, io.lamB, s, lam);
+            rload8(io.rec, s, R_LAM, lam);
             if (io.lean) {
 #pragma unroll
                 for (int w = 0; w < 8; ++w) pdf[w] = visible_pdf(lam[w]);  // the value k_generate would have stored
             } else {
                 load8(io.pdfA, io.pdfB, s, pdf);
             }
-            load8(io.LA, io.LB, s, L);
+            rload8(io.rec, s, R_L, L);
             to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
             const float w = 1.0f;
             f.x += w * gclamp(rgb[0], 0.0f, 1.0f);

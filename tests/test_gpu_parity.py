@@ -543,3 +543,83 @@ def test_full_size_workload_sampled_pixels_bitexact(oracle_lib, kind, i0, i1):
     assert np.all(np.isfinite(fg)) and np.all(fg >= 0)
     assert np.all(fg[:, 3] == fg[0, 3]) and fg[0, 3] > 0
     assert g.stats()["samples"] >= npx * (i1 - i0)
+
+
+@pytest.mark.parametrize("kind", ["path", "reference"])
+def test_independent_sampler_bitexact(oracle_lib, kind):
+    """IndependentSampler (samplers.h:38-62: PCG32 per pixel, Advance(index·65536 + dim), every Get1D/Get2D a
+    fresh draw) on the Cornell path integrator and on the CFG0 reference integrator: films and, in reference mode,
+    the per-sample records (λ, pdf, ray, hit, L, rgb) bit-exact (tolerance 0)."""
+    if kind == "path":
+        cfg = scene.cfg_cornell(res=(48, 40), spp_side=2)
+    else:
+        cfg = scene.cfg0_reference(res=(64, 64), frequency=16, n_index=5)
+    cfg.sampler = scene.IndependentSampler(samples_per_pixel=7, seed=3)
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    fg = g.render_pass(0, 5)
+    fo = o.render(0, 5)
+    assert np.array_equal(bits(fg), bits(fo))
+    if kind == "reference":
+        rng = np.random.default_rng(2)
+        pix = rng.integers(0, 64 * 64, 4000)
+        idx = rng.integers(0, 50, 4000)          # indices beyond spp are fine for the independent sampler
+        a = records_to_arrays(g.samples(pix, idx))
+        b = records_to_arrays(o.samples(pix, idx))
+        for k in a:
+            assert np.array_equal(bits(a[k]), bits(b[k])), k
+
+
+def _triangle_simple_scene():
+    """Cornell box + two TriangleSimple shapes (Shapes.h:760-907): one floating in the box, one in the back wall's
+    plane (world z = 559.2: object y, Shapes.h:178), so rays to the back wall hit both at (nearly) the same t and
+    the shape's `t >= tMax` rejection (Shapes.h:866) decides against it on ties."""
+    cfg = scene.cfg_cornell(res=(48, 40), spp_side=2)
+    m = cfg.model
+    mats = list(m.materials)
+    mid = len(mats)
+    mats.append((scene.CORNELL_RED, 0.0, capi.RT_MAT_DIFFUSE, 0.0))
+    m.materials = mats
+    m.shapes = [scene.TriangleSimple(scene.translate((0.0, 0.0, 0.0)), mid,
+                                     p=((150.0, 250.0, 200.0), (420.0, 300.0, 260.0), (260.0, 200.0, 470.0))),
+                scene.TriangleSimple(np.eye(4), mid, p=((100.0, 559.2, 100.0), (400.0, 559.2, 100.0),
+                                                         (250.0, 559.2, 450.0)))]
+    cfg.integrator = scene.Integrator(capi.RT_INTEGRATOR_PATH_MIS, max_depth=4)
+    return cfg
+
+
+def test_triangle_simple_trace_and_film_bitexact(oracle_lib):
+    cfg = _triangle_simple_scene()
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    ntri = len(cfg.model.indices)
+    rng = np.random.default_rng(9)
+    n = 30000
+    ro = np.stack([rng.uniform(5, 550, n), rng.uniform(5, 543, n), rng.uniform(5, 300, n)], 1).astype(np.float32)
+    tgt = np.where(rng.random((n, 1)) < 0.5,
+                   np.c_[rng.uniform(100, 400, n), rng.uniform(100, 450, n), np.full(n, 559.2)],   # back wall
+                   np.c_[rng.uniform(150, 420, n), rng.uniform(200, 300, n), rng.uniform(200, 470, n)])
+    rd = tgt - ro
+    rd = (rd / np.linalg.norm(rd, axis=1, keepdims=True)).astype(np.float32)
+    pg, bg = g.trace(ro, rd, False)
+    po, bo, _ = o.trace(ro, rd, False)
+    assert (po == ntri).mean() > 0.1           # the floating TriangleSimple
+    assert np.array_equal(pg, po)
+    assert np.array_equal(bits(bg), bits(bo))
+    t = np.where(po >= 0, bo[:, 3], 400.0)
+    tmax = (t * rng.choice([0.5, 0.999, 1.0, 1.001, 2.0], size=n)).astype(np.float32)
+    assert np.array_equal(g.occluded(ro, rd, tmax), o.occluded(ro, rd, tmax))
+    fg = g.render_pass(0, 4)
+    fo = o.render(0, 4)
+    assert np.array_equal(bits(fg), bits(fo))
+
+
+def test_bvh_fast_path_counters(cfg3_pair):
+    """Multi-level scenes trace through the BVH: executed box / triangle tests per ray far below
+    the reference BFS's, and the BFS fallback reserved to the rare ambiguous rays."""
+    cfg, g, _ = cfg3_pair
+    g.reset_stats()
+    g.render_pass(0, 2)
+    st = g.stats()
+    assert st["rays"] > 0 and st["shadow_rays"] > 0
+    assert st["tris_tested"] / st["rays"] < 12, st
+    assert st["fallback_rays"] <= 1e-3 * st["rays"], st
+    assert st["shadow_fallback_rays"] <= 1e-2 * st["shadow_rays"], st

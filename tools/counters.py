@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Per-launch PMC counters of the hot kernels -> profiles/counters_<config>.json (read by bench.py's roofline).
+
+usage: tools/counters.py --config cfg3 --tag r02c --dir gpurun_out/cnt_cfg3_r02c [--out profiles/counters_cfg3.json]
+
+The directory holds the single-lane (RTMI_LANES=1) rocprofv3 runs of `bench.py --config <config>` written by
+scripts/gpu_counters.sh: kt/ (kernel trace stats), fetch/ (FETCH_SIZE), write/ (WRITE_SIZE), sq/ (SQ_INSTS_VALU and
+the stall mix), each pass in a run of its own.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the
+bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.  Both count
+L2 misses to the fabric (Infinity-Cache hits included), so they bound HBM bytes from above.  SQ_INSTS_VALU counts
+wave-level VALU instructions (one per wave64 instruction issued).
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+from pathlib import Path
+
+KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_generate", "k_path_film", "k_ref_shade_film",
+           "k_sort_gather")
+
+
+def kname(raw):
+    base = raw.split("(")[0].replace("void ", "")
+    base = base.split("<")[0]
+    return base.split("::")[-1]
+
+
+def per_dispatch(d, counter):
+    vals = collections.defaultdict(list)
+    for f in glob.glob(str(Path(d) / "**" / "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            vals[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--config", required=True)
+    p.add_argument("--tag", required=True)
+    p.add_argument("--dir", required=True)
+    p.add_argument("--out")
+    a = p.parse_args()
+    d = Path(a.dir)
+    fetch = per_dispatch(d / "fetch", "FETCH_SIZE")
+    write = per_dispatch(d / "write", "WRITE_SIZE")
+    sq = {c: per_dispatch(d / "sq", c) for c in ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES",
+                                                  "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_WAVES")}
+    avg_ns = {}
+    for f in glob.glob(str(d / "kt" / "**" / "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            avg_ns[kname(r["Name"])] = float(r["AverageNs"])
+    out = {"tag": a.tag, "config": a.config, "lanes": 1,
+           "units": "per launch (mean over the run's dispatches); bytes; wave-level instructions",
+           "correction": "FETCH_SIZE x2 (gfx950 half-count of 16 B/lane reads), KiB -> bytes x1024",
+           "kernels": {}}
+    for k in KERNELS:
+        e = {}
+        if k in fetch and k in write:
+            f = sum(fetch[k]) / len(fetch[k])
+            w = sum(write[k]) / len(write[k])
+            e.update(dispatches=len(fetch[k]), fetch_kib_raw=round(f, 1), write_kib=round(w, 1),
+                     dram_bytes_per_launch=int((2 * f + w) * 1024))
+        for c, v in sq.items():
+            if k in v:
+                e[c.lower() + "_per_launch"] = round(sum(v[k]) / len(v[k]), 1)
+        if "sq_insts_valu_per_launch" in e:
+            e["valu_insts_per_launch"] = e["sq_insts_valu_per_launch"]
+        if k in avg_ns:
+            e["rocprof_avg_ns"] = round(avg_ns[k], 1)
+            if "dram_bytes_per_launch" in e:
+                e["dram_gbs"] = round(e["dram_bytes_per_launch"] / avg_ns[k], 1)
+        if e:
+            out["kernels"][k] = e
+    dst = Path(a.out or f"profiles/counters_{a.config}.json")
+    dst.write_text(json.dumps(out, indent=1) + "\n")
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
