@@ -280,7 +280,7 @@ def main():
                    "res": [W, H], "spp_total": spp, "spp_per_step_per_gpu": a.spp_per_step, "max_depth": 5,
                    "parallelism": f"pixel-tile shards x{world} (32x32 tiles) + RCCL film reduce"},
         "roofline": roofline,
-        "stage_ms": {k: round(st[k], 2) for k in ("ms_generate", "ms_trace", "ms_shade", "ms_shadow", "ms_film")},
+        "stage_ms": {k: round(st[k], 2) for k in ("ms_generate", "ms_sort", "ms_trace", "ms_shade", "ms_shadow", "ms_film")},
         "counters": {k: st[k] for k in ("samples", "rays", "shadow_rays", "nodes_tested", "tris_tested",
                                         "shadow_nodes_tested", "shadow_tris_tested", "hits", "fallback_rays",
                                         "shadow_fallback_rays")},

@@ -101,7 +101,8 @@ class rt_stats(C.Structure):
                 ("shadow_tris_tested", C.c_int64), ("hits", C.c_int64),
                 ("ms_generate", C.c_double), ("ms_trace", C.c_double), ("ms_shade", C.c_double),
                 ("ms_shadow", C.c_double), ("ms_film", C.c_double), ("launches_trace", C.c_int64),
-                ("launches_shade", C.c_int64), ("fallback_rays", C.c_int64), ("shadow_fallback_rays", C.c_int64)]
+                ("launches_shade", C.c_int64), ("fallback_rays", C.c_int64), ("shadow_fallback_rays", C.c_int64),
+                ("ms_sort", C.c_double)]
 
 
 class rt_sample_record(C.Structure):

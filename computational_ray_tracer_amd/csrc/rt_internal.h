@@ -228,11 +228,12 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
                            int* out, unsigned long long* ctr);
 struct SortRaysIO {
-    const float4* o; const float4* d; const int* slot;   // the queue (bin 0, contiguous)
+    const float4* o; const float4* d; const int* slot;   // the queue
     float4* so; float4* sd; int* ss;                      // the sorted side queue
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp; size_t temp_bytes;
     float4 lo, scale;                                     // origin quantisation: (p - lo) * scale in [0, 512)
+    int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin
     const int* count = nullptr;  // device queue length: sort all n slots, entries >= *count get the largest key
 };
 size_t sort_rays_temp_bytes(int nmax);

@@ -1,19 +1,16 @@
-// Coherence sort of a path-mode ray queue (multi-level octrees): rays are reordered by (direction octant, 27-bit
-// Morton code of the origin within the scene bounds) with a device radix sort, then gathered into a side queue
-// that the bounce's trace and shade kernels read.  Traversal results are per ray, so the order changes nothing
-// but which rays share a wave: neighbouring rays walk the same nodes and leaves (fewer divergent fetches).
+// Coherence sort of a path-mode ray queue (multi-level octrees): rays are reordered by (direction octant, direction
+// cell on an octahedral grid, Morton code of the origin within the scene bounds) with a stable device radix sort,
+// then gathered into a side queue that the bounce's trace and shade kernels read.  Traversal results are per ray, so
+// the order changes nothing but which rays share a wave: neighbouring rays walk the same nodes and leaves.  The sort
+// must be stable: within a key, rays keep their slot order, so the shade kernel's per-slot state reads stay close
+// (an atomic counting sort with the same keys, unstable, measured CFG3 463 -> 375 Msamples/s).
 #include <hipcub/hipcub.hpp>
 
 #include "rt_internal.h"
 
-// key = direction octant, then the octahedral position of the direction on a 2^kDirB x 2^kDirB grid, then a Morton
-// code of the origin with kOrgB bits per axis (DESIGN.md §6 key table: CFG3 83 / CFG4 55 Msamples/s, best measured)
 namespace rtmi {
 namespace {
 
-constexpr int kDirB = 3, kOrgB = 7;
-constexpr int kKeyBits = 3 + 2 * kDirB + 3 * kOrgB;
-static_assert(kKeyBits <= 32, "sort key wider than 32 bits");
 
 __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every third bit of 27
     v &= 0x1ffu;
@@ -24,10 +21,12 @@ __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every th
     return v;
 }
 
+// key = direction octant, then the octahedral position of the direction on a 2^B x 2^B grid, then a Morton code of
+// the origin with O bits per axis (DESIGN.md §6 key table)
 __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const float4* __restrict__ o,
                                                               const float4* __restrict__ d, float4 lo, float4 scale,
-                                                              unsigned* __restrict__ keys, int* __restrict__ vals,
-                                                              const int* __restrict__ count) {
+                                                              int kDirB, int kOrgB, unsigned* __restrict__ keys,
+                                                              int* __restrict__ vals, const int* __restrict__ count) {
     const int nv = count ? *count : n;  // slots past the device count sort last (largest key, stable)
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         if (k >= nv) {
@@ -72,7 +71,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int*
 size_t sort_rays_temp_bytes(int nmax) {
     size_t bytes = 0;
     hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned*)nullptr, (unsigned*)nullptr,
-                                       (const int*)nullptr, (int*)nullptr, nmax, 0, kKeyBits);
+                                       (const int*)nullptr, (int*)nullptr, nmax, 0, 32);
     return bytes;
 }
 
@@ -80,11 +79,12 @@ hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
     if (n <= 0) return hipSuccess;
     int g = (n + kBlockThreads - 1) / kBlockThreads;
     g = g < 8192 ? g : 8192;
-    hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.o, io.d, io.lo, io.scale, io.keys,
-                       io.vals, io.count);
+    const int key_bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
+    hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.o, io.d, io.lo, io.scale, io.dir_bits,
+                       io.org_bits, io.keys, io.vals, io.count);
     size_t bytes = io.temp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
-                                                      kKeyBits, st);
+                                                      key_bits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.o, io.d, io.slot, io.so,
                        io.sd, io.ss, io.count);

@@ -213,6 +213,7 @@ typedef struct {
     int64_t fallback_rays;           /* multi-level octrees: closest-hit rays the fast BVH traversal found
                                         ambiguous (canonical rule), traced by the reference BFS */
     int64_t shadow_fallback_rays;    /* the same for any-hit (shadow) rays                */
+    double ms_sort;                  /* multi-level octrees: coherence binning of bounce rays (HIP events) */
 } rt_stats;   /* multi-device contexts: every field summed over the devices */
 
 /* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */
