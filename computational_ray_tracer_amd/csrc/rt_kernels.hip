@@ -923,7 +923,10 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 // Register budgets (amdgpu_waves_per_eu) of the multi-level instantiations: 4 waves/SIMD (128 VGPRs) on the trace,
 // path shade and mixed-scene shade kernels (CFG3 121 -> 144, CFG4 87 -> 111 Msamples/s; 5 waves spill too much).
 // The single-leaf instantiations (107 / 125 VGPRs) are unbudgeted.
-#define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : 4)))
+#ifndef RT_MULTI_WAVES
+#define RT_MULTI_WAVES 4  // the one tuning macro left: variant builds for A/B (Makefile `variants`)
+#endif
+#define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_MULTI_WAVES)))
 
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
