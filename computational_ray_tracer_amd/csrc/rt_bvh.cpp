@@ -50,6 +50,7 @@ constexpr int kMaxLeaf = 8;
 
 struct Builder {
     const float* tri9;
+    float node_cost = 1.f;       // SAH: cost of opening a node relative to one triangle test
     std::vector<Box> pbox;
     std::vector<float> cen;      // 3 per primitive
     std::vector<int> perm;
@@ -102,7 +103,7 @@ struct Builder {
             }
         }
         const double parea = std::max(bb.area(), 1e-30);
-        const double split_cost = 1.0 + best / parea;  // node cost 1, triangle cost 1
+        const double split_cost = node_cost + best / parea;
         if (bax < 0 || (n <= kMaxLeaf && (double)n <= split_cost)) {
             if (n <= kMaxLeaf) {
                 nodes[id].first = b; nodes[id].count = n;
@@ -192,9 +193,7 @@ struct Collapse {
             nd[2 * a] = make_float4(lo[a][0], lo[a][1], lo[a][2], lo[a][3]);
             nd[2 * a + 1] = make_float4(hi[a][0], hi[a][1], hi[a][2], hi[a][3]);
         }
-        float w[4];
-        std::memcpy(w, word, 16);
-        nd[6] = make_float4(w[0], w[1], w[2], w[3]);
+        std::memcpy(&nd[6], word, 16);  // the child words' bits, never through float registers
         nd[7] = make_float4(0.f, 0.f, 0.f, 0.f);
         return me;
     }
@@ -202,7 +201,7 @@ struct Collapse {
 
 }  // namespace
 
-void build_bvh4(const float* tri9, const int* ids, int n, float pad, BvhData& out) {
+void build_bvh4(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out) {
     out.nodes.clear();
     out.tiles.clear();
     out.max_leaf = 0;
@@ -217,6 +216,7 @@ void build_bvh4(const float* tri9, const int* ids, int n, float pad, BvhData& ou
     }
     Builder B;
     B.tri9 = tri9;
+    B.node_cost = node_cost;
     B.pbox.resize(n);
     B.cen.resize(3 * (size_t)n);
     B.perm.resize(n);

@@ -492,7 +492,8 @@ struct rt_ctx {
     // the inline any-hit, kept as a parity-tested option), depth first (RTMI_SHADOW_DFS, exact any-hit, §6)
     int shadow_queue = 0;
     int shadow_dfs = 1;
-    int sort_rays = 1;         // RTMI_SORT=0: no coherence binning (A/B)
+    int sort_rays = 1;         // RTMI_SORT=0: no coherence sort (A/B)
+    float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
     int sort_dir_bits = 3, sort_org_bits = 4;  // sort key widths (RTMI_SORT_BITS="dir/org"; 3/7 3/2 2/5 within 2 %)
     hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
     size_t batch_samples = 0;  // samples in flight per batch (0: 8 Mi path / 16 Mi reference; RTMI_BATCH_SAMPLES)
@@ -1375,6 +1376,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_SHADOW_QUEUE")) c->shadow_queue = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SHADOW_DFS")) c->shadow_dfs = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT")) c->sort_rays = std::atoi(e);
+    if (const char* e = std::getenv("RTMI_BVH_CI")) c->bvh_node_cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) std::sscanf(e, "%d/%d", &c->sort_dir_bits, &c->sort_org_bits);
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
     c->hs.init();
@@ -1662,7 +1664,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
                 }
                 ids.push_back(t);
             }
-            build_bvh4(t9.data(), ids.data(), (int)ids.size(), pad, bvh[st]);
+            build_bvh4(t9.data(), ids.data(), (int)ids.size(), pad, c->bvh_node_cost, bvh[st]);
         }
     }
     c->info.n_nodes = nn;

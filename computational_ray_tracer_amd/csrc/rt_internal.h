@@ -124,7 +124,7 @@ struct BvhData {
     std::vector<float4> nodes, tiles;
     int depth = 0, max_leaf = 0;
 };
-void build_bvh4(const float* tri9, const int* ids, int n, float pad, BvhData& out);
+void build_bvh4(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out);
 
 }  // namespace rtmi
 
