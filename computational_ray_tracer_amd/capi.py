@@ -127,7 +127,7 @@ EXPORTS = [
     "rt_render_pass", "rt_render_pass_device", "rt_film_resolve",
     "rt_get_stats", "rt_reset_stats", "rt_octree_get_info", "rt_octree_export",
     "rt_debug_trace", "rt_debug_occluded", "rt_debug_samples",
-    "rt_film_resolve_srgb", "rt_load_obj", "rt_mesh_free", "rt_image_write", "rt_rgb_to_sigmoid",
+    "rt_film_resolve_srgb", "rt_load_obj", "rt_mesh_free", "rt_image_write", "rt_rgb_to_sigmoid", "rt_rgb_fit_sigmoid",
     "rt_sensor_name", "rt_film_matrices",
 ]
 
@@ -177,6 +177,7 @@ def load_library(path=None):
         "rt_mesh_free": ([P(rt_mesh)], None),
         "rt_image_write": ([C.c_char_p, C.c_int, C.c_int, P(C.c_uint8), C.c_int], C.c_int),
         "rt_rgb_to_sigmoid": ([P(C.c_float), P(C.c_float)], C.c_int),
+        "rt_rgb_fit_sigmoid": ([P(C.c_float), P(C.c_float)], C.c_int),
         "rt_sensor_name": ([C.c_int], C.c_char_p),
         "rt_film_matrices": ([C.c_void_p, P(C.c_float), P(C.c_float)], C.c_int),
     }

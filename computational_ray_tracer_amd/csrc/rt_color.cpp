@@ -1,139 +1,109 @@
-// RGB -> RGBSigmoidPolynomial coefficients: the reference's RGBToSpectrumTable
-// (color.cpp:26-72) interpolates a precomputed 3 x 64^3 coefficient table loaded from "rgb2spec/sRGB64binary"
-// (color.cpp:114), which is not in the repository.  This fits the coefficients for one colour directly with the
-// table generator's method (Jakob & Hanika 2019, pbrt-v4 rgb2spec_opt): Gauss-Newton on the CIELAB difference
-// between the target sRGB colour and the sigmoid spectrum under D65, wavelength normalised to [0, 1] over
-// 360..830 nm, then re-expressed in nm so that R(λ) = s(c0 λ² + c1 λ + c2) (color.h:363-403).  Grey inputs take
-// the reference's closed-form branch (color.cpp:35-37).  Host only; double precision.
+// RGB -> RGBSigmoidPolynomial coefficients.  The reference's RGBToSpectrumTable (color.cpp:26-72)
+// trilinearly interpolates a 3 x 64^3 x 3 coefficient table that RGBToSpectrumTable::Init (color.cpp:107-171) reads
+// from "../rgb2spec/sRGB64binary" — a file the repository does not contain.  The build regenerates that table with
+// the generator's method (tools/rgb2spec_gen.cpp over the fit of rt_rgb2spec.h; file layout exactly the one Init
+// reads: a big-endian int resolution, 64 float z-nodes, the float[3][64][64][64][3] coefficients; checksum in
+// data/srgb64.rgbspec.sha256) and restates the reference's lookup over it:
+//   rt_rgb_to_sigmoid  = RGBToSpectrumTable::operator() — uniform-RGB closed form (color.cpp:35-37), else the largest
+//                        component's table, (x, y) = the other two scaled by (res - 1) / z, z's interval by
+//                        FindInterval over the z-nodes (helpers.h:159-172), then float trilinear Lerps;
+//   rt_rgb_fit_sigmoid = the fit itself, for one colour (the table generator's per-entry solve).
+// The table is found next to the library (../data/srgb64.rgbspec) or through RTMI_RGBSPEC_TABLE.
+#include <dlfcn.h>
+
 #include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <utility>
+#include <mutex>
+#include <string>
+#include <vector>
 
 #include "rt_guard.h"
+#include "rt_rgb2spec.h"
 #include "../../include/rtmi355x.h"
-#include "../data/spectra_data.h"
 
 namespace {
 
-constexpr int kN = 471;  // 360..830 nm, 1 nm
-constexpr double kLmin = 360.0, kLmax = 830.0;
-
-// sRGB (D65) from XYZ, IEC 61966-2-1
-const double kXYZ2RGB[3][3] = {{3.2404542, -1.5371385, -0.4985314},
-                               {-0.9692660, 1.8760108, 0.0415560},
-                               {0.0556434, -0.2040259, 1.0572252}};
-const double kRGB2XYZ[3][3] = {{0.4124564, 0.3575761, 0.1804375},
-                               {0.2126729, 0.7151522, 0.0721750},
-                               {0.0193339, 0.1191920, 0.9503041}};
-
-struct Tables {
-    double w[3][kN];   // CIE x/y/z * D65, normalised so that a unit spectrum has Y = 1
-    double white[3];   // XYZ of the unit spectrum
-    Tables() {
-        const float* il = rtdata::illum_d65;  // interleaved (λ, value)
-        int n = rtdata::illum_d65_n / 2;
-        auto d65 = [&](double l) {
-            if (l <= il[0]) return (double)il[1];
-            for (int i = 0; i + 1 < n; ++i)
-                if (l <= il[2 * (i + 1)]) {
-                    double t = (l - il[2 * i]) / (il[2 * (i + 1)] - il[2 * i]);
-                    return (1 - t) * il[2 * i + 1] + t * il[2 * (i + 1) + 1];
-                }
-            return (double)il[2 * n - 1];
-        };
-        const float* cie[3] = {rtdata::cie_x, rtdata::cie_y, rtdata::cie_z};
-        double norm = 0;
-        for (int i = 0; i < kN; ++i) norm += cie[1][i] * d65(kLmin + i);
-        for (int c = 0; c < 3; ++c) {
-            white[c] = 0;
-            for (int i = 0; i < kN; ++i) {
-                w[c][i] = cie[c][i] * d65(kLmin + i) / norm;
-                white[c] += w[c][i];
-            }
-        }
-    }
+struct RgbTable {
+    int res = 0;
+    std::vector<float> z, coeffs;  // res z-nodes; [3][res][res][res][3]
 };
 
-const Tables& tables() {
-    static Tables t;
-    return t;
-}
-
-double lab_f(double t) {
-    const double d = 6.0 / 29.0;
-    return t > d * d * d ? std::cbrt(t) : t / (3 * d * d) + 4.0 / 29.0;
-}
-void xyz_to_lab(const double* xyz, double* lab) {
-    const Tables& T = tables();
-    double fx = lab_f(xyz[0] / T.white[0]), fy = lab_f(xyz[1] / T.white[1]), fz = lab_f(xyz[2] / T.white[2]);
-    lab[0] = 116 * fy - 16;
-    lab[1] = 500 * (fx - fy);
-    lab[2] = 200 * (fy - fz);
-}
-double sigmoid(double x) { return 0.5 + x / (2 * std::sqrt(1 + x * x)); }
-
-void spectrum_lab(const double* c, double* lab) {
-    const Tables& T = tables();
-    double xyz[3] = {0, 0, 0};
-    for (int i = 0; i < kN; ++i) {
-        double l = i / (kLmax - kLmin);
-        double s = sigmoid((c[0] * l + c[1]) * l + c[2]);
-        for (int k = 0; k < 3; ++k) xyz[k] += T.w[k][i] * s;
+// RGBToSpectrumTable::Init's reader (color.cpp:107-171): 4-byte big-endian int, res floats, 3 * res^3 * 3 floats
+bool load_table(const std::string& path, RgbTable& t) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    unsigned char b[4];
+    bool ok = std::fread(b, 1, 4, f) == 4;
+    const int res = (b[0] << 24) | (b[1] << 16) | (b[2] << 8) | b[3];  // UtoInt
+    ok = ok && res == 64;
+    if (ok) {
+        t.res = res;
+        t.z.resize(res);
+        t.coeffs.resize((size_t)3 * res * res * res * 3);
+        ok = std::fread(t.z.data(), 4, t.z.size(), f) == t.z.size() &&
+             std::fread(t.coeffs.data(), 4, t.coeffs.size(), f) == t.coeffs.size();
     }
-    xyz_to_lab(xyz, lab);
+    std::fclose(f);
+    return ok;
 }
 
-void residual(const double* c, const double* target_lab, double* r) {
-    double lab[3];
-    spectrum_lab(c, lab);
-    for (int k = 0; k < 3; ++k) r[k] = target_lab[k] - lab[k];
+std::string table_path() {
+    if (const char* e = std::getenv("RTMI_RGBSPEC_TABLE")) return e;
+    Dl_info info;
+    if (dladdr((void*)&table_path, &info) && info.dli_fname) {
+        std::string so(info.dli_fname);
+        size_t p = so.find_last_of('/');
+        std::string dir = p == std::string::npos ? "." : so.substr(0, p);
+        return dir + "/../data/srgb64.rgbspec";
+    }
+    return "srgb64.rgbspec";
 }
 
-bool solve3(double A[3][3], double* b) {  // Gaussian elimination with partial pivoting, A x = b
-    for (int col = 0; col < 3; ++col) {
-        int p = col;
-        for (int r = col + 1; r < 3; ++r)
-            if (std::fabs(A[r][col]) > std::fabs(A[p][col])) p = r;
-        if (std::fabs(A[p][col]) < 1e-15) return false;
-        if (p != col) {
-            for (int k = 0; k < 3; ++k) std::swap(A[p][k], A[col][k]);
-            std::swap(b[p], b[col]);
-        }
-        for (int r = col + 1; r < 3; ++r) {
-            double f = A[r][col] / A[col][col];
-            for (int k = col; k < 3; ++k) A[r][k] -= f * A[col][k];
-            b[r] -= f * b[col];
-        }
+const RgbTable* table() {
+    static RgbTable t;
+    static bool ok = false;
+    static std::once_flag once;
+    std::call_once(once, [] { ok = load_table(table_path(), t); });
+    return ok ? &t : nullptr;
+}
+
+inline float lerp(float x, float a, float b) { return (1 - x) * a + x * b; }  // helpers.h:154-157
+
+// color.cpp:26-72 RGBToSpectrumTable::operator() (non-uniform branch)
+void table_lookup(const RgbTable& T, const float* rgb, float* c) {
+    const int res = T.res;
+    const int maxc = (rgb[0] > rgb[1]) ? ((rgb[0] > rgb[2]) ? 0 : 2) : ((rgb[1] > rgb[2]) ? 1 : 2);
+    const float z = rgb[maxc];
+    const float x = rgb[(maxc + 1) % 3] * (res - 1) / z;
+    const float y = rgb[(maxc + 2) % 3] * (res - 1) / z;
+    const int xi = std::min((int)x, res - 2), yi = std::min((int)y, res - 2);
+    long size = (long)res - 2, first = 1;  // FindInterval(res, zNodes[i] < z)
+    while (size > 0) {
+        const long half = size >> 1, middle = first + half;
+        const bool r = T.z[middle] < z;
+        first = r ? middle + 1 : first;
+        size = r ? size - (half + 1) : half;
     }
-    for (int r = 2; r >= 0; --r) {
-        for (int k = r + 1; k < 3; ++k) b[r] -= A[r][k] * b[k];
-        b[r] /= A[r][r];
+    const int zi = (int)std::min(std::max(first - 1, 0L), (long)res - 2);
+    const float dx = x - xi, dy = y - yi, dz = (z - T.z[zi]) / (T.z[zi + 1] - T.z[zi]);
+    for (int i = 0; i < 3; ++i) {
+        auto co = [&](int ox, int oy, int oz) {
+            const size_t index = (size_t)maxc * 64 * 64 * 64 * 3 + (size_t)(zi + oz) * 64 * 64 * 3 +
+                                 (size_t)(yi + oy) * 64 * 3 + (size_t)(xi + ox) * 3 + i;
+            return T.coeffs[index];
+        };
+        c[i] = lerp(dz, lerp(dy, lerp(dx, co(0, 0, 0), co(1, 0, 0)), lerp(dx, co(0, 1, 0), co(1, 1, 0))),
+                    lerp(dy, lerp(dx, co(0, 0, 1), co(1, 0, 1)), lerp(dx, co(0, 1, 1), co(1, 1, 1))));
     }
+}
+
+bool valid_rgb(const float* rgb) {
+    for (int k = 0; k < 3; ++k)
+        if (!(rgb[k] >= 0.f && rgb[k] <= 1.f)) return false;
     return true;
-}
-
-void gauss_newton(const double* rgb, double* c) {
-    double xyz[3], lab[3];
-    for (int k = 0; k < 3; ++k) xyz[k] = kRGB2XYZ[k][0] * rgb[0] + kRGB2XYZ[k][1] * rgb[1] + kRGB2XYZ[k][2] * rgb[2];
-    xyz_to_lab(xyz, lab);
-    for (int it = 0; it < 30; ++it) {
-        double r[3];
-        residual(c, lab, r);
-        double J[3][3];
-        for (int j = 0; j < 3; ++j) {  // central differences, eps 1e-5 (rgb2spec_opt eval_jacobian)
-            double cp[3] = {c[0], c[1], c[2]}, cm[3] = {c[0], c[1], c[2]}, rp[3], rm[3];
-            cp[j] += 1e-5; cm[j] -= 1e-5;
-            residual(cp, lab, rp);
-            residual(cm, lab, rm);
-            for (int i = 0; i < 3; ++i) J[i][j] = (rp[i] - rm[i]) / 2e-5;
-        }
-        double x[3] = {r[0], r[1], r[2]};
-        if (!solve3(J, x)) break;
-        for (int k = 0; k < 3; ++k) c[k] -= x[k];
-        double m = std::fmax(std::fmax(std::fabs(c[0]), std::fabs(c[1])), std::fabs(c[2]));
-        if (m > 200) for (int k = 0; k < 3; ++k) c[k] *= 200 / m;  // rgb2spec_opt's coefficient clamp
-        if (std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]) < 1e-6) break;
-    }
 }
 
 }  // namespace
@@ -141,16 +111,23 @@ void gauss_newton(const double* rgb, double* c) {
 extern "C" {
 
 static int impl_rt_rgb_to_sigmoid(const float* rgb, float* coeffs) {
-    if (!rgb || !coeffs) return RT_E_ARG;
-    for (int k = 0; k < 3; ++k)
-        if (!(rgb[k] >= 0.f && rgb[k] <= 1.f)) return RT_E_ARG;
+    if (!rgb || !coeffs || !valid_rgb(rgb)) return RT_E_ARG;
     if (rgb[0] == rgb[1] && rgb[1] == rgb[2]) {  // color.cpp:35-37, in float like the reference
         float g = rgb[0];
         coeffs[0] = 0; coeffs[1] = 0;
         coeffs[2] = (g - .5f) / std::sqrt(g * (1 - g));  // +-inf at 0 and 1: s(+-inf) = 1, 0
         return RT_OK;
     }
-    // continuation from the grey of equal mean towards the target (rgb2spec_opt marches from the grey axis)
+    const RgbTable* T = table();
+    if (!T) return RT_E_STATE;  // the coefficient table was not generated (python __graft_entry__.py build)
+    table_lookup(*T, rgb, coeffs);
+    return RT_OK;
+}
+
+static int impl_rt_rgb_fit_sigmoid(const float* rgb, float* coeffs) {
+    if (!rgb || !coeffs || !valid_rgb(rgb)) return RT_E_ARG;
+    if (rgb[0] == rgb[1] && rgb[1] == rgb[2]) return impl_rt_rgb_to_sigmoid(rgb, coeffs);
+    // continuation from the grey of equal mean towards the target (rgb2spec_opt marches from a solved neighbour)
     double c[3] = {0, 0, 0};
     double mean = (rgb[0] + rgb[1] + rgb[2]) / 3.0;
     double mc = std::fmin(std::fmax(mean, 1e-3), 1 - 1e-3);
@@ -159,12 +136,11 @@ static int impl_rt_rgb_to_sigmoid(const float* rgb, float* coeffs) {
     for (int s = 1; s <= steps; ++s) {
         double f = (double)s / steps, t[3];
         for (int k = 0; k < 3; ++k) t[k] = mc + f * (rgb[k] - mc);
-        gauss_newton(t, c);
+        rgb2spec::gauss_newton(t, c);
     }
-    // λ_n = (λ - 360) / 470  ->  coefficients of λ in nm
-    double s = 1.0 / (kLmax - kLmin);
-    double A = c[0] * s * s, B = c[1] * s - 2 * c[0] * kLmin * s * s, C = c[2] - c[1] * kLmin * s + c[0] * kLmin * kLmin * s * s;
-    coeffs[0] = (float)A; coeffs[1] = (float)B; coeffs[2] = (float)C;
+    double nm[3];
+    rgb2spec::to_nm(c, nm);
+    for (int k = 0; k < 3; ++k) coeffs[k] = (float)nm[k];
     return RT_OK;
 }
 
@@ -175,6 +151,9 @@ using rtmi::guarded;
 extern "C" {
 int rt_rgb_to_sigmoid(const float* rgb, float* coeffs) {
     return guarded([&] { return impl_rt_rgb_to_sigmoid(rgb, coeffs); }, [](const std::string&) {});
+}
+int rt_rgb_fit_sigmoid(const float* rgb, float* coeffs) {
+    return guarded([&] { return impl_rt_rgb_fit_sigmoid(rgb, coeffs); }, [](const std::string&) {});
 }
 
 }  // extern "C"

@@ -486,8 +486,19 @@ def procedural_blob(frequency=32, radius=8.0, seed=1):
 
 # ------------------------------------------------------------------- Cornell box (build-defined)
 CORNELL_WHITE = grey_sigmoid(0.73)
-CORNELL_RED = (0.00011812533193733543, -0.11407465487718582, 25.552812576293945)    # fitted: sRGB (.63,.065,.05)
-CORNELL_GREEN = (-0.00015027547487989068, 0.16323941946029663, -44.40605926513672)  # fitted: sRGB (.14,.45,.091)
+# The Cornell box's red and green walls: sRGB (.63, .065, .05) and (.14, .45, .091) through RGBToSpectrumTable
+# (color.cpp:26-72): the reference's trilinear lookup in the regenerated coefficient table (rt_rgb_to_sigmoid).
+# Module attributes CORNELL_RED / CORNELL_GREEN, computed on first use (they need the built library and its table).
+CORNELL_RGB = {"CORNELL_RED": (0.63, 0.065, 0.05), "CORNELL_GREEN": (0.14, 0.45, 0.091)}
+_colour_cache = {}
+
+
+def __getattr__(name):
+    if name in CORNELL_RGB:
+        if name not in _colour_cache:
+            _colour_cache[name] = rgb_albedo(CORNELL_RGB[name])
+        return _colour_cache[name]
+    raise AttributeError(name)
 CORNELL_LIGHT_SCALE = 25.0
 
 
@@ -554,7 +565,8 @@ def cornell_box(blocks=True, extra=None):
     light = dict(p=(343.0, ly, 227.0), e1=(0.0, 0.0, 105.0), e2=(-130.0, 0.0, 0.0), n=(0.0, -1.0, 0.0), material=L)
     model = TriModel(pos, nrm, idx, rigid=np.eye(4), cull_backfaces=False, octree_capacity=40,
                      tri_material=np.array(mats, dtype=np.int32),
-                     materials=[(CORNELL_WHITE, 0.0), (CORNELL_RED, 0.0), (CORNELL_GREEN, 0.0), ((0.0, 0.0, 0.0), CORNELL_LIGHT_SCALE)],
+                     materials=[(CORNELL_WHITE, 0.0), (__getattr__("CORNELL_RED"), 0.0), (__getattr__("CORNELL_GREEN"), 0.0),
+                                ((0.0, 0.0, 0.0), CORNELL_LIGHT_SCALE)],
                      lights=[light])
     return model
 
@@ -640,7 +652,7 @@ def mixed_scene(frequency=70):
     mats = list(model.materials)
     mats[L] = ((0.0, 0.0, 0.0), 12.0)                                            # ceiling quad: dimmer
     DIFF, MIRR, GLASS, DISKL = len(mats), len(mats) + 1, len(mats) + 2, len(mats) + 3
-    mats += [(CORNELL_GREEN, 0.0, capi.RT_MAT_DIFFUSE, 0.0),
+    mats += [(__getattr__("CORNELL_GREEN"), 0.0, capi.RT_MAT_DIFFUSE, 0.0),
              (grey_sigmoid(0.9), 0.0, capi.RT_MAT_MIRROR, 0.0),
              ((0.0, 0.0, 0.0), 0.0, capi.RT_MAT_DIELECTRIC, 0.0),                # eta 0 = glass-BK7
              ((0.0, 0.0, 0.0), 30.0)]
@@ -697,13 +709,15 @@ def load_obj(path):
 
 
 def rgb_albedo(rgb):
-    """rt_rgb_to_sigmoid: RGBAlbedoSpectrum(sRGB, rgb) sigmoid coefficients (color.cpp:26-72 without its table)."""
+    """rt_rgb_to_sigmoid: RGBAlbedoSpectrum(sRGB, rgb) sigmoid coefficients — RGBToSpectrumTable::operator()
+    (color.cpp:26-72) over the regenerated coefficient table."""
     lib = capi.load_library()
     src = (C.c_float * 3)(*[float(x) for x in rgb])
     out = (C.c_float * 3)()
     rc = lib.rt_rgb_to_sigmoid(src, out)
     if rc != capi.RT_OK:
-        raise capi.RTError("rt_rgb_to_sigmoid", rc, f"rgb {rgb} outside [0,1]")
+        raise capi.RTError("rt_rgb_to_sigmoid", rc, f"rgb {rgb} outside [0,1]" if rc == capi.RT_E_ARG
+                           else "coefficient table missing (python __graft_entry__.py build)")
     return tuple(float(x) for x in out)
 
 

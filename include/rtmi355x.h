@@ -286,9 +286,13 @@ void rt_mesh_free(rt_mesh* mesh);
 /* Write w x h 8-bit RGB to `path`: PNG when it ends in .png, binary PPM otherwise; flip_y writes rows bottom-up
  * (the film's row 0 is the image bottom: the reference uploads it as a GL texture, RayTracerTestApp.h:453-455). */
 int rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_y);
-/* RGBAlbedoSpectrum coefficients for an sRGB reflectance in [0,1]^3 (replaces the missing RGBToSpectrumTable file,
- * color.cpp:26-72, 114): grey = the closed form of color.cpp:35-37, otherwise a Gauss-Newton fit in CIELAB. */
+/* RGBToSpectrumTable::operator() (color.cpp:26-72) for an sRGB reflectance in [0,1]^3: grey = the closed form of
+ * color.cpp:35-37, otherwise the reference's trilinear lookup in the 3 x 64^3 coefficient table, which the build
+ * regenerates (the reference's "../rgb2spec/sRGB64binary", color.cpp:114, is not in its repository; data/srgb64.rgbspec,
+ * found next to the library or through RTMI_RGBSPEC_TABLE).  RT_E_STATE when the table is missing. */
 int rt_rgb_to_sigmoid(const float* rgb, float* coeffs);
+/* The table generator's per-entry solve for one colour: Gauss-Newton in CIELAB (rgb2spec_opt's method). */
+int rt_rgb_fit_sigmoid(const float* rgb, float* coeffs);
 /* Name of a PixelSensor (RT_SENSOR_XYZ -> "xyz", 1.. -> the reference's camera name), NULL when out of range. */
 const char* rt_sensor_name(int sensor);
 /* The film's resolve matrices (column-major, glm layout): XYZFromSensorRGB of the current sensor, sRGB RGBFromXYZ. */

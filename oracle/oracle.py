@@ -87,6 +87,8 @@ def lib():
             "orc_trace": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), C.c_int, P(C.c_int), P(C.c_float), P(C.c_int64)], C.c_int),
             "orc_occluded": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_int)], C.c_int),
             "orc_samples": ([C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(capi.rt_sample_record)], C.c_int),
+            "orc_rgb_table_lookup": ([P(C.c_float), P(C.c_float), C.c_int, C.c_int, P(C.c_float), P(C.c_float)],
+                                     C.c_int),
             "orc_canonical_check": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int, C.c_int,
                                      P(C.c_int64)], C.c_int),
             "orc_render": ([C.c_void_p, C.c_int, C.c_int, P(C.c_float), C.c_int, P(C.c_int64), P(C.c_int), C.c_int], C.c_int),

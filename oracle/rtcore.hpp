@@ -610,6 +610,28 @@ struct Sigmoid {
 };
 // color.cpp:35-37 uniform-RGB branch of RGBToSpectrumTable (the only branch usable without the missing table)
 static inline Sigmoid SigmoidFromGrey(float g) { return {0, 0, (g - .5f) / std::sqrt(g * (1 - g))}; }
+// color.cpp:26-72 RGBToSpectrumTable::operator() over a table in the layout Init reads (color.cpp:107-171):
+// zNodes[res], coeffs[3][res][res][res][3] (the build regenerates the missing file, tools/rgb2spec_gen.cpp)
+static inline Sigmoid RGBToSpectrumTableLookup(const float* zNodes, const float* coeffs, int res, const float rgb[3]) {
+    if (rgb[0] == rgb[1] && rgb[1] == rgb[2]) return SigmoidFromGrey(rgb[0]);
+    int maxc = (rgb[0] > rgb[1]) ? ((rgb[0] > rgb[2]) ? 0 : 2) : ((rgb[1] > rgb[2]) ? 1 : 2);
+    float z = rgb[maxc];
+    float x = rgb[(maxc + 1) % 3] * (res - 1) / z;
+    float y = rgb[(maxc + 2) % 3] * (res - 1) / z;
+    int xi = std::min((int)x, res - 2), yi = std::min((int)y, res - 2);
+    int zi = (int)FindInterval(res, [&](int i) { return zNodes[i] < z; });
+    float dx = x - xi, dy = y - yi, dz = (z - zNodes[zi]) / (zNodes[zi + 1] - zNodes[zi]);
+    float c[3];
+    for (int i = 0; i < 3; ++i) {
+        auto co = [&](int ox, int oy, int oz) {
+            return coeffs[(size_t)maxc * 64 * 64 * 64 * 3 + (size_t)(zi + oz) * 64 * 64 * 3 + (size_t)(yi + oy) * 64 * 3 +
+                          (size_t)(xi + ox) * 3 + i];
+        };
+        c[i] = Lerp(dz, Lerp(dy, Lerp(dx, co(0, 0, 0), co(1, 0, 0)), Lerp(dx, co(0, 1, 0), co(1, 1, 0))),
+                    Lerp(dy, Lerp(dx, co(0, 0, 1), co(1, 0, 1)), Lerp(dx, co(0, 1, 1), co(1, 1, 1))));
+    }
+    return {c[0], c[1], c[2]};
+}
 
 // pixelsensor.h:81-87 ToSensorRGB (XYZ sensor: r_bar=X, g_bar=Y, b_bar=Z), imagingRatio = 1/CIE_Y_integral
 static inline void ToSensorRGB(const Spectra& sp, SS L, const SW& w, float imagingRatio, float rgb[3]) {

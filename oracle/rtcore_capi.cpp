@@ -464,6 +464,15 @@ int orc_canonical_check(void* h, int n, const float* ro, const float* rd, const 
     return 0;
 }
 
+// RGBToSpectrumTable::operator() over n colours (rgb[3 n] -> out[3 n]) with the given table
+int orc_rgb_table_lookup(const float* znodes, const float* coeffs, int res, int n, const float* rgb, float* out) {
+    for (int i = 0; i < n; ++i) {
+        Sigmoid s = RGBToSpectrumTableLookup(znodes, coeffs, res, rgb + 3 * i);
+        out[3 * i] = s.c0; out[3 * i + 1] = s.c1; out[3 * i + 2] = s.c2;
+    }
+    return 0;
+}
+
 int orc_samples(void* h, int n, const int* pixel_ids, const int* indices, rt_sample_record* out) {
     auto* o = static_cast<OracleScene*>(h);
     for (int i = 0; i < n; ++i) {
