@@ -41,6 +41,15 @@ struct CompactWave {
     unsigned short pair[64 * kCompactMaxClusters];  // lane | cluster << 6
 };
 __shared__ CompactWave g_cmp[kBlock / 64];  // one per wave, shared by every single-leaf traversal call site
+// the single leaf's tiles (<= 64 triangles, 3 KB) staged in LDS at kernel start by every kernel that traverses it
+__shared__ float4 g_leaf1[3 * 64];
+__device__ __forceinline__ void stage_leaf1(const DevScene& sc, int set) {
+    const int2 r = sc.leafRange[set][0];
+    if (r.y <= 64)
+        for (int i = threadIdx.x; i < 3 * r.y; i += blockDim.x) g_leaf1[i] = sc.tiles[set][3 * r.x + i];
+    __syncthreads();
+}
+#define RT_LEAF1(tiles, base, j) (g_leaf1 + 3 * (j))
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -201,7 +210,8 @@ __device__ __forceinline__ void rec_set_prev_pdf(const RecView& r, int slot, flo
 // ===================================================================================== K1 generate
 // RayTracerTestApp.h:305-323: StartPixelSample → SampleVisible(Get1D) → filter.Sample(GetPixel2D) →
 // pixel + .5 + p → PerspectiveCamera::generateRay (Cameras.h:273-297) → Ray::Transform (Shapes.h:37-41).
-__global__ void __launch_bounds__(kBlock) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
+// 4 waves/SIMD (158 -> 128 VGPRs, 112 B/lane spill): +3 % on the Cornell box
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
                                                      DevFilm film, GenOut out) {
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nS; s += gridDim.x * blockDim.x) {
         int pixel, index, x, y;
@@ -486,7 +496,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                             Q.kz = KZ >= 0 ? KZ : __float_as_int(rb.z);
                             Q.kx = Q.kz + 1; if (Q.kx == 3) Q.kx = 0;
                             Q.ky = Q.kx + 1; if (Q.ky == 3) Q.ky = 0;
-                            const float4* tp = tiles + 3 * (r.x + 2 * c);
+                            const float4* tp = RT_LEAF1(tiles, r.x, 2 * c);
                             unsigned bits;
                             if ((fp >> (2 * c)) & 1) {
                                 bits = tri_candidate_pair<KZ>(Q, tp[0], tp[1], tp[2], tp[4], tp[5]);
@@ -548,7 +558,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 while (cand) {
                     int j = __builtin_ctzll(cand);
                     cand &= cand - 1;
-                    const float4* tp = tiles + 3 * (r.x + j);
+                    const float4* tp = RT_LEAF1(tiles, r.x, j);
                     float b0, b1, b2, t;
                     if (tri_intersect<KZ>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax) {
                         best = __float_as_int(tp[2].y);
@@ -922,7 +932,7 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 
 // Register budgets (amdgpu_waves_per_eu) of the multi-level instantiations: 4 waves/SIMD (128 VGPRs) on the trace,
 // path shade and mixed-scene shade kernels (CFG3 121 -> 144, CFG4 87 -> 111 Msamples/s; 5 waves spill too much).
-// The single-leaf instantiations (107 / 125 VGPRs) are unbudgeted.
+// The single-leaf instantiations (107 / 123 VGPRs) are unbudgeted (5 waves: trace -2 %, shade -7 %).
 #ifndef RT_MULTI_WAVES
 #define RT_MULTI_WAVES 4  // the one tuning macro left: variant builds for A/B (Makefile `variants`)
 #endif
@@ -931,8 +941,44 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
     const int n = io.count ? *io.count : io.n;
+    if constexpr (QCAP == 1) stage_leaf1(sc, io.set);
     ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
-    // no block-level synchronisation here: each wave takes its own tickets (WaveChunks)
+    // no block-level synchronisation here: each wave takes its own tickets (WaveChunks).  Without tickets (single
+    // leaf) a thread's items are k(j) = (block + (j / S) grid) S kBlock + (j % S) kBlock + thread, S = kStaticItems,
+    // and the next item's ray is loaded while the current one is traced.
+    if (!io.ticket) {
+        auto item = [&](int j) {
+            return (blockIdx.x + (j / kStaticItems) * gridDim.x) * (kStaticItems * kBlock) + (j % kStaticItems) * kBlock +
+                   (int)threadIdx.x;
+        };
+        int k = item(0);
+        float4 o4 = make_float4(0, 0, 0, 0), d4 = o4;
+        if (k < n) { o4 = io.rayO[k]; d4 = io.rayD[k]; }
+        for (int j = 1; k < n; ++j) {
+            const int kn = item(j);
+            float4 on = o4, dn = d4;
+            if (kn < n) { on = io.rayO[kn]; dn = io.rayD[kn]; }
+            float b0 = 0, b1 = 0, b2 = 0, t = 0;
+            int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z),
+                                                 3.402823466e+38f, b0, b1, b2, t, nn, nt, nfb);
+            if (sc.n_shapes) {
+                float tm = prim >= 0 ? t : 3.402823466e+38f;
+                for (int si = 0; si < sc.n_shapes; ++si) {
+                    DevShape sh = ldconst(sc.shapes, si);
+                    V3 ph;
+                    float th;
+                    if (shape_isect(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
+                        prim = sc.n_tris + si; b0 = ph.x; b1 = ph.y; b2 = ph.z; t = th; tm = th;
+                    }
+                }
+            }
+            io.hitB[k] = make_float4(b0, b1, b2, t);
+            io.hitPrim[k] = prim;
+            nh += prim >= 0;
+            nr += 1;
+            k = kn; o4 = on; d4 = dn;
+        }
+    } else {
     WaveChunks chunks(io.ticket);
     for (int cb = chunks.next(); cb < n; cb = chunks.next())
     for (int k = cb + chunks.lane; k < cb + chunks.size && k < n; k += chunks.step) {
@@ -955,6 +1001,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
         io.hitPrim[k] = prim;
         nh += prim >= 0;
         nr += 1;
+    }
     }
     count_add(ctr, C_NODES, nn);
     count_add(ctr, C_TRIS, nt);
@@ -1080,6 +1127,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                                                                          DevFilm film, SampleIds ids, PathIO io,
                                                                          unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
+    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
     __shared__ int lds[kBlock / 64 + 1];
     const int n = *io.count;
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
@@ -1164,19 +1212,24 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                             stmax = dist * 0.999f;
                         }
                     }
-                    // --- cosine-hemisphere BSDF sample (Sampling.h:449-454), frame = pbrt CoordinateSystem
-                    sm.get2d(smp, u0, u1);
-                    V3 wi;
-                    float z;
-                    if (cosine_bounce(u0, u1, nrm, wi, z)) {
+                    // --- cosine-hemisphere BSDF sample (Sampling.h:449-454), frame = pbrt CoordinateSystem.  The host
+                    // never traces depth max_depth in this integrator (only emitter hits could add there, and they
+                    // count at depth 0 only), so the last shaded depth draws no bounce: its β, ray and sampler state
+                    // would never be read.
+                    if (io.depth + 1 < io.max_depth) {
+                        sm.get2d(smp, u0, u1);
+                        V3 wi;
+                        float z;
+                        if (cosine_bounce(u0, u1, nrm, wi, z)) {
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) beta[i] *= R[i];
-                        rstore8(io.rec, slot, R_BETA, beta);
-                        wantNext = true;
-                        nO = make_float4(po.x, po.y, po.z, 0.f);
-                        nD = make_float4(wi.x, wi.y, wi.z, 0.f);
+                            for (int i = 0; i < 8; ++i) beta[i] *= R[i];
+                            rstore8(io.rec, slot, R_BETA, beta);
+                            wantNext = true;
+                            nO = make_float4(po.x, po.y, po.z, 0.f);
+                            nD = make_float4(wi.x, wi.y, wi.z, 0.f);
+                        }
+                        save_sampler(io, slot, sm);
                     }
-                    save_sampler(io, slot, sm);
                 }
             }
         }
@@ -1280,6 +1333,7 @@ template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const float4* o, const float4* d, int* out,
                                                      unsigned long long* ctr) {
     ctr_t nn = 0, nt = 0, ns = 0, nfb = 0;
+    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         float4 o4 = o[k], d4 = d[k];
         out[k] = scene_occluded<QCAP>(sc, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, nn, nt, nfb) ? 1 : 0;
@@ -1297,6 +1351,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                                                               SampleIds ids, PathIO io,
                                                                               unsigned long long* ctr) {
     const float InvPi = 0.31830988618379067154f;
+    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
     __shared__ int lds[kBlock / 64 + 1];
     const int n = *io.count;
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;

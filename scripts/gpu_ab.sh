@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B the kernel variants in computational_ray_tracer_amd/lib/variants/*.so (interleaved rounds, one process each).
 cd "$GRAFT_REPO_ROOT"
+export RTMI_RGBSPEC_TABLE=$PWD/computational_ray_tracer_amd/data/srgb64.rgbspec  # variants live one level deeper
 mkdir -p gpurun_out
 for round in 1 2; do
   for so in computational_ray_tracer_amd/lib/variants/*.so; do
