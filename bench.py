@@ -90,15 +90,17 @@ def single_lane_pass(cfg, world, rank, spp_per_step, steps):
     """Per-kernel launch times with ONE batch in flight (RTMI_LANES=1): with two lanes a launch's HIP-event time
     also covers the other lane's kernels sharing the CUs, so per-kernel rooflines come from this pass (the rocprof
     kernel traces under profiles/ are single-lane too).  Untimed for `value`; same workload and step size."""
-    old = os.environ.get("RTMI_LANES")
+    old = {k: os.environ.get(k) for k in ("RTMI_LANES", "RTMI_NO_STAGE_EVENTS")}
     os.environ["RTMI_LANES"] = "1"
+    os.environ.pop("RTMI_NO_STAGE_EVENTS", None)  # this pass times every stage
     try:
         r1 = Renderer(cfg, device=torch.cuda.current_device())
     finally:
-        if old is None:
-            del os.environ["RTMI_LANES"]
-        else:
-            os.environ["RTMI_LANES"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     r1.set_shard(32, world, rank)
     W, H = cfg.film.res
     film = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")

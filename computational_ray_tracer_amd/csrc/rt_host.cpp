@@ -487,6 +487,7 @@ struct rt_ctx {
     int* d_work = nullptr;
     // batch workspaces, one per lane (path mode runs kLanes batches concurrently on separate streams)
     Work ws[kLanes];
+    bool stage_events = true;   // per-stage HIP events (rt_stats ms_*); RTMI_NO_STAGE_EVENTS=1 turns them off
     int lanes = kDefaultLanes;  // batches in flight in path mode (RTMI_LANES overrides)
     // multi-level simple path scenes: NEE rays traced by k_path_shadow (RTMI_SHADOW_QUEUE=1; measured slower than
     // the inline any-hit, kept as a parity-tested option), depth first (RTMI_SHADOW_DFS, exact any-hit, §6)
@@ -675,11 +676,13 @@ hipEvent_t ev_get(rt_ctx* c) {
     return e;
 }
 void ev_mark(rt_ctx* c, hipStream_t st, int stage, hipEvent_t a) {
+    if (!a) return;  // stage timing off
     hipEvent_t b = ev_get(c);
     hipEventRecord(b, st);
     c->pending.push_back({a, b, stage});
 }
 hipEvent_t ev_start(rt_ctx* c, hipStream_t st) {
+    if (!c->stage_events) return nullptr;
     hipEvent_t a = ev_get(c);
     hipEventRecord(a, st);
     return a;
@@ -1372,6 +1375,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
         return RT_E_HIP;
     }
     c->grid = prop.multiProcessorCount * 8;  // persistent grid: 8 blocks of 256 per CU
+    if (std::getenv("RTMI_NO_STAGE_EVENTS")) c->stage_events = false;
     if (const char* e = std::getenv("RTMI_LANES")) c->lanes = std::max(1, std::min(kLanes, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_SHADOW_QUEUE")) c->shadow_queue = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SHADOW_DFS")) c->shadow_dfs = std::atoi(e);
@@ -1381,7 +1385,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
     c->hs.init();
     if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->ws[0].d_qcount, 2 * kQRegion) != hipSuccess ||
-        dalloc(&c->d_ctr, (size_t)C_NCOUNTERS) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
+        dalloc(&c->d_ctr, kCtrWords) != hipSuccess || dalloc(&c->d_resolve, 18) != hipSuccess) {
         destroy_one(c);
         return RT_E_OOM;
     }
@@ -1397,7 +1401,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     std::memcpy(ds.bk7_lambda, c->hs.BK7.l.data(), 4 * ds.bk7_n);
     std::memcpy(ds.bk7_value, c->hs.BK7.v.data(), 4 * ds.bk7_n);
     hipMemcpy(c->d_spec, &ds, sizeof(ds), hipMemcpyHostToDevice);
-    hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * C_NCOUNTERS);
+    hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords);
     {
         rt_film_desc fd{};  // XYZ sensor under D65 until rt_film_set says otherwise
         if (setup_sensor(c, fd) != RT_OK) {
@@ -1976,8 +1980,11 @@ static int get_stats_one(rt_ctx* c, rt_stats* out) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipDeviceSynchronize());
     harvest(c);
-    unsigned long long h[C_NCOUNTERS];
-    HIPCHK(c, hipMemcpy(h, c->d_ctr, sizeof(h), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> raw(kCtrWords);
+    HIPCHK(c, hipMemcpy(raw.data(), c->d_ctr, kCtrWords * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long h[C_NCOUNTERS] = {};
+    for (int k = 0; k < C_NCOUNTERS; ++k)
+        for (int u = 0; u < kCtrSubs; ++u) h[k] += raw[ctr_word(k, u)];
     rt_stats s = c->stats;
     s.nodes_tested = (int64_t)h[C_NODES];
     s.tris_tested = (int64_t)h[C_TRIS];
@@ -1999,7 +2006,7 @@ static int reset_stats_one(rt_ctx* c) {
     HIPCHK(c, hipDeviceSynchronize());
     harvest(c);
     c->stats = rt_stats{};
-    HIPCHK(c, hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * C_NCOUNTERS));
+    HIPCHK(c, hipMemset(c->d_ctr, 0, sizeof(unsigned long long) * kCtrWords));
     return RT_OK;
 }
 

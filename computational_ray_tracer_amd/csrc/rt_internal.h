@@ -115,9 +115,15 @@ struct DevScene {
     float wabs;                     // canonical-rule window W(t) = t 2^-16 + wabs
 };
 
-// device counter slots (u64)
+// device counter slots (u64).  Every wave of a persistent kernel adds its totals at the end, all at about the same
+// time: one counter word per slot serialised those atomics (a fixed ~0.15 ms tail per trace launch), so each slot
+// is spread over kCtrSubs words, one per 256-B line, picked by wave; the host sums them (ctr_word, ctr_total).
 enum { C_NODES = 0, C_TRIS, C_HITS, C_RAYS, C_SHADOW, C_SAMPLES, C_SNODES, C_STRIS, C_FALLBACK, C_SFALLBACK,
        C_NCOUNTERS = 16 };
+constexpr int kCtrSubs = 32;   // words per counter slot
+constexpr int kCtrLine = 32;   // u64 between words: 256 B
+constexpr size_t kCtrWords = (size_t)C_NCOUNTERS * kCtrSubs * kCtrLine;
+__host__ __device__ inline size_t ctr_word(int slot, int sub) { return ((size_t)slot * kCtrSubs + sub) * kCtrLine; }
 
 // host: 4-wide BVH build (rt_bvh.cpp)
 struct BvhData {

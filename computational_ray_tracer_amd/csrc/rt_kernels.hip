@@ -154,7 +154,8 @@ typedef unsigned long long ctr_t;
 __device__ __forceinline__ void count_add(unsigned long long* ctr, int slot, unsigned long long v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (lane_id() == 0 && v) atomicAdd(ctr + slot, v);
+    const int sub = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kCtrSubs - 1));
+    if (lane_id() == 0 && v) atomicAdd(ctr + ctr_word(slot, sub), v);
 }
 
 __device__ __forceinline__ void sample_of(const SampleIds& ids, int s, int& pixel, int& index) {
@@ -411,6 +412,25 @@ __device__ __forceinline__ bool occluded_dfs(const DevScene& sc, int set, V3 o, 
     }
 }
 
+// Per-lane mask of the single-leaf culling clusters whose conservative box the ray reaches within tMax (bit c =
+// cluster c, ncl <= 32).  The boxes are read through the scalar cache three clusters at a time, so a wave waits once
+// per group instead of once per cluster (scalar loads return out of order: every use waits for all of them).
+__device__ __forceinline__ uint32_t cluster_mask(const float4* cl, int ncl, bool far, V3 o, V3 inv, float tmax) {
+    uint32_t hm = 0;
+    for (int c0 = 0; c0 < ncl; c0 += 3) {
+        float4 A[3], B[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int c = c0 + u < ncl ? c0 + u : ncl - 1;
+            A[u] = ldc4(cl, 2 * c);
+            B[u] = ldc4(cl, 2 * c + 1);
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+            if (c0 + u < ncl && (far || cluster_hit(A[u], B[u], o, inv, tmax))) hm |= 1u << (c0 + u);
+    }
+    return hm;
+}
 // ===================================================================================== K2 traverse
 // Octtree_Model.h:66-127 — FIFO BFS.  The 8 children of an internal node are contiguous, so the queue
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
@@ -460,7 +480,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 const int ncl = sc.n_clusters[set];
                 constexpr bool kCompact = !ANYHIT && KZ < 0;
                 constexpr bool kCull = ANYHIT || KZ >= 0 || kCompact;
-                if (kCull && ncl * kClusterTris >= r.y) {
+                if (kCull && ncl * kClusterTris >= r.y && ncl <= 32) {
                     const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
                     const float gx = o.x - sc.cl_guard.x, gy = o.y - sc.cl_guard.y, gz = o.z - sc.cl_guard.z;
                     const bool far = gx * gx + gy * gy + gz * gz > sc.cl_guard.w;  // pad not sized for it
@@ -479,8 +499,9 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         cw.rb[ln] = make_float4(R.oy, R.oz, __int_as_float(R.kz), 0.f);
                         cw.cand[ln] = 0;
                         int np = 0;
+                        const uint32_t hm = cluster_mask(cl, ncl, far, o, inv, cl_t);
                         for (int c = 0; c < ncl; ++c) {
-                            bool hb = far || cluster_hit(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t);
+                            const bool hb = (hm >> c) & 1u;
                             uint64_t m = __ballot(hb);
                             if (hb) cw.pair[np + mbcnt64(m)] = (unsigned short)(ln | (c << 6));
                             np += __popcll(m);
@@ -510,8 +531,9 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         cand = cw.cand[ln];
                         k = r.y;
                     } else {
+                    const uint32_t hm = cluster_mask(cl, ncl, far, o, inv, cl_t);
                     for (int c = 0; c < ncl; ++c) {
-                        bool hb = far || cluster_hit(ldc4(cl, 2 * c), ldc4(cl, 2 * c + 1), o, inv, cl_t);
+                        const bool hb = (hm >> c) & 1u;
                         if (__ballot(hb) == 0) continue;
                         if (kClusterTris == 2 && ((fp >> (2 * c)) & 1)) {
                             int e = 3 * (r.x + 2 * c);
