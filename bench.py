@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=4)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--spp-per-step", type=int, default=8)
+    p.add_argument("--spp-per-step", type=int, default=16)  # two lanes x 16 Mi-sample batches at 1080p
     p.add_argument("--res", type=str, default="1920x1080")
     p.add_argument("--config", choices=["cornell", "cfg3", "cfg4", "cfg5"], default="cornell",
                    help="cornell = BASELINE configs[1] (the metric's workload); cfg3..cfg5 = configs[2..4]")

@@ -497,7 +497,7 @@ struct rt_ctx {
     float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
     int sort_dir_bits = 3, sort_org_bits = 4;  // sort key widths (RTMI_SORT_BITS="dir/org"; 3/7 3/2 2/5 within 2 %)
     hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
-    size_t batch_samples = 0;  // samples in flight per batch (0: 8 Mi path / 16 Mi reference; RTMI_BATCH_SAMPLES)
+    size_t batch_samples = 0;  // samples in flight per batch (0: 16 Mi; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     float* d_cdf = nullptr;    // Gaussian / Lanczos filter tables: x then y, cdf_n + 1 floats each
@@ -950,15 +950,19 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     bool path = c->integ.kind == RT_INTEGRATOR_PATH || c->integ.kind == RT_INTEGRATOR_PATH_MIS;
     c->dsc.mis = c->integ.kind == RT_INTEGRATOR_PATH_MIS;
     c->dsc.full = c->scene_full || c->dsc.mis;
-    const size_t target = c->batch_samples ? c->batch_samples : path ? (size_t)8 << 20 : (size_t)16 << 20;
+    // 16 Mi samples per path batch (8 Mi: Cornell 1874 -> 1827, CFG3 503 -> 484, CFG4 298 -> 284 Msamples/s)
+    const size_t target = c->batch_samples ? c->batch_samples : (size_t)16 << 20;
     int B = (int)std::max<size_t>(1, target / (size_t)c->n_work);
     B = std::min(B, ie - ib);
     size_t nmax = (size_t)B * c->n_work;
+    // queue / hit capacity: the shards of the largest batch (>= nmax); single-leaf scenes use one shard
+    const int nsh = c->dsc.qcap == 1 ? 1 : kShards;
+    const size_t ncap = (size_t)nsh * (size_t)shard_stride((int)nmax, nsh);
     DevCamera cam = dev_camera(c->cam);
     DevFilm fd = dev_film(c);
     if (!path) {
         Work& w = c->ws[0];
-        if ((rc = ensure_workspace(c, w, nmax, false))) return rc;
+        if ((rc = ensure_workspace(c, w, ncap, false))) return rc;
         for (int b0 = ib; b0 < ie; b0 += B) {
             int nIdx = std::min(B, ie - b0);
             int nS = nIdx * c->n_work;
@@ -967,7 +971,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             hipEvent_t e0 = ev_start(c, st);
             HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, st, ST_GEN, e0);
-            TraceIO tio{w.rayO, w.rayD, nullptr, nS, c->cull ? 1 : 0, w.hitB, w.hitPrim};
+            TraceIO tio{w.rayO, w.rayD, QueueView{nullptr, shard_stride(nS, nsh), nS, nsh}, c->cull ? 1 : 0, w.hitB, w.hitPrim};
             e0 = ev_start(c, st);
             HIPCHK(c, launch_trace_closest(st, 0, c->dsc.qcap, lane_scene(c, w), tio, c->d_ctr));
             ev_mark(c, st, ST_TRACE, e0);
@@ -991,8 +995,8 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     // costs more than it saves (1110 -> 720 Msamples/s)
     const bool sort_rays = c->dsc.qcap != 1 && c->sort_rays;
     for (int l = 0; l < lanes; ++l) {
-        if ((rc = ensure_workspace(c, c->ws[l], nmax, true))) return rc;
-        if (sort_rays && (rc = ensure_sort_workspace(c, c->ws[l], nmax))) return rc;
+        if ((rc = ensure_workspace(c, c->ws[l], ncap, true))) return rc;
+        if (sort_rays && (rc = ensure_sort_workspace(c, c->ws[l], ncap))) return rc;
     }
     // Cornell-like single-leaf scenes cost the same per ray: static chunks on a resident grid beat tickets there
     // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
@@ -1002,7 +1006,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const bool shq = c->shadow_queue && c->dsc.qcap != 1 && !c->dsc.full;
     if (shq)
         for (int l = 0; l < lanes; ++l)
-            if ((rc = ensure_shadow_workspace(c, c->ws[l], nmax))) return rc;
+            if ((rc = ensure_shadow_workspace(c, c->ws[l], ncap))) return rc;
     // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
     // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
     // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
@@ -1012,7 +1016,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
         HIPCHK(c, hipEventRecord(c->ws[0].film_done, st));
         for (int l = 1; l < lanes; ++l) HIPCHK(c, hipStreamWaitEvent(c->ws[l].stream, c->ws[0].film_done, 0));
     }
-    const size_t qs = nmax;  // one queue
+    const size_t qs = ncap;  // one queue (nsh shards of stride Sq[lane])
     // slot state layout (rt_internal.h RecView): records for multi-level scenes (sorted, scattered slots), SoA for
     // single-leaf ones (slots stay in queue order)
     const bool records = c->dsc.qcap != 1;
@@ -1020,7 +1024,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const unsigned rec_ss = records ? (unsigned)kRecF4 : 1u;
     int last_film = -1;      // lane of the most recent film launch
     for (int g0 = ib; g0 < ie; g0 += B * lanes) {
-        int nIdx[kLanes] = {0}, cur[kLanes] = {0};
+        int nIdx[kLanes] = {0}, cur[kLanes] = {0}, nSq[kLanes] = {0}, Sq[kLanes] = {0};
         for (int l = 0; l < lanes; ++l) {
             int b0 = g0 + l * B;
             if (b0 >= ie) break;
@@ -1029,14 +1033,16 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             const RecView rv{w.rec, rec_fs, rec_ss};
             nIdx[l] = std::min(B, ie - b0);
             int nS = nIdx[l] * c->n_work;
+            nSq[l] = nS;
+            Sq[l] = shard_stride(nS, nsh);  // every queue of this batch: shard j at [j S, j S + len_j)
             SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
             GenOut go{w.rayO, w.rayD, w.slot, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0};
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, s, ST_GEN, e0);
-            // camera rays fill queue 0
+            // camera rays fill queue 0 densely (positions 0..nS-1: QueueView without lengths); both counter regions
+            // start at zero
             HIPCHK(c, hipMemsetAsync(w.d_qcount, 0, 2 * kQRegion * sizeof(int), s));
-            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)w.d_qcount, nS, 1, s));
         }
         for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
             // the last trace can only add emitter hits, which count only after specular bounces or with MIS
@@ -1058,28 +1064,33 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 // multi-level octrees: bounce rays sorted by (octant, direction cell, origin Morton code) before
                 // the trace.  The queue length is read back so only live rays are sorted (sorting the capacity with
                 // padded keys instead, without the host read: -0.6 %); the other lane keeps the GPU busy meanwhile.
+                const QueueView qv = depth == 0 ? QueueView{nullptr, Sq[l], nSq[l], nsh}
+                                                : QueueView{qc_cur + kQLen, Sq[l], 0, nsh};
                 if (sort_rays && depth > 0) {
-                    int nq = 0;
                     SortRaysIO so{cO, cD, cS, w.sO, w.sD, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt,
-                                  w.sTemp, w.sTempBytes, c->sort_lo, c->sort_scale, c->sort_dir_bits, c->sort_org_bits};
-                    HIPCHK(c, hipMemcpyAsync(&nq, qc_cur, sizeof(int), hipMemcpyDeviceToHost, s));
+                                  w.sTemp, w.sTempBytes, c->sort_lo, c->sort_scale, c->sort_dir_bits, c->sort_org_bits,
+                                  qc_cur + kQLen, Sq[l]};
+                    int lens[kShards * kQStride];
+                    HIPCHK(c, hipMemcpyAsync(lens, qc_cur + kQLen, sizeof(lens), hipMemcpyDeviceToHost, s));
                     HIPCHK(c, hipStreamSynchronize(s));
+                    int nq = 0;
+                    for (int j = 0; j < kShards; ++j) nq += lens[j * kQStride];
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, nq, so));
                     ev_mark(c, s, ST_SORT, e0);
                     cO = w.sO; cD = w.sD; cS = w.sS;
                 }
                 const DevScene dsl = lane_scene(c, w);
-                TraceIO tio{cO, cD, qc_cur, 0, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr};
+                TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr};
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
                 ev_mark(c, s, ST_TRACE, e0);
                 PathIO pio{};
                 pio.lean = lean ? 1 : 0;
-                pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.count = qc_cur;
+                pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.q = qv;
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
                 pio.nO = w.rayO + (size_t)nxt * qs; pio.nD = w.rayD + (size_t)nxt * qs;
-                pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt;
+                pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt + kQLen;
                 pio.rec = RecView{w.rec, rv.fs, rv.ss}; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 pio.ticket = dyn ? qc_cur + kQShadeTicket : nullptr;
@@ -2045,7 +2056,7 @@ static int impl_rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* r
     if (!rc && (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dH, n) || dalloc(&dP, n)))
         rc = fail(c, RT_E_OOM, "debug trace buffers");
     if (!rc) {
-        TraceIO io{dO, dD, nullptr, n, (use_cull && c->cull) ? 1 : 0, dH, dP};
+        TraceIO io{dO, dD, QueueView{nullptr, shard_stride(n, 1), n, 1}, (use_cull && c->cull) ? 1 : 0, dH, dP};
         if (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
             launch_trace_closest(c->stream, 0, c->dsc.qcap, lane_scene(c, c->ws[0]), io, c->d_ctr) != hipSuccess ||
@@ -2114,7 +2125,8 @@ static int impl_rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, con
         GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].slot, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA,
                   c->ws[0].pdfB, RecView{nullptr, 0, 0}, 0};
         DevFilm fd = dev_film(c);
-        TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, nullptr, n, c->cull ? 1 : 0, c->ws[0].hitB, c->ws[0].hitPrim};
+        TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, QueueView{nullptr, shard_stride(n, 1), n, 1}, c->cull ? 1 : 0, c->ws[0].hitB,
+                    c->ws[0].hitPrim};
         ShadeRefIO sio = shade_ref_io(c);
         sio.rayD = c->ws[0].rayD; sio.lamA = c->ws[0].lamA; sio.lamB = c->ws[0].lamB; sio.pdfA = c->ws[0].pdfA; sio.pdfB = c->ws[0].pdfB;
         sio.hitB = c->ws[0].hitB; sio.hitPrim = c->ws[0].hitPrim;

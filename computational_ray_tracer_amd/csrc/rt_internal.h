@@ -168,22 +168,45 @@ struct GenOut {
     int lean;  // simple path kernel: no β = 1 / L = 0 / pdf stores (depth 0 and the film kernel derive them)
 };
 
-// Queue counters of a path-mode ray queue: one 256-B line each (never two hot atomics in one cache line), in a
-// region of kQRegion ints: the queue length, the chunk tickets of its trace and shade launches, and the shadow-queue
-// length and chunk ticket (multi-level octrees).
+// Ray queues are split into kShards shards, each with its own length and chunk-ticket counters: one returning
+// device-scope atomic word saturates at ~88 operations/us (MI355X_MICROARCH "dequeue"), and a 16 Mi-ray bounce makes
+// 65 k block appends (single leaf) or 262 k wave tickets + appends (multi-level) per launch.  Shard j of a queue
+// holds positions [j S, j S + len_j); a kernel processes the items of shard j into shard j of its output queue, so
+// an output shard never outgrows S.  Blocks prefer shard blockIdx % kShards (blocks are dealt round-robin to the 8
+// XCDs), waves drain other shards when theirs is empty.
+static const int kShards = 8;
+// Queue counters: one 256-B line each (never two hot atomics in one cache line), in a region of kQRegion ints:
+// per shard the queue length, the chunk tickets of its trace and shade launches, and the shadow-queue length and
+// chunk ticket (multi-level octrees).  Counter x of shard j is at x + j * kQStride.
 static const int kQStride = 64;
-enum { kQLen = 0, kQTraceTicket = 1 * kQStride, kQShadeTicket = 2 * kQStride, kQShadowLen = 3 * kQStride,
-       kQShadowTicket = 4 * kQStride, kQRegion = 5 * kQStride };
+enum { kQLen = 0, kQTraceTicket = 1 * kShards * kQStride, kQShadeTicket = 2 * kShards * kQStride,
+       kQShadowLen = 3 * kShards * kQStride, kQShadowTicket = 4 * kShards * kQStride,
+       kQRegion = 5 * kShards * kQStride };
+// Shard stride of a queue of ns shards for n items (a multiple of 64, so wave chunks stay line-aligned); capacity
+// ns * S.  Single-leaf scenes (static chunks, one block append per 256 rays) keep one shard: sharding their queues
+// cost the Cornell box 3 %; multi-level scenes (per-wave tickets and appends) use kShards (CFG3 +5.5 %).
+inline __host__ __device__ int shard_stride(int n, int ns) {
+    int s = (n + ns - 1) / ns;
+    return (s + 63) & ~63;
+}
+// A queue of ns shards: shard lengths at len[j * kQStride], or len == nullptr for the dense queue of n items in
+// positions [0, n) (shard j = [j S, min(n, (j + 1) S))).
+struct QueueView {
+    const int* len;
+    int S;
+    int n;
+    int ns;
+};
 static const int kBlockThreads = 256;  // threads per block of every kernel
 static const int kClusterTris = 2;     // leaf tiles per culling cluster (single-leaf scenes; 4 or 6: -2 %)
 
 struct TraceIO {
     const float4* rayO; const float4* rayD;
-    const int* count; int n;  // queue length in device memory (count != nullptr) or a fixed n
+    QueueView q;              // the queue's shards
     int set;                  // tile set: 0 = all triangles, 1 = back-face culled
-    float4* hitB;             // (b0, b1, b2, t) at flat index
+    float4* hitB;             // (b0, b1, b2, t) at the ray's queue position
     int* hitPrim;
-    int* ticket = nullptr;    // dynamic chunk counter (zeroed before the launch) or nullptr: static grid-stride
+    int* ticket = nullptr;    // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
 };
 
 struct ShadeRefIO {
@@ -195,18 +218,19 @@ struct ShadeRefIO {
 };
 
 struct PathIO {
-    const float4* rayO; const float4* rayD; const int* slot; const int* count;  // current queue
+    const float4* rayO; const float4* rayD; const int* slot; QueueView q;       // current queue
     const float4* hitB; const int* hitPrim;                                     // at queue position
-    float4* nO; float4* nD; int* nSlot; int* nCount;                            // next queue
+    float4* nO; float4* nD; int* nSlot; int* nCount;  // next queue: same shard stride, lengths at nCount + j kQStride
     RecView rec;                                                          // slot state (R_LAM ...)
     float4* pdfA; float4* pdfB;                                           // TerminateSecondary writes them
     int depth, max_depth;
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
-    int* ticket;  // dynamic chunk counter (zeroed before the launch) or nullptr: static grid-stride
+    int* ticket;  // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
 };
 
 // Shadow queue (multi-level octrees): the shade kernel appends NEE shadow rays {o, tMax}, {d, slot} and their
-// pending contribution instead of tracing them inline; k_path_shadow traces them.  shO == nullptr: inline.
+// pending contribution instead of tracing them inline; k_path_shadow traces them.  shO == nullptr: inline.  Sharded
+// like the ray queues (same stride; lengths and tickets at shCount / shTicket + j kQStride).
 // A separate trailing kernel argument, so PathIO (and the single-leaf kernels' code) is unchanged.
 struct ShadowQueueIO {
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
@@ -240,9 +264,11 @@ struct SortRaysIO {
     void* temp; size_t temp_bytes;
     float4 lo, scale;                                     // origin quantisation: (p - lo) * scale in [0, 512)
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin
-    const int* count = nullptr;  // device queue length: sort all n slots, entries >= *count get the largest key
+    int* len;     // the queue's shard lengths (kQLen region): read, then rewritten for the sorted queue
+    int S;        // shard stride (the sorted queue keeps it; its shards split the sorted order evenly)
 };
 size_t sort_rays_temp_bytes(int nmax);
+// n = total length of the queue's shards (read back by the host)
 hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io);
 hipError_t launch_oct_classify(hipStream_t st, int nnodes, const float* cbox, const int* seg, const int* ent,
                                const float* tri9, unsigned char* mask, int* stats);

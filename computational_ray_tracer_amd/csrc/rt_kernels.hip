@@ -97,52 +97,139 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     return pred ? base + rank : -1;
 }
 
-// Work distribution of the persistent queue kernels.  With a ticket counter (zeroed before the launch) a block takes
-// the next chunk of kBlock items whenever it finishes one, so blocks whose rays are expensive (incoherent bounces,
-// big leaves) do not hold back the launch; the next ticket is requested while the current chunk runs.  Without one,
-// block b takes chunks b, b + grid, ... of kStaticItems x kBlock items.  Every thread of the block must call next().
-static constexpr int kStaticItems = 2;  // items per thread per chunk without a ticket (single-leaf scenes)
-struct BlockChunks {
-    int* ticket;
-    int pref, it, size, lane, step;
-    __device__ __forceinline__ explicit BlockChunks(int* t)
-        : ticket(t), pref(0), it(0), size((t ? 1 : kStaticItems) * kBlock), lane(threadIdx.x),
-          step(kBlock) {
-        if (ticket && threadIdx.x == 0) pref = atomicAdd(ticket, 1);
+// Work distribution of the persistent queue kernels over a sharded queue (rt_internal.h QueueView).
+__device__ __forceinline__ int q_len(const QueueView& q, int j) {
+    if (q.len) return q.len[j * kQStride];
+    const int c = q.n - j * q.S;
+    return c < 0 ? 0 : (c > q.S ? q.S : c);
+}
+
+// Static chunks (no tickets): the chunks of kStaticItems x kBlock items are interleaved over the shards (list entry
+// 8c + j = chunk c of shard j) and block b takes entries b, b + grid, ... — with a grid that is a multiple of 8
+// (resident grids are), a block stays on shard b % 8.  Every thread of the block walks the same entries.
+static constexpr int kStaticItems = 2;  // items per thread per chunk (single-leaf scenes)
+static constexpr int kChunk = kStaticItems * kBlock;
+struct StaticChunks {
+    QueueView q;
+    int e, end;  // current list entry, list length
+    int j, len;  // its shard and that shard's length
+    __device__ __forceinline__ explicit StaticChunks(const QueueView& qv) : q(qv), e((int)blockIdx.x - (int)gridDim.x) {
+        int mx = 0;
+#pragma unroll
+        for (int k = 0; k < kShards; ++k) {
+            const int l = k < q.ns ? q_len(q, k) : 0;
+            mx = l > mx ? l : mx;
+        }
+        end = q.ns * ((mx + kChunk - 1) / kChunk);
     }
-    // first item of the block's next chunk (>= n once the queue is drained)
-    __device__ __forceinline__ int next(int* lds) {
-        if (!ticket) return (blockIdx.x + (it++) * gridDim.x) * size;
-        if (threadIdx.x == 0) { *lds = pref; pref = atomicAdd(ticket, 1); }
-        __syncthreads();
-        int c = *lds;
-        __syncthreads();
-        return c * size;
+    // next non-empty entry of this block: false when the list is done; chunk items are idx in [base, base + kChunk)
+    __device__ __forceinline__ bool next(int& base) {
+        while ((e += gridDim.x) < end) {
+            j = e % q.ns;
+            len = q_len(q, j);
+            base = (e / q.ns) * kChunk;
+            if (base < len) return true;
+        }
+        return false;
     }
 };
 
-// The same for kernels without block-level synchronisation: with a ticket each wave takes 64 items per ticket
-// (128: CFG3 -5 %); without one the block-static mapping of BlockChunks.
-struct WaveChunks {
-    int* ticket;
-    int pref, it, size, lane, step;
-    __device__ __forceinline__ explicit WaveChunks(int* t) : ticket(t), pref(0), it(0) {
-        if (ticket) {
-            size = 64; lane = lane_id(); step = 64;
-            if (lane == 0) pref = atomicAdd(ticket, 1);
-        } else {
-            size = kStaticItems * kBlock; lane = threadIdx.x; step = kBlock;
+// Wave tickets: a wave takes 64-item chunks of its preferred shard (blockIdx % 8) from that shard's ticket counter
+// (the next ticket is requested while the current chunk runs), then drains the other shards in turn.  A shard whose
+// ticket already passed its length is skipped without an atomic.
+struct WaveTickets {
+    int* tk;
+    QueueView q;
+    int j0, tries, j, len, pref;
+    __device__ __forceinline__ int grab(int jj, int l) {
+        int t = 0;
+        if (lane_id() == 0 && l > 0) {
+            t = __hip_atomic_load(tk + jj * kQStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t * 64 < l) t = atomicAdd(tk + jj * kQStride, 1);
+        }
+        return t;
+    }
+    __device__ __forceinline__ WaveTickets(int* t, const QueueView& qv) : tk(t), q(qv) {
+        j0 = (int)(blockIdx.x % (unsigned)q.ns);
+        tries = 0;
+        j = j0;
+        len = q_len(q, j);
+        pref = grab(j, len);
+    }
+    // next chunk: shard jj, items idx in [base, min(base + 64, len)); false when every shard is drained
+    __device__ __forceinline__ bool next(int& jj, int& base) {
+        while (true) {
+            const int t = __shfl(pref, 0);
+            if (t * 64 < len) {
+                jj = j;
+                base = t * 64;
+                if (lane_id() == 0) pref = atomicAdd(tk + j * kQStride, 1);
+                return true;
+            }
+            if (++tries >= q.ns) return false;
+            j = (j0 + tries) % q.ns;
+            len = q_len(q, j);
+            pref = grab(j, len);
         }
     }
-    __device__ __forceinline__ int next() {
-        if (!ticket) return (blockIdx.x + (it++) * gridDim.x) * size;
-        int c = __shfl(pref, 0);
-        if (lane == 0) pref = atomicAdd(ticket, 1);
-        return c * size;
-    }
-    __device__ __forceinline__ int next(int*) { return next(); }
 };
-// Append to the next queue: per wave (WaveChunks kernels, no block-level synchronisation) or per block.
+
+// The items of a queue for kernels that append (every thread of the block, or of the wave, calls next() in step):
+// WAVE = per-wave tickets (one item per lane per chunk), otherwise the block's static chunks (kStaticItems steps per
+// chunk).  Yields the shard j, the index within it and whether this lane's item exists.
+template <bool WAVE>
+struct QueueItems;
+template <>
+struct QueueItems<true> {
+    WaveTickets tk;
+    __device__ __forceinline__ QueueItems(int* t, const QueueView& q) : tk(t, q) {}
+    __device__ __forceinline__ bool next(int& j, int& idx, bool& live) {
+        int base;
+        if (!tk.next(j, base)) return false;
+        idx = base + lane_id();
+        live = idx < tk.len;
+        return true;
+    }
+};
+template <>
+struct QueueItems<false> {
+    StaticChunks ch;
+    int base, r;
+    __device__ __forceinline__ QueueItems(int*, const QueueView& q) : ch(q), base(0), r(kStaticItems) {}
+    __device__ __forceinline__ bool next(int& j, int& idx, bool& live) {
+        if (r >= kStaticItems) {
+            if (!ch.next(base)) return false;
+            r = 0;
+        }
+        j = ch.j;
+        idx = base + r * kBlock + (int)threadIdx.x;
+        ++r;
+        live = idx < ch.len;
+        return true;
+    }
+};
+
+// One shard, static chunks (single-leaf scenes): block b takes chunks b, b + grid, ... of the queue's only shard.
+struct QueueItemsOne {
+    int n, c, r;
+    __device__ __forceinline__ QueueItemsOne(int*, const QueueView& q)
+        : n(q_len(q, 0)), c((int)blockIdx.x), r(0) {}
+    __device__ __forceinline__ bool next(int& j, int& idx, bool& live) {
+        if (r == kStaticItems) {
+            r = 0;
+            c += gridDim.x;
+        }
+        const int base = c * kChunk;
+        if (base >= n) return false;
+        j = 0;
+        idx = base + r * kBlock + (int)threadIdx.x;
+        ++r;
+        live = idx < n;
+        return true;
+    }
+};
+
+// Append to the next queue: per wave (ticket kernels, no block-level synchronisation) or per block.
 template <bool WAVE>
 __device__ __forceinline__ int queue_append(int* counter, bool pred, int* lds) {
     if constexpr (WAVE) return wave_append(counter, pred);
@@ -962,53 +1049,15 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
-    const int n = io.count ? *io.count : io.n;
     if constexpr (QCAP == 1) stage_leaf1(sc, io.set);
     ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
-    // no block-level synchronisation here: each wave takes its own tickets (WaveChunks).  Without tickets (single
-    // leaf) a thread's items are k(j) = (block + (j / S) grid) S kBlock + (j % S) kBlock + thread, S = kStaticItems,
-    // and the next item's ray is loaded while the current one is traced.
-    if (!io.ticket) {
-        auto item = [&](int j) {
-            return (blockIdx.x + (j / kStaticItems) * gridDim.x) * (kStaticItems * kBlock) + (j % kStaticItems) * kBlock +
-                   (int)threadIdx.x;
-        };
-        int k = item(0);
-        float4 o4 = make_float4(0, 0, 0, 0), d4 = o4;
-        if (k < n) { o4 = io.rayO[k]; d4 = io.rayD[k]; }
-        for (int j = 1; k < n; ++j) {
-            const int kn = item(j);
-            float4 on = o4, dn = d4;
-            if (kn < n) { on = io.rayO[kn]; dn = io.rayD[kn]; }
-            float b0 = 0, b1 = 0, b2 = 0, t = 0;
-            int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z),
-                                                 3.402823466e+38f, b0, b1, b2, t, nn, nt, nfb);
-            if (sc.n_shapes) {
-                float tm = prim >= 0 ? t : 3.402823466e+38f;
-                for (int si = 0; si < sc.n_shapes; ++si) {
-                    DevShape sh = ldconst(sc.shapes, si);
-                    V3 ph;
-                    float th;
-                    if (shape_isect(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
-                        prim = sc.n_tris + si; b0 = ph.x; b1 = ph.y; b2 = ph.z; t = th; tm = th;
-                    }
-                }
-            }
-            io.hitB[k] = make_float4(b0, b1, b2, t);
-            io.hitPrim[k] = prim;
-            nh += prim >= 0;
-            nr += 1;
-            k = kn; o4 = on; d4 = dn;
-        }
-    } else {
-    WaveChunks chunks(io.ticket);
-    for (int cb = chunks.next(); cb < n; cb = chunks.next())
-    for (int k = cb + chunks.lane; k < cb + chunks.size && k < n; k += chunks.step) {
-        float4 o4 = io.rayO[k], d4 = io.rayD[k];
+    // one ray at queue position p: octree (BVH / BFS), then the analytic shapes with the running tMax (DESIGN.md §5;
+    // hitB = object-space point for a shape)
+    auto trace_one = [&](int p, float4 o4, float4 d4) __attribute__((always_inline)) {
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
         int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
                                              b0, b1, b2, t, nn, nt, nfb);
-        if (sc.n_shapes) {  // analytic shapes after the octree, running tMax; hitB = object-space point
+        if (sc.n_shapes) {
             float tm = prim >= 0 ? t : 3.402823466e+38f;
             for (int si = 0; si < sc.n_shapes; ++si) {
                 DevShape sh = ldconst(sc.shapes, si);
@@ -1019,11 +1068,53 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                 }
             }
         }
-        io.hitB[k] = make_float4(b0, b1, b2, t);
-        io.hitPrim[k] = prim;
+        io.hitB[p] = make_float4(b0, b1, b2, t);
+        io.hitPrim[p] = prim;
         nh += prim >= 0;
         nr += 1;
-    }
+    };
+    // no block-level synchronisation here.  Static chunks (single leaf, dense queues) or per-wave tickets.  One shard
+    // (single leaf): a thread's items are k(i) = (block + (i / S) grid) S kBlock + (i % S) kBlock + thread,
+    // S = kStaticItems, and the next item's ray is loaded while the current one is traced.
+    if (!io.ticket && io.q.ns == 1) {
+        const int n = q_len(io.q, 0);
+        auto item = [&](int i) {
+            return (blockIdx.x + (i / kStaticItems) * gridDim.x) * kChunk + (i % kStaticItems) * kBlock +
+                   (int)threadIdx.x;
+        };
+        int k = item(0);
+        float4 o4 = make_float4(0, 0, 0, 0), d4 = o4;
+        if (k < n) { o4 = io.rayO[k]; d4 = io.rayD[k]; }
+        for (int i = 1; k < n; ++i) {
+            const int kn = item(i);
+            float4 on = o4, dn = d4;
+            if (kn < n) { on = io.rayO[kn]; dn = io.rayD[kn]; }
+            trace_one(k, o4, d4);
+            k = kn; o4 = on; d4 = dn;
+        }
+    } else if (!io.ticket) {
+        StaticChunks ch(io.q);
+        int base;
+        while (ch.next(base)) {
+#pragma unroll 1
+            for (int r = 0; r < kStaticItems; ++r) {  // (one copy of the traversal: no unrolling)
+                const int idx = base + r * kBlock + (int)threadIdx.x;
+                if (idx < ch.len) {
+                    const int p = ch.j * io.q.S + idx;
+                    trace_one(p, io.rayO[p], io.rayD[p]);
+                }
+            }
+        }
+    } else {
+        WaveTickets tk(io.ticket, io.q);
+        int j, base;
+        while (tk.next(j, base)) {
+            const int idx = base + lane_id();
+            if (idx < tk.len) {
+                const int p = j * io.q.S + idx;
+                trace_one(p, io.rayO[p], io.rayD[p]);
+            }
+        }
     }
     count_add(ctr, C_NODES, nn);
     count_add(ctr, C_TRIS, nt);
@@ -1151,24 +1242,24 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
     const float InvPi = 0.31830988618379067154f;
     if constexpr (QCAP == 1) stage_leaf1(sc, 0);
     __shared__ int lds[kBlock / 64 + 1];
-    const int n = *io.count;
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = QCAP != 1;
-    __shared__ int s_tk;
-    std::conditional_t<WAVE, WaveChunks, BlockChunks> chunks(io.ticket);
-    for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
-    for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
-        int k = base + chunks.lane;
+    // single leaf: the host gives the queues one shard (rt_host.cpp nsh)
+    std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<WAVE>> items(io.ticket, io.q);
+    int qj, qidx;
+    bool live;
+    while (items.next(qj, qidx, live)) {
+        const int k = qj * io.q.S + qidx;  // queue position
         bool wantShadow = false, wantNext = false, storedL = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         V3 so = v3(0, 0, 0), sd = so;
         float stmax = 0.f;
         float Ld[8];
         int slot = -1;
-        if (k < n) {
+        if (live) {
             slot = io.slot[k];
             const int prim = io.hitPrim[k];
             if (prim >= 0) {
@@ -1257,7 +1348,9 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         }
         if constexpr (QCAP != 1) {  // shadow queue: the ray and its pending contribution go to k_path_shadow
             if (shq.shO) {
-                int sp = WAVE ? wave_append(shq.shCount, wantShadow) : block_append(shq.shCount, wantShadow, lds);
+                int sp = WAVE ? wave_append(shq.shCount + qj * kQStride, wantShadow)
+                              : block_append(shq.shCount + qj * kQStride, wantShadow, lds);
+                sp += qj * io.q.S;
                 if (wantShadow) {
                     shq.shO[sp] = make_float4(so.x, so.y, so.z, stmax);
                     shq.shD[sp] = make_float4(sd.x, sd.y, sd.z, __int_as_float(slot));
@@ -1286,7 +1379,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
             const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             rstore8(io.rec, slot, R_L, z);
         }
-        const int pn = queue_append<WAVE>(io.nCount, wantNext, lds);
+        const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1302,13 +1395,12 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
 // between this bounce's shade and the next one's, so every L sees its additions in the same order.
 template <int QCAP, bool DFS>
 __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
-    const int n = *shq.shCount;
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
-    WaveChunks chunks(shq.shTicket);
-    for (int cb = chunks.next(); cb < n; cb = chunks.next())
-    for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
-        int k = base + chunks.lane;
-        if (k >= n) continue;
+    WaveTickets tk(shq.shTicket, QueueView{shq.shCount, io.q.S, 0, io.q.ns});
+    int qj, base;
+    while (tk.next(qj, base)) {
+        if (base + lane_id() >= tk.len) continue;  // (reconverges at the loop latch, before the next ticket)
+        const int k = qj * io.q.S + base + lane_id();
         float4 o4 = shq.shO[k], d4 = shq.shD[k];
         float b0, b1, b2, t;
         int hit = traverse_any<QCAP, true, DFS>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), o4.w, b0, b1, b2,
@@ -1375,19 +1467,19 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
     const float InvPi = 0.31830988618379067154f;
     if constexpr (QCAP == 1) stage_leaf1(sc, 0);
     __shared__ int lds[kBlock / 64 + 1];
-    const int n = *io.count;
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = QCAP != 1;
-    __shared__ int s_tk;
-    std::conditional_t<WAVE, WaveChunks, BlockChunks> chunks(io.ticket);
-    for (int cb = chunks.next(&s_tk); cb < n; cb = chunks.next(&s_tk))
-    for (int base = cb; base < cb + chunks.size && base < n; base += chunks.step) {
-        int k = base + chunks.lane;
+    // single leaf: the host gives the queues one shard (rt_host.cpp nsh)
+    std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<WAVE>> items(io.ticket, io.q);
+    int qj, qidx;
+    bool live;
+    while (items.next(qj, qidx, live)) {
+        const int k = qj * io.q.S + qidx;  // queue position
         bool wantNext = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int slot = -1;
-        if (k < n) {
+        if (live) {
             slot = io.slot[k];
             int prim = io.hitPrim[k];
             if (prim >= 0) {
@@ -1584,7 +1676,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                 }
             }
         }
-        const int pn = queue_append<WAVE>(io.nCount, wantNext, lds);
+        const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1721,7 +1813,7 @@ hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& id
 
 hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
                                 unsigned long long* ctr) {
-    int gb = grid_for(io.count ? grid * kBlock : io.n, grid);
+    int gb = grid_for(io.q.len ? grid * kBlock : io.q.n, grid);
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
     switch (qcap) {

@@ -22,19 +22,26 @@ __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every th
 }
 
 // key = direction octant, then the octahedral position of the direction on a 2^B x 2^B grid, then a Morton code of
-// the origin with O bits per axis (DESIGN.md §6 key table)
-__global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const float4* __restrict__ o,
+// the origin with O bits per axis (DESIGN.md §6 key table).  Entry k of the sort is the k-th live ray of the sharded
+// queue (shards in order); its value is the ray's queue position.
+__global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const int* __restrict__ len, int S,
+                                                              const float4* __restrict__ o,
                                                               const float4* __restrict__ d, float4 lo, float4 scale,
                                                               int kDirB, int kOrgB, unsigned* __restrict__ keys,
-                                                              int* __restrict__ vals, const int* __restrict__ count) {
-    const int nv = count ? *count : n;  // slots past the device count sort last (largest key, stable)
+                                                              int* __restrict__ vals) {
+    int pre[kShards + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int j = 0; j < kShards; ++j) pre[j + 1] = pre[j] + len[j * kQStride];
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        if (k >= nv) {
-            keys[k] = 0xffffffffu;
-            vals[k] = k;
-            continue;
-        }
-        float4 p = o[k], v = d[k];
+        int j = 0;
+#pragma unroll
+        for (int u = 1; u < kShards; ++u) j += k >= pre[u] ? 1 : 0;
+        int base = pre[0];
+#pragma unroll
+        for (int u = 1; u < kShards; ++u) base = j == u ? pre[u] : base;
+        const int pos = j * S + (k - base);
+        float4 p = o[pos], v = d[pos];
         auto q = [](float x) {
             x = x < 0.f ? 0.f : (x > 511.f ? 511.f : x);
             return (unsigned)x;
@@ -47,22 +54,29 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const float4
                       spread3(q((p.y - lo.y) * scale.y) >> (9 - kOrgB)) << 1 |
                       spread3(q((p.z - lo.z) * scale.z) >> (9 - kOrgB));
         keys[k] = ((oct << (2 * kDirB) | ux << kDirB | uy) << (3 * kOrgB)) | mo;
-        vals[k] = k;
+        vals[k] = pos;
     }
 }
 
-__global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int* __restrict__ perm,
+// sorted entry k -> shard k / S2 of the side queue (S2 = shard_stride(n, kShards) <= S; sorted queues have kShards: the sorted order split evenly over
+// the shards), and the side queue's shard lengths replace the queue's (every reader of this bounce uses the side
+// queue)
+__global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int* __restrict__ perm, int S, int S2,
                                                                 const float4* __restrict__ o,
                                                                 const float4* __restrict__ d,
                                                                 const int* __restrict__ slot, float4* __restrict__ so,
                                                                 float4* __restrict__ sd, int* __restrict__ ss,
-                                                                const int* __restrict__ count) {
-    const int nv = count ? *count : n;
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nv; k += gridDim.x * blockDim.x) {
-        int j = perm[k];
-        so[k] = o[j];
-        sd[k] = d[j];
-        ss[k] = slot[j];
+                                                                int* __restrict__ len) {
+    if (blockIdx.x == 0 && threadIdx.x < kShards) {
+        const int c = n - (int)threadIdx.x * S2;
+        len[threadIdx.x * kQStride] = c < 0 ? 0 : (c > S2 ? S2 : c);
+    }
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const int j = perm[k];
+        const int pos = (k / S2) * S + k % S2;
+        so[pos] = o[j];
+        sd[pos] = d[j];
+        ss[pos] = slot[j];
     }
 }
 
@@ -80,14 +94,14 @@ hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
     int g = (n + kBlockThreads - 1) / kBlockThreads;
     g = g < 8192 ? g : 8192;
     const int key_bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
-    hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.o, io.d, io.lo, io.scale, io.dir_bits,
-                       io.org_bits, io.keys, io.vals, io.count);
+    hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.len, io.S, io.o, io.d, io.lo, io.scale,
+                       io.dir_bits, io.org_bits, io.keys, io.vals);
     size_t bytes = io.temp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
                                                       key_bits, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.o, io.d, io.slot, io.so,
-                       io.sd, io.ss, io.count);
+    hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.S, shard_stride(n, kShards),
+                       io.o, io.d, io.slot, io.so, io.sd, io.ss, io.len);
     return hipGetLastError();
 }
 
