@@ -665,6 +665,25 @@ int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
 }
 int ensure_workspace(rt_ctx* c, size_t n, bool path) { return ensure_workspace(c, c->ws[0], n, path); }
 
+// Sampler dimension bookkeeping of the simple path integrator (rt_device.h Smp): every path of a depth has drawn
+// the same dimensions — the camera sample, then two Get2D per bounce — so the shade kernel takes its starting
+// dimension as an argument instead of a per-slot field.  (A stratified sample with index >= spp draws zeros without
+// advancing; its dimension is never read again.)
+static int dim_get2d(const DevSampler& S, int dim) {
+    if (S.kind == 1) return dim + 2;
+    if (S.kind == 2) return (dim + 1 >= kSobolDims ? 2 : dim) + 2;
+    return dim;
+}
+static int dim_after_camera(const DevSampler& S, const DevCamera& cam) {
+    int dim = S.kind == 2 ? 2 : 0;                                                // StartPixelSample
+    if (S.kind == 1) dim += 1;                                                    // Get1D (wavelengths)
+    else if (S.kind == 2) dim = (dim >= kSobolDims ? 2 : dim) + 1;
+    if (S.kind == 1) dim += 2;                                                    // GetPixel2D
+    if ((cam.type == RT_CAMERA_PERSPECTIVE && cam.lens_radius > 0) || cam.type > RT_CAMERA_PINHOLE)
+        dim = dim_get2d(S, dim);                                                  // lens sample
+    return dim;
+}
+
 hipEvent_t ev_get(rt_ctx* c) {
     if (!c->pool.empty()) {
         hipEvent_t e = c->pool.back();
@@ -1022,6 +1041,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const bool records = c->dsc.qcap != 1;
     const size_t rec_fs = records ? 1 : nmax;
     const unsigned rec_ss = records ? (unsigned)kRecF4 : 1u;
+    const int rec_rng8 = !records && lean ? 1 : 0;  // SoA simple path: dense 8-byte PCG states
     int last_film = -1;      // lane of the most recent film launch
     for (int g0 = ib; g0 < ie; g0 += B * lanes) {
         int nIdx[kLanes] = {0}, cur[kLanes] = {0}, nSq[kLanes] = {0}, Sq[kLanes] = {0};
@@ -1030,7 +1050,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             if (b0 >= ie) break;
             Work& w = c->ws[l];
             hipStream_t s = lstream(l);
-            const RecView rv{w.rec, rec_fs, rec_ss};
+            const RecView rv{w.rec, rec_fs, rec_ss, rec_rng8};
             nIdx[l] = std::min(B, ie - b0);
             int nS = nIdx[l] * c->n_work;
             nSq[l] = nS;
@@ -1050,7 +1070,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             for (int l = 0; l < lanes && nIdx[l] > 0; ++l) {
                 Work& w = c->ws[l];
                 hipStream_t s = lstream(l);
-                const RecView rv{w.rec, rec_fs, rec_ss};
+                const RecView rv{w.rec, rec_fs, rec_ss, rec_rng8};
                 SampleIds ids{c->d_work, c->n_work, g0 + l * B, nullptr, nullptr};
                 int nxt = cur[l] ^ 1;
                 const float4* cO = w.rayO + (size_t)cur[l] * qs;
@@ -1091,8 +1111,13 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
                 pio.nO = w.rayO + (size_t)nxt * qs; pio.nD = w.rayD + (size_t)nxt * qs;
                 pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt + kQLen;
-                pio.rec = RecView{w.rec, rv.fs, rv.ss}; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
+                pio.rec = rv; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
+                pio.dim = -1;
+                if (lean) {
+                    pio.dim = dim_after_camera(smp, cam);
+                    for (int d = 0; d < depth; ++d) pio.dim = dim_get2d(smp, dim_get2d(smp, pio.dim));
+                }
                 pio.ticket = dyn ? qc_cur + kQShadeTicket : nullptr;
                 ShadowQueueIO sqio{};
                 if (shq) {  // this queue's region holds the shadow-queue length and ticket (zeroed with it)
@@ -1114,9 +1139,9 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
         for (int l = 0; l < lanes && nIdx[l] > 0; ++l) {
             Work& w = c->ws[l];
             hipStream_t s = lstream(l);
-            const RecView rv{w.rec, rec_fs, rec_ss};
+            const RecView rv{w.rec, rec_fs, rec_ss, rec_rng8};
             if (last_film >= 0 && last_film != l) HIPCHK(c, hipStreamWaitEvent(s, c->ws[last_film].film_done, 0));
-            PathFilmIO fio{c->d_work, c->n_work, nIdx[l], RecView{w.rec, rv.fs, rv.ss}, w.pdfA, w.pdfB, film};
+            PathFilmIO fio{c->d_work, c->n_work, nIdx[l], rv, w.pdfA, w.pdfB, film};
             fio.lean = lean ? 1 : 0;
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_path_film(s, 0, c->d_spec, fd, fio, c->d_ctr));

@@ -159,13 +159,16 @@ struct RecView {
     float4* p;
     size_t fs;    // float4s between fields
     unsigned ss;  // float4s between slots
+    int rng8;     // 1: the R_RNG field holds only the 8-byte PCG state per slot, densely (uint2 array; SoA simple path
+                  // scenes), the increment is recomputed from the pixel hash; 0: state + increment (uint4)
 };
 
 struct GenOut {
     float4* rayO; float4* rayD; int* slot;
     float4* lamA; float4* lamB; float4* pdfA; float4* pdfB;  // reference mode (lamA/lamB) + pdfs
     RecView rec;                                             // path mode: the slot state (λ, sampler, β, L, ...)
-    int lean;  // simple path kernel: no β = 1 / L = 0 / pdf stores (depth 0 and the film kernel derive them)
+    int lean;  // simple path kernel: no β = 1 / L = 0 / pdf / dimension stores (depth 0, the film kernel and the
+               // host's per-depth dimension derive them)
 };
 
 // Ray queues are split into kShards shards, each with its own length and chunk-ticket counters: one returning
@@ -225,6 +228,8 @@ struct PathIO {
     float4* pdfA; float4* pdfB;                                           // TerminateSecondary writes them
     int depth, max_depth;
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
+    int dim;    // >= 0: the sampler dimension every path of this depth starts from (simple path: each bounce takes
+                // two Get2D); -1: per slot in R_MISC
     int* ticket;  // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
 };
 

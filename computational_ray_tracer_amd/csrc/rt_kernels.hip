@@ -290,6 +290,7 @@ __device__ __forceinline__ void rstore8(const RecView& r, int slot, int f, const
     float4* q = recf(r, slot, f);
     store8(q, q + r.fs, 0, v);
 }
+__device__ __forceinline__ uint2* rng8_state(const RecView& r) { return reinterpret_cast<uint2*>(r.p + R_RNG * r.fs); }
 __device__ __forceinline__ float rec_prev_pdf(const RecView& r, int slot) { return recf(r, slot, R_MISC)->y; }
 __device__ __forceinline__ void rec_set_prev_pdf(const RecView& r, int slot, float p) {
     reinterpret_cast<float*>(recf(r, slot, R_MISC))[1] = p;
@@ -379,11 +380,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         if (!out.lean) store8(out.pdfA, out.pdfB, s, pdf);
         if (out.rec.p) {  // path mode: the slot's state
             rstore8(out.rec, s, R_LAM, lam);
-            *reinterpret_cast<uint4*>(recf(out.rec, s, R_RNG)) =
-                make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
-                           (uint32_t)(sm.rng.inc >> 32));
-            *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, 0.f);  // (dimension, prevPdf 0)
+            if (out.rec.rng8)
+                rng8_state(out.rec)[s] = make_uint2((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32));
+            else
+                *reinterpret_cast<uint4*>(recf(out.rec, s, R_RNG)) =
+                    make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
+                               (uint32_t)(sm.rng.inc >> 32));
             if (!out.lean) {
+                *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, 0.f);  // (dimension, prevPdf 0)
                 const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
                 const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 rstore8(out.rec, s, R_BETA, one);
@@ -1205,19 +1209,29 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 // pending contribution added on a miss) and a cosine-hemisphere bounce (Get2D, β *= R) appended to the next queue.
 // Sampler state (PCG state + dimension) lives per path slot.
 __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevFilm& film, const PathIO& io, int slot,
-                                                Smp& sm) {
+                                                Smp& sm, int smp_kind, int smp_seed) {
     int pixel, index, x, y;
     sample_of(ids, slot, pixel, index);
     pixel_xy(film, pixel, x, y);
-    const uint4 rs = *reinterpret_cast<const uint4*>(recf(io.rec, slot, R_RNG));
-    sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
-    sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
-    sm.px = x; sm.py = y; sm.index = index; sm.dim = __float_as_int(recf(io.rec, slot, R_MISC)->x);
+    if (io.rec.rng8) {
+        const uint2 st = rng8_state(io.rec)[slot];
+        sm.rng.state = (uint64_t)st.x | ((uint64_t)st.y << 32);
+        // the increment SetSequence gave the path (rng.h:36-39); Sobol keeps its index in the state
+        sm.rng.inc = smp_kind == 2 ? 0ull : (hash_pixel(x, y, smp_seed) << 1u) | 1u;
+    } else {
+        const uint4 rs = *reinterpret_cast<const uint4*>(recf(io.rec, slot, R_RNG));
+        sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
+        sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
+    }
+    sm.px = x; sm.py = y; sm.index = index;
+    sm.dim = io.dim >= 0 ? io.dim : __float_as_int(recf(io.rec, slot, R_MISC)->x);
 }
 // the PCG increment of a path never changes after generation: only the 8-byte state half is written back
 __device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm) {
-    *reinterpret_cast<uint2*>(recf(io.rec, slot, R_RNG)) = make_uint2((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32));
-    *reinterpret_cast<int*>(recf(io.rec, slot, R_MISC)) = sm.dim;
+    const uint2 st = make_uint2((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32));
+    if (io.rec.rng8) rng8_state(io.rec)[slot] = st;
+    else *reinterpret_cast<uint2*>(recf(io.rec, slot, R_RNG)) = st;
+    if (io.dim < 0) *reinterpret_cast<int*>(recf(io.rec, slot, R_MISC)) = sm.dim;
 }
 // cosine-hemisphere direction (Sampling.h:449-454) in the pbrt CoordinateSystem frame of nrm; false when z == 0
 __device__ __forceinline__ bool cosine_bounce(float u0, float u1, V3 nrm, V3& wi, float& z) {
@@ -1298,7 +1312,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
 #pragma unroll
                     for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.x, mt.y, mt.z, lam[i]);
                     Smp sm;
-                    restore_sampler(ids, film, io, slot, sm);
+                    restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed);
                     // --- NEE on the quad light
                     float u0, u1;
                     sm.get2d(smp, u0, u1);
@@ -1558,7 +1572,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                         rec_set_prev_pdf(io.rec, slot, 0.f);
                     } else {
                         Smp sm;
-                        restore_sampler(ids, film, io, slot, sm);
+                        restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed);
                         if (mt.type == 2) {  // smooth dielectric
                             if (mt.eta == 0) {  // dispersive BK7: TerminateSecondary (spectrum.h:302-310)
                                 float pdf[8];
