@@ -446,6 +446,10 @@ struct Work {
     // shadow queue (multi-level octrees): {o, tMax}, {d, slot}, pending contribution (2 x float4)
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
     size_t shCap = 0;
+    // deferred NEE of the mixed-scene shade (rt_internal.h NeeIO): records per slot, the NEE queue's slots
+    float4* neeRec = nullptr;
+    int* neeSlot = nullptr;
+    size_t neeRecCap = 0, neeSlotCap = 0;  // float4s, ints
     // BFS FIFO overflow ring of the multi-level traversal (qcap 0): one per lane, because the lanes' kernels run
     // concurrently and index the ring by their own global thread id
     int* ring = nullptr;
@@ -558,11 +562,31 @@ void free_scene(rt_ctx* c) {
 }
 
 void free_shadow_workspace(Work& w) {
-    void* ptrs[] = {w.shO, w.shD, w.shLA, w.shLB};
+    void* ptrs[] = {w.shO, w.shD, w.shLA, w.shLB, w.neeRec, w.neeSlot};
     for (void* p : ptrs)
         if (p) hipFree(p);
     w.shO = w.shD = w.shLA = w.shLB = nullptr;
-    w.shCap = 0;
+    w.neeRec = nullptr;
+    w.neeSlot = nullptr;
+    w.shCap = w.neeRecCap = w.neeSlotCap = 0;
+}
+
+int ensure_nee_workspace(rt_ctx* c, Work& w, size_t rec_f4, size_t nq) {
+    if (w.neeRecCap < rec_f4) {
+        if (w.neeRec) hipFree(w.neeRec);
+        w.neeRec = nullptr;
+        w.neeRecCap = 0;
+        HIPCHK(c, dalloc(&w.neeRec, rec_f4));
+        w.neeRecCap = rec_f4;
+    }
+    if (w.neeSlotCap < nq) {
+        if (w.neeSlot) hipFree(w.neeSlot);
+        w.neeSlot = nullptr;
+        w.neeSlotCap = 0;
+        HIPCHK(c, dalloc(&w.neeSlot, nq));
+        w.neeSlotCap = nq;
+    }
+    return RT_OK;
 }
 
 int ensure_shadow_workspace(rt_ctx* c, Work& w, size_t n) {
@@ -1026,6 +1050,11 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     if (shq)
         for (int l = 0; l < lanes; ++l)
             if ((rc = ensure_shadow_workspace(c, c->ws[l], ncap))) return rc;
+    // mixed scenes: NEE deferred to k_path_nee (one record per slot, one queue entry per Lambert vertex)
+    const bool nee = c->dsc.full && c->dsc.n_lights > 0;
+    if (nee)
+        for (int l = 0; l < lanes; ++l)
+            if ((rc = ensure_nee_workspace(c, c->ws[l], nmax * (size_t)nee_stride(c->dsc.n_lights), ncap))) return rc;
     // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
     // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
     // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
@@ -1125,9 +1154,16 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     sqio.shCount = qc_cur + kQShadowLen;
                     sqio.shTicket = qc_cur + kQShadowTicket;
                 }
+                NeeIO nio{};
+                if (nee) nio = NeeIO{w.neeRec, w.neeSlot, qc_cur + kQShadowLen, qc_cur + kQShadowTicket};
                 e0 = ev_start(c, s);
-                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio));
+                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio, nio));
                 ev_mark(c, s, ST_SHADE, e0);
+                if (nee) {  // this bounce's shadow rays, before the next bounce reads L
+                    e0 = ev_start(c, s);
+                    HIPCHK(c, launch_path_nee(s, grid, c->dsc.qcap, dsl, c->d_spec, pio, nio, c->d_ctr));
+                    ev_mark(c, s, ST_SHADOW, e0);
+                }
                 if (shq) {
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_path_shadow(s, grid, c->dsc.qcap, c->shadow_dfs != 0, dsl, pio, sqio, c->d_ctr));

@@ -242,6 +242,22 @@ struct ShadowQueueIO {
     int *shCount = nullptr, *shTicket = nullptr;
 };
 
+// Deferred NEE of the mixed-scene shade: k_path_shade_full samples every light at a Lambert vertex (same sampler
+// dimensions and order as inline) and leaves one NEE record per slot — {po.xyz, -}, per light {wi.xyz, tMax}
+// (tMax < 0: the light is skipped), the light weights 4 per float4, then x[8] = β (R / π) — and appends the slot to
+// the NEE queue (sharded like the ray queues, counters at kQShadowLen / kQShadowTicket); k_path_nee traces a
+// vertex's shadow rays in light order and adds the visible lights' terms to L in that order, so L is bit-identical
+// to the inline loop.  The traversals no longer share a kernel with the path state (CFG4: 198 VGPRs unbudgeted,
+// 464-656 B/lane spill under the 4-wave budget).
+inline __host__ __device__ int nee_stride(int n_lights) { return 3 + n_lights + (n_lights + 3) / 4; }  // float4s
+enum { N_PO = 0, N_RAY = 1 };  // N_WGT = 1 + n, N_X = 1 + n + ceil(n / 4)
+struct NeeIO {
+    float4* rec;   // NEE records, nee_stride(n_lights) float4s per slot; nullptr: inline NEE (not used)
+    int* slot;     // NEE queue: slot per position (same shard stride as the ray queues)
+    int* len;      // shard lengths (zeroed with the queue's counter region)
+    int* ticket;   // per-shard chunk tickets of k_path_nee
+};
+
 struct PathFilmIO {
     const int* work_pixels; int n_pixels; int n_index;
     RecView rec; const float4* pdfA; const float4* pdfB;
@@ -287,9 +303,12 @@ hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, cons
                               const ShadowQueueIO& shq, unsigned long long* ctr);
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
-                             unsigned long long* ctr, const ShadowQueueIO& shq = ShadowQueueIO{});
+                             unsigned long long* ctr, const ShadowQueueIO& shq = ShadowQueueIO{},
+                             const NeeIO& nee = NeeIO{});
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr);
+hipError_t launch_path_nee(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
+                           const PathIO& io, const NeeIO& nee, unsigned long long* ctr);
 hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* m_xyz_from_sensor,
                           const float* m_rgb_from_xyz, unsigned char* out, int srgb);
 hipError_t launch_film_gather(hipStream_t st, int n, const int* work, const float4* film, float4* out);

@@ -1477,11 +1477,10 @@ template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(DevScene sc, const DevSpectra* sp,
                                                                               DevSampler smp, DevFilm film,
                                                                               SampleIds ids, PathIO io,
-                                                                              unsigned long long* ctr) {
+                                                                              NeeIO nee) {
     const float InvPi = 0.31830988618379067154f;
-    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
     __shared__ int lds[kBlock / 64 + 1];
-    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
+    const int nee_f4 = nee_stride(sc.n_lights);
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = QCAP != 1;
     // single leaf: the host gives the queues one shard (rt_host.cpp nsh)
@@ -1490,17 +1489,16 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
     bool live;
     while (items.next(qj, qidx, live)) {
         const int k = qj * io.q.S + qidx;  // queue position
-        bool wantNext = false;
+        bool wantNext = false, wantNee = false;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int slot = -1;
         if (live) {
             slot = io.slot[k];
             int prim = io.hitPrim[k];
             if (prim >= 0) {
-                float lam[8], beta[8], L[8];
+                float lam[8], beta[8];
                 rload8(io.rec, slot, R_LAM, lam);
                 rload8(io.rec, slot, R_BETA, beta);
-                rload8(io.rec, slot, R_L, L);
                 float4 o4 = io.rayO[k], d4 = io.rayD[k];
                 V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
                 V3 rayd = vnorm(rdw);
@@ -1539,6 +1537,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                 float prevPdf = rec_prev_pdf(io.rec, slot);
                 if (mt.emit > 0) {  // one-sided pure emitter, ends the path
                     if (front) {
+                        float L[8];
+                        rload8(io.rec, slot, R_L, L);
                         if (prevPdf == 0) {
 #pragma unroll
                             for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.emit * dense_query(sp->D65, lam[i]));
@@ -1607,16 +1607,18 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                             nO = make_float4(po.x, po.y, po.z, 0.f);
                             nD = make_float4(wi.x, wi.y, wi.z, 0.f);
                             rec_set_prev_pdf(io.rec, slot, 0.f);
-                        } else {  // Lambert: NEE per light, then a cosine-hemisphere bounce
+                        } else {  // Lambert: NEE per light (deferred to k_path_nee), then a cosine-hemisphere bounce
                             V3 po = vadd(p, vmul(nrm, off));
+                            float4* nr = nee.rec + (size_t)slot * nee_f4;
+                            float* nwgt = reinterpret_cast<float*>(nr + N_RAY + sc.n_lights);
+                            nr[N_PO] = make_float4(po.x, po.y, po.z, 0.f);
                             for (int li = 0; li < sc.n_lights; ++li) {
                                 const DevLight Lt = ldconst(sc.lights, li);
                                 float u0, u1;
                                 sm.get2d(smp, u0, u1);
                                 V3 wi;
-                                float tmax, wgt, sc_le;
+                                float tmax, wgt;
                                 bool ok;
-                                int lmat = Lt.material;
                                 if (Lt.type <= 1) {
                                     V3 pl;
                                     if (Lt.type == 0) {
@@ -1638,7 +1640,6 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                     float G = (cs * cl) / dist2;
                                     wgt = G * Lt.area;
                                     if (sc.mis) wgt = wgt * power_heuristic(dist2 / (cl * Lt.area), cs * InvPi);
-                                    sc_le = sc.materials[lmat].emit;
                                 } else {
                                     float fall;
                                     if (Lt.type == 2) {
@@ -1656,20 +1657,18 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                     float cs = vdot(nrm, wi);
                                     ok = cs > 0;
                                     wgt = cs * fall;
-                                    sc_le = Lt.scale;
                                 }
-                                if (ok) {
-                                    ++nsh;
-                                    if (!scene_occluded<QCAP>(sc, po, wi, tmax, snn, snt, sfb)) {
-#pragma unroll
-                                        for (int i = 0; i < 8; ++i) {
-                                            float Le = sc_le * dense_query(sp->D65, lam[i]);
-                                            L[i] += ((beta[i] * (R[i] * InvPi)) * Le) * wgt;
-                                        }
-                                    }
-                                }
+                                nr[N_RAY + li] = make_float4(wi.x, wi.y, wi.z, ok ? tmax : -1.0f);
+                                nwgt[li] = wgt;
+                                wantNee = wantNee || ok;
                             }
-                            rstore8(io.rec, slot, R_L, L);
+                            if (wantNee) {
+                                float x[8];
+#pragma unroll
+                                for (int i = 0; i < 8; ++i) x[i] = beta[i] * (R[i] * InvPi);
+                                nr[nee_f4 - 2] = make_float4(x[0], x[1], x[2], x[3]);
+                                nr[nee_f4 - 1] = make_float4(x[4], x[5], x[6], x[7]);
+                            }
                             // cosine-hemisphere bounce (Sampling.h:449-454), pbrt CoordinateSystem frame
                             float u0, u1;
                             sm.get2d(smp, u0, u1);
@@ -1690,8 +1689,59 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                 }
             }
         }
+        const int pe = queue_append<WAVE>(nee.len + qj * kQStride, wantNee, lds) + qj * io.q.S;
+        if (wantNee) nee.slot[pe] = slot;
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
+    }
+}
+
+// Deferred NEE (NeeIO): per queued Lambert vertex, the shadow rays of its lights in light order (any hit, fixed
+// tMax, then the analytic shapes: scene_occluded), then L += ((x (Le D65(λ))) wgt) for the visible lights in the
+// same order — the inline loop's arithmetic term for term.  Only the shadow rays and L are live here.
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_nee(DevScene sc, const DevSpectra* sp, PathIO io,
+                                                                       NeeIO nee, unsigned long long* ctr) {
+    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
+    const int nl = sc.n_lights, nf4 = nee_stride(nl);
+    const QueueView q{nee.len, io.q.S, 0, io.q.ns};
+    std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<QCAP != 1>> items(nee.ticket, q);
+    int qj, qidx;
+    bool live;
+    while (items.next(qj, qidx, live)) {
+        if (!live) continue;  // (no block-level synchronisation in this kernel)
+        const int slot = nee.slot[qj * q.S + qidx];
+        const float4* r = nee.rec + (size_t)slot * nf4;
+        const float4 p4 = r[N_PO];
+        const V3 po = v3(p4.x, p4.y, p4.z);
+        uint64_t vis = 0;
+        for (int li = 0; li < nl; ++li) {
+            const float4 ray = r[N_RAY + li];
+            if (ray.w < 0) continue;  // light not sampled (cos <= 0)
+            ++nsh;
+            if (!scene_occluded<QCAP>(sc, po, v3(ray.x, ray.y, ray.z), ray.w, snn, snt, sfb)) vis |= 1ull << li;
+        }
+        if (vis) {
+            float lam[8], L[8];
+            rload8(io.rec, slot, R_LAM, lam);
+            rload8(io.rec, slot, R_L, L);
+            const float4 xa = r[nf4 - 2], xb = r[nf4 - 1];
+            const float x[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+            const float* wg = reinterpret_cast<const float*>(r + N_RAY + nl);
+            for (int li = 0; li < nl; ++li) {
+                if (!((vis >> li) & 1)) continue;
+                const DevLight Lt = ldconst(sc.lights, li);
+                const float sc_le = Lt.type <= 1 ? sc.materials[Lt.material].emit : Lt.scale;
+                const float wgt = wg[li];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    float Le = sc_le * dense_query(sp->D65, lam[i]);
+                    L[i] += ((x[i] * Le)) * wgt;
+                }
+            }
+            rstore8(io.rec, slot, R_L, L);
+        }
     }
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
@@ -1876,15 +1926,16 @@ hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, cons
 
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
-                             unsigned long long* ctr, const ShadowQueueIO& shq) {
+                             unsigned long long* ctr, const ShadowQueueIO& shq, const NeeIO& nee) {
     int gb = grid > 0 ? grid : 1;
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
+    if (sc.full && sc.n_lights > 0 && !nee.rec) return hipErrorInvalidValue;  // NEE records are required
 #define RT_SHADE_CASE(Q)                                                                                         \
     case Q:                                                                                                      \
         if (sc.full)                                                                                             \
             hipLaunchKernelGGL(k_path_shade_full<Q>, dim3(resident_grid(k_path_shade_full<Q>, gb, grid)), b, 0, st, \
-                               sc, sp, smp, film, ids, io, ctr);                                                 \
+                               sc, sp, smp, film, ids, io, nee);                                                 \
         else                                                                                                     \
             hipLaunchKernelGGL(k_path_shade<Q>, dim3(resident_grid(k_path_shade<Q>, gb, grid)), b, 0, st, sc, sp,  \
                                smp, film, ids, io, ctr, shq);                                                    \
@@ -1896,6 +1947,20 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
         default: return hipErrorInvalidValue;
     }
 #undef RT_SHADE_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_path_nee(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
+                           const PathIO& io, const NeeIO& nee, unsigned long long* ctr) {
+    int gb = grid > 0 ? grid : 1;
+    if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
+    dim3 b(kBlock);
+    switch (qcap) {
+        case 0: hipLaunchKernelGGL(k_path_nee<0>, dim3(resident_grid(k_path_nee<0>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        case 1: hipLaunchKernelGGL(k_path_nee<1>, dim3(resident_grid(k_path_nee<1>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        case 16: hipLaunchKernelGGL(k_path_nee<16>, dim3(resident_grid(k_path_nee<16>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
