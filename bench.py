@@ -49,7 +49,7 @@ def parse():
     return p.parse_args()
 
 
-def kernel_rooflines(st, counters):
+def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
     """Per-kernel HBM and VALU rooflines from HIP-event launch times (the single-lane pass: one launch at a time).
 
     Algorithmic bytes follow SURVEY.md §8(d): the per-ray HBM streams are `achieved` (k_trace_closest: 40 B per
@@ -64,12 +64,17 @@ def kernel_rooflines(st, counters):
         "k_path_shade": (st["ms_shade"], st["launches_shade"], 312 * st["rays"] + 32 * st["shadow_rays"],
                          32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"]),
     }
+    if st["ms_shadow"] > 0:  # shadow rays in a kernel of their own, one launch per shade launch: the §8(d) 32 B per
+        # shadow ray and the shadow scene terms move to it (k_path_nee: mixed scenes; k_path_shadow: shadow queue)
+        ks[shadow_kernel] = (st["ms_shadow"], st["launches_shade"], 32 * st["shadow_rays"],
+                             32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"])
+        ks["k_path_shade"] = (st["ms_shade"], st["launches_shade"], 312 * st["rays"], 0)
     res = {}
     for name, (ms, launches, stream_b, scene_b) in ks.items():
         launches = max(1, launches)
         avg_s = ms / launches * 1e-3
         a = stream_b / launches / avg_s / 1e9
-        kc = (counters or {}).get(name, {})
+        kc = (counters or {}).get(name) or (counters or {}).get(name + "_full", {})  # mixed scenes: k_path_shade_full
         res[name] = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(a / HBM_PEAK_GBS, 4),
                      "traffic": kc.get("dram_bytes_per_launch"),
@@ -257,7 +262,7 @@ def main():
     roofline = {}
     if rank == 0:
         st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
-        rl = kernel_rooflines(st1, counters)
+        rl = kernel_rooflines(st1, counters, "k_path_nee" if a.config in ("cfg4", "cfg5") else "k_path_shadow")
         dom = max(rl, key=lambda k: rl[k]["total_ms"])
         roofline = dict(rl[dom])
         roofline["basis"] = (f"single-lane pass (RTMI_LANES=1, {a.steps} steps, {dt1 / a.steps * 1e3:.3f} ms/step): "

@@ -17,8 +17,8 @@ import glob
 import json
 from pathlib import Path
 
-KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_generate", "k_path_film", "k_ref_shade_film",
-           "k_sort_gather")
+KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_nee", "k_path_shadow", "k_generate",
+           "k_path_film", "k_ref_shade_film", "k_sort_keys", "k_sort_gather")
 
 
 def kname(raw):
