@@ -137,6 +137,17 @@ RT_DEV int permutation_element(uint32_t i, uint32_t l, uint32_t p) {
     return (int)((i + p) % l);
 }
 
+// PermutationElement for a power-of-two l: the cycle-walking loop runs once (w = l - 1 masks every value below l,
+// and i ^ (i >> 5) stays below it) and (i + p) % l is (i + p) & (l - 1) on the wrapped 32-bit sum
+RT_DEV int permutation_element_p2(uint32_t i, uint32_t l, uint32_t p) {
+    const uint32_t w = l - 1;
+    i ^= p; i *= 0xe170893du; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8; i *= 0x0929eb3fu;
+    i ^= p >> 23; i ^= (i & w) >> 1; i *= 1u | p >> 27; i *= 0x6935fa69u; i ^= (i & w) >> 11;
+    i *= 0x74dcb303u; i ^= (i & w) >> 2; i *= 0x9e501cc3u; i ^= (i & w) >> 2; i *= 0xc860a3dfu;
+    i &= w; i ^= i >> 5;
+    return (int)((i + p) & w);
+}
+
 struct Pcg {  // rng.h:24-144
     uint64_t state, inc;
     RT_DEV uint32_t next() {
@@ -158,17 +169,39 @@ struct Pcg {  // rng.h:24-144
         state += seed;
         next();
     }
-    RT_DEV void advance(uint64_t delta) {  // rng.h:131-144
-        uint64_t curMult = 0x5851f42d4c957f2dull, curPlus = inc, accMult = 1u, accPlus = 0u;
-        while (delta > 0) {
-            if (delta & 1) { accMult *= curMult; accPlus = accPlus * curMult + curPlus; }
-            curPlus = (curMult + 1) * curPlus;
-            curMult *= curMult;
-            delta /= 2;
-        }
-        state = accMult * state + accPlus;
-    }
+    // rng.h:131-144.  The square-and-multiply's curMult after i halvings is M^(2^i) and its curPlus is inc times
+    // prod_{k<i} (M^(2^k) + 1), both mod 2^64: they come from a constant table (kPcgJump), so only the set bits of
+    // delta cost multiplications — the same ring values, hence the same state.
+    RT_DEV void advance(uint64_t delta);
 };
+
+struct PcgJumpTable {
+    uint64_t mult[64], plus[64];
+};
+constexpr PcgJumpTable make_pcg_jump() {
+    PcgJumpTable t{};
+    uint64_t m = 0x5851f42d4c957f2dull, p = 1;
+    for (int i = 0; i < 64; ++i) {
+        t.mult[i] = m;
+        t.plus[i] = p;
+        p = (m + 1) * p;
+        m *= m;
+    }
+    return t;
+}
+__constant__ constexpr PcgJumpTable kPcgJump = make_pcg_jump();
+
+RT_DEV void Pcg::advance(uint64_t delta) {
+    uint64_t accMult = 1u, accPlus = 0u;
+    for (int i = 0; delta > 0; ++i, delta >>= 1) {
+        if (delta & 1) {
+            const uint64_t cm = kPcgJump.mult[i];
+            accMult *= cm;
+            accPlus = accPlus * cm + inc * kPcgJump.plus[i];
+        }
+    }
+    state = accMult * state + accPlus;
+}
 
 // ------------------------------------------------------------------------------------- Sobol
 // hash.h:96-104 Hash(int, int): an 8-byte key, one block, no tail
@@ -253,10 +286,11 @@ struct Smp {
             return sobol_dim(S, dim++);
         }
         uint64_t h = hash_pixel_dim(px, py, dim, S.seed);
-        int stratum = permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
+        int stratum = S.p2 ? permutation_element_p2((uint32_t)index, (uint32_t)S.spp, (uint32_t)h)
+                           : permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
         ++dim;
         float delta = S.jitter ? rng.uniform() : 0.5f;
-        return ((float)stratum + delta) / (float)S.spp;
+        return S.p2 ? ((float)stratum + delta) * S.inv_spp : ((float)stratum + delta) / (float)S.spp;
     }
     RT_DEV void get2d(const DevSampler& S, float& u0, float& u1) {  // samplers.h:107-123
         if (S.kind == 0) { u0 = rng.uniform(); u1 = rng.uniform(); return; }
@@ -269,8 +303,17 @@ struct Smp {
         }
         if (index >= S.spp) { u0 = 0; u1 = 0; return; }
         uint64_t h = hash_pixel_dim(px, py, dim, S.seed);
-        int stratum = permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
         dim += 2;
+        if (S.p2) {  // power-of-two strata: the same values without integer or float divisions
+            int stratum = permutation_element_p2((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
+            int x = stratum & (S.xs - 1), y = stratum >> S.lg_xs;
+            float dx = S.jitter ? rng.uniform() : 0.5f;
+            float dy = S.jitter ? rng.uniform() : 0.5f;
+            u0 = ((float)x + dx) * S.inv_xs;
+            u1 = ((float)y + dy) * S.inv_ys;
+            return;
+        }
+        int stratum = permutation_element((uint32_t)index, (uint32_t)S.spp, (uint32_t)h);
         int x = stratum % S.xs, y = stratum / S.xs;
         float dx = S.jitter ? rng.uniform() : 0.5f;
         float dy = S.jitter ? rng.uniform() : 0.5f;

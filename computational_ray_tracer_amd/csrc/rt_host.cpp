@@ -506,6 +506,7 @@ struct rt_ctx {
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     float* d_cdf = nullptr;    // Gaussian / Lanczos filter tables: x then y, cdf_n + 1 floats each
     int cdf_n = 0;
+    int film_y_int = 0;  // the film's raster y (float division + floor) equals the integer division for every pixel
     uint32_t* d_sobol_mats = nullptr;  // Sobol generator columns; d_sobol_fwd: fwd then inv tables for sobol_m
     uint64_t* d_sobol_fwd = nullptr;
     int sobol_m = 0;
@@ -905,7 +906,22 @@ DevSampler dev_sampler(const rt_ctx* c) {
     s.sobol_mats = c->d_sobol_mats;
     s.sobol_fwd = c->d_sobol_fwd;
     s.sobol_inv = c->d_sobol_fwd ? c->d_sobol_fwd + kSobolMatrixSize : nullptr;
+    auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+    if (s.kind == RT_SAMPLER_STRATIFIED && pow2(s.xs) && pow2(s.ys)) {
+        s.p2 = 1;
+        while ((1 << s.lg_xs) < s.xs) ++s.lg_xs;
+        s.inv_xs = 1.0f / (float)s.xs;   // exact: powers of two
+        s.inv_ys = 1.0f / (float)s.ys;
+        s.inv_spp = 1.0f / (float)s.spp;
+    }
     return s;
+}
+
+// sample ids of a batch starting at sample index b0 (s = i n_pixels + j)
+SampleIds sample_ids(const rt_ctx* c, int b0) {
+    SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
+    ids.np_div = make_intdiv((uint32_t)c->n_work);
+    return ids;
 }
 
 // Sobol tables on the device for the current film (scale = RoundUpPow2(max(res)), samplers.h:243)
@@ -938,6 +954,8 @@ DevFilm dev_film(const rt_ctx* c) {
     f.cdf_x = c->d_cdf;
     f.cdf_y = c->d_cdf ? c->d_cdf + (c->cdf_n + 1) : nullptr;
     f.cdf_n = c->cdf_n;
+    f.rx_div = make_intdiv((uint32_t)d.res_x);
+    f.y_int = c->film_y_int;
     return f;
 }
 
@@ -1009,7 +1027,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
         for (int b0 = ib; b0 < ie; b0 += B) {
             int nIdx = std::min(B, ie - b0);
             int nS = nIdx * c->n_work;
-            SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
+            SampleIds ids = sample_ids(c, b0);
             GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, RecView{nullptr, 0, 0}, 0};
             hipEvent_t e0 = ev_start(c, st);
             HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
@@ -1084,7 +1102,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             int nS = nIdx[l] * c->n_work;
             nSq[l] = nS;
             Sq[l] = shard_stride(nS, nsh);  // every queue of this batch: shard j at [j S, j S + len_j)
-            SampleIds ids{c->d_work, c->n_work, b0, nullptr, nullptr};
+            SampleIds ids = sample_ids(c, b0);
             GenOut go{w.rayO, w.rayD, w.slot, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0};
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
@@ -1100,7 +1118,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 Work& w = c->ws[l];
                 hipStream_t s = lstream(l);
                 const RecView rv{w.rec, rec_fs, rec_ss, rec_rng8};
-                SampleIds ids{c->d_work, c->n_work, g0 + l * B, nullptr, nullptr};
+                SampleIds ids = sample_ids(c, g0 + l * B);
                 int nxt = cur[l] ^ 1;
                 const float4* cO = w.rayO + (size_t)cur[l] * qs;
                 const float4* cD = w.rayD + (size_t)cur[l] * qs;
@@ -1938,6 +1956,12 @@ static int film_set_one(rt_ctx* c, const rt_film_desc* d) {
         return fail(c, RT_E_ARG, "unknown sensor or sensor illuminant");
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);  // queued passes may still read the old tables
+    {  // RayTracerTestApp.h:289-291 divides in float; the kernels may divide integers where that is identical
+        const int w = d->res_x, n = d->res_x * d->res_y;
+        int ok = 1;
+        for (int p = 0; p < n && ok; ++p) ok = (int)std::floor((float)p / (float)w) == p / w;
+        c->film_y_int = ok;
+    }
     int rc = setup_sensor(c, *d);
     if (rc) return rc;
     if (c->d_cdf) { hipFree(c->d_cdf); c->d_cdf = nullptr; c->cdf_n = 0; }

@@ -39,6 +39,10 @@ struct DevCamera {
 
 struct DevSampler {
     int kind, xs, ys, jitter, seed, spp;
+    // stratified with power-of-two xs and ys: the stratum split, PermutationElement's final modulo and the divisions
+    // by xs / ys / spp become masks, shifts and multiplications by the exact reciprocals (same values)
+    int p2, lg_xs;
+    float inv_xs, inv_ys, inv_spp;
     int randomize, sobol_m, scale;  // SobolSampler (samplers.h:229-327)
     const uint32_t* sobol_mats;     // kSobolDims x kSobolMatrixSize generator columns
     const uint64_t* sobol_fwd;      // SobolIntervalToIndex tables for sobol_m (kSobolMatrixSize each)
@@ -46,8 +50,27 @@ struct DevSampler {
 };
 static const int kSobolDims = 32, kSobolMatrixSize = 52;
 
+// Division by an invariant divisor d for dividends 0 <= n < 2^31 (Granlund & Montgomery, Thm 4.2 with N = 31):
+// l = ceil(log2 d), m = ceil(2^(31 + l) / d), n / d = (n m) >> (31 + l) exactly (n m < 2^63).  m == 0: unset.
+struct IntDiv {
+    uint64_t m = 0;
+    int l = 0;
+};
+inline IntDiv make_intdiv(uint32_t d) {
+    IntDiv r;
+    if (d == 0) return r;
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    r.l = l;
+    r.m = ((1ull << (31 + l)) + d - 1) / d;
+    return r;
+}
+__device__ __forceinline__ int intdiv(int n, const IntDiv& D) { return (int)(((uint64_t)(uint32_t)n * D.m) >> (31 + D.l)); }
+
 struct DevFilm {
     int res_x, res_y, filter;
+    IntDiv rx_div;  // pixel / res_x
+    int y_int;      // 1: floorf((float)p / (float)res_x) == p / res_x for every pixel of the film (checked at film set)
     float rx, ry, imaging_ratio;
     const float* cdf_x;             // Gaussian / Lanczos: Continuous_Inversion_Sampler tables (N + 1 floats each)
     const float* cdf_y;
@@ -145,6 +168,7 @@ struct SampleIds {
     int index_begin;
     const int* ex_pixel;     // explicit (pixel, index) pairs (parity entry point) or nullptr
     const int* ex_index;
+    IntDiv np_div;           // s / n_pixels (unset: plain division)
 };
 
 // Path state of a slot (path mode): 8 float4 fields — λ[8] at R_LAM.., β[8] at R_BETA.., L[8] at R_L.., the PCG

@@ -247,13 +247,19 @@ __device__ __forceinline__ void count_add(unsigned long long* ctr, int slot, uns
 
 __device__ __forceinline__ void sample_of(const SampleIds& ids, int s, int& pixel, int& index) {
     if (ids.ex_pixel) { pixel = ids.ex_pixel[s]; index = ids.ex_index[s]; return; }
-    int i = s / ids.n_pixels;
+    int i = ids.np_div.m ? intdiv(s, ids.np_div) : s / ids.n_pixels;
     int j = s - i * ids.n_pixels;
     pixel = ids.work_pixels[j];
     index = ids.index_begin + i;
 }
 // RayTracerTestApp.h:289-291 (raster y in [1, resY], a kept quirk)
 __device__ __forceinline__ void pixel_xy(const DevFilm& film, int pixel, int& x, int& y) {
+    if (film.rx_div.m) {
+        const int q = intdiv(pixel, film.rx_div);
+        x = pixel - q * film.res_x;
+        y = film.y_int ? film.res_y - q : (int)((float)film.res_y - floorf((float)pixel / (float)film.res_x));
+        return;
+    }
     x = pixel % film.res_x;
     y = (int)((float)film.res_y - floorf((float)pixel / (float)film.res_x));
 }
