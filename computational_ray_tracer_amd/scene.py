@@ -555,7 +555,8 @@ def cornell_box(blocks=True, extra=None):
     faces[flip | lflip] = faces[flip | lflip][:, [0, 2, 1]]
     # blocks: outward
     blk = (np.arange(len(faces)) >= 12) & (np.arange(len(faces)) < n_fixed)
-    bc = np.where(np.arange(len(faces))[:, None] < 24, faces[12:24].reshape(-1, 3).mean(0), faces[24:].reshape(-1, 3).mean(0))
+    cmean = lambda f: f.reshape(-1, 3).mean(0) if len(f) else np.zeros(3)  # (no blocks: unused)
+    bc = np.where(np.arange(len(faces))[:, None] < 24, cmean(faces[12:24]), cmean(faces[24:]))
     nn = np.cross(faces[:, 1] - faces[:, 0], faces[:, 2] - faces[:, 0])
     bflip = blk & (np.einsum("ij,ij->i", nn, cen - bc) < 0)
     faces[bflip] = faces[bflip][:, [0, 2, 1]]

@@ -623,3 +623,33 @@ def test_bvh_fast_path_counters(cfg3_pair):
     assert st["tris_tested"] / st["rays"] < 12, st
     assert st["fallback_rays"] <= 1e-3 * st["rays"], st
     assert st["shadow_fallback_rays"] <= 1e-2 * st["shadow_rays"], st
+
+
+@pytest.mark.parametrize("nl,single_leaf", [(1, False), (2, True), (6, False), (6, True)])
+def test_deferred_nee_light_counts_bitexact(oracle_lib, nl, single_leaf):
+    """Deferred NEE (k_path_shade_full -> k_path_nee) with 1, 2 and 6 lights: NEE records of nee_stride(n) float4
+    (the light weights spill into a second float4 at 6 lights), light order kept per vertex; MIS on; a 3 x 3
+    stratified sampler (the non-power-of-two sampler path) on an odd film; single-leaf (Cornell box + spheres,
+    one shard, static chunks) and multi-level (the CFG4 mesh, 8 shards, tickets) scenes."""
+    import copy
+    from computational_ray_tracer_amd import capi
+    res = (37, 23)
+    base = scene.cfg4_mixed(res=res, spp=(3, 3), frequency=16)
+    m = copy.deepcopy(base.model)
+    if single_leaf:  # the box without the mesh: 12 triangles, one leaf; the shapes make it a mixed scene
+        cb = scene.cornell_box(blocks=False)
+        m.positions, m.normals, m.indices = cb.positions, cb.normals, cb.indices
+        m.tri_material = cb.tri_material
+    extra = [dict(type=capi.RT_LIGHT_POINT, p=(100.0 + 60 * k, 380.0, 200.0 + 40 * k), scale=1.0e4 * (k + 1))
+             for k in range(4)]
+    lights = list(m.lights) + extra
+    m.lights = lights[:nl]
+    cfg = scene.Config(f"nee{nl}", m, base.camera, scene.StratifiedSampler(3, 3, True, 0), base.film,
+                       scene.Integrator(capi.RT_INTEGRATOR_PATH_MIS, max_depth=4), 0, 9)
+    r = Renderer(cfg)
+    assert (r.octree()["depth"] == 0) == single_leaf
+    fg = r.render_pass(0, 3)
+    fo = oracle_lib.OracleScene(cfg).render(0, 3)
+    bad = np.any(bits(fg) != bits(fo), axis=1)
+    assert bad.sum() == 0, f"{bad.sum()} pixels differ; max |diff| {np.abs(fg - fo).max()}"
+    assert r.stats()["shadow_rays"] > 0
