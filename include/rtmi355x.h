@@ -205,15 +205,16 @@ typedef struct {
     int64_t shadow_nodes_tested;     /* node box tests by any-hit (shadow) rays          */
     int64_t shadow_tris_tested;      /* triangle tests by any-hit (shadow) rays          */
     int64_t hits;                    /* closest-hit rays that hit                        */
-    double ms_generate, ms_trace, ms_shade, ms_shadow, ms_film;  /* HIP-event kernel time; ms_shadow is
-                                        the shadow-queue kernel (RTMI_SHADOW_QUEUE=1), else 0: shadow rays
-                                        are traced inside the path shade kernel */
+    double ms_generate, ms_trace, ms_shade, ms_shadow, ms_film;  /* HIP-event kernel time (0 with
+                                        RTMI_NO_STAGE_EVENTS); ms_shadow is the deferred NEE kernel of mixed
+                                        scenes or the shadow-queue kernel (RTMI_SHADOW_QUEUE=1), else 0: the
+                                        simple path traces its shadow rays inside the shade kernel */
     int64_t launches_trace;          /* closest-hit trace launches (per-launch averages) */
     int64_t launches_shade;          /* shade launches (path mode: includes the inline shadow rays) */
     int64_t fallback_rays;           /* multi-level octrees: closest-hit rays the fast BVH traversal found
                                         ambiguous (canonical rule), traced by the reference BFS */
     int64_t shadow_fallback_rays;    /* the same for any-hit (shadow) rays                */
-    double ms_sort;                  /* multi-level octrees: coherence binning of bounce rays (HIP events) */
+    double ms_sort;                  /* multi-level octrees: coherence sort of bounce rays (HIP events)  */
 } rt_stats;   /* multi-device contexts: every field summed over the devices */
 
 /* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */
