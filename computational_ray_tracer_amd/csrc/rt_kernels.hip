@@ -50,6 +50,22 @@ __device__ __forceinline__ void stage_leaf1(const DevScene& sc, int set) {
     __syncthreads();
 }
 #define RT_LEAF1(tiles, base, j) (g_leaf1 + 3 * (j))
+// the simple path's per-triangle shading inputs on single-leaf scenes (<= 64 triangles): world vertices and the
+// material's (c0, c1, c2, emission), staged in LDS by k_path_shade<1>
+__shared__ float4 g_tri1[4 * 64];
+__device__ __forceinline__ bool stage_tris1(const DevScene& sc) {
+    const bool ok = sc.n_tris <= 64;
+    if (ok)
+        for (int i = threadIdx.x; i < sc.n_tris; i += blockDim.x) {
+            g_tri1[4 * i] = sc.triWorld[3 * i];
+            g_tri1[4 * i + 1] = sc.triWorld[3 * i + 1];
+            g_tri1[4 * i + 2] = sc.triWorld[3 * i + 2];
+            const DevMaterial dm = sc.materials[sc.triMaterial[i]];
+            g_tri1[4 * i + 3] = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
+        }
+    __syncthreads();
+    return ok;
+}
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -1260,7 +1276,11 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                                                                          DevFilm film, SampleIds ids, PathIO io,
                                                                          unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
-    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
+    bool lds_tris = false;
+    if constexpr (QCAP == 1) {
+        stage_leaf1(sc, 0);
+        lds_tris = stage_tris1(sc);
+    }
     __shared__ int lds[kBlock / 64 + 1];
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
@@ -1291,13 +1311,18 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                 } else {
                     rload8(io.rec, slot, R_BETA, beta);
                 }
-                float4 P0 = sc.triWorld[3 * prim], P1 = sc.triWorld[3 * prim + 1], P2 = sc.triWorld[3 * prim + 2];
+                float4 P0, P1, P2, mt;
+                if (QCAP == 1 && lds_tris) {
+                    P0 = g_tri1[4 * prim]; P1 = g_tri1[4 * prim + 1]; P2 = g_tri1[4 * prim + 2]; mt = g_tri1[4 * prim + 3];
+                } else {
+                    P0 = sc.triWorld[3 * prim]; P1 = sc.triWorld[3 * prim + 1]; P2 = sc.triWorld[3 * prim + 2];
+                    const DevMaterial dm = sc.materials[sc.triMaterial[prim]];
+                    mt = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
+                }
                 V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
                 V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
                 const float4 d4 = io.rayD[k];
                 V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
-                DevMaterial dm = sc.materials[sc.triMaterial[prim]];
-                float4 mt = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
                 if (mt.w > 0) {
                     if (io.depth == 0 && vdot(ng, rayd) < 0) {
                         float L[8];
