@@ -156,46 +156,93 @@ struct Collapse {
         out.max_leaf = std::max(out.max_leaf, lf.count);
         return (int)(0x80000000u | ((unsigned)first << 4) | (unsigned)(lf.count - 1));
     }
-    // emits the 4-wide node for binary node `n2`, returns its index
-    int emit(int n2, int depth) {
-        depth_max = std::max(depth_max, depth);
-        const int me = (int)(out.nodes.size() / 8);
-        out.nodes.resize(out.nodes.size() + 8);
+    // the up-to-4 binary nodes that become the children of the 4-wide node for binary node n2 (opening the
+    // largest-area internal child until there are 4)
+    std::vector<int> children4(int n2) const {
         std::vector<int> ch;
         if (B.nodes[n2].left < 0) {
             ch.push_back(n2);  // a leaf root
-        } else {
-            ch = {B.nodes[n2].left, B.nodes[n2].right};
-            while (ch.size() < 4) {
-                int pick = -1;
-                double pa = -1;
-                for (size_t k = 0; k < ch.size(); ++k)
-                    if (B.nodes[ch[k]].left >= 0 && B.nodes[ch[k]].box.area() > pa) { pa = B.nodes[ch[k]].box.area(); pick = (int)k; }
-                if (pick < 0) break;
-                const int o = ch[pick];
-                ch[pick] = B.nodes[o].left;
-                ch.push_back(B.nodes[o].right);
-            }
+            return ch;
         }
+        ch = {B.nodes[n2].left, B.nodes[n2].right};
+        while (ch.size() < 4) {
+            int pick = -1;
+            double pa = -1;
+            for (size_t k = 0; k < ch.size(); ++k)
+                if (B.nodes[ch[k]].left >= 0 && B.nodes[ch[k]].box.area() > pa) { pa = B.nodes[ch[k]].box.area(); pick = (int)k; }
+            if (pick < 0) break;
+            const int o = ch[pick];
+            ch[pick] = B.nodes[o].left;
+            ch.push_back(B.nodes[o].right);
+        }
+        return ch;
+    }
+    int reserve() {
+        const int me = (int)(out.nodes.size() / 8);
+        out.nodes.resize(out.nodes.size() + 8);
+        return me;
+    }
+    void write_node(int me, const std::vector<int>& ch, const int* word) {
         float lo[3][4], hi[3][4];
-        int word[4];
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 4; ++k)
             for (int a = 0; a < 3; ++a) { lo[a][k] = 0.f; hi[a][k] = 0.f; }
-            word[k] = -1;
-        }
+        int w[4] = {-1, -1, -1, -1};
         for (size_t k = 0; k < ch.size(); ++k) {
             const Node2& c = B.nodes[ch[k]];
             for (int a = 0; a < 3; ++a) { lo[a][k] = c.box.lo[a] - pad; hi[a][k] = c.box.hi[a] + pad; }
-            word[k] = c.left < 0 ? leaf_word(c) : emit(ch[k], depth + 1);
+            w[k] = word[k];
         }
         float4* nd = &out.nodes[8 * (size_t)me];
         for (int a = 0; a < 3; ++a) {
             nd[2 * a] = make_float4(lo[a][0], lo[a][1], lo[a][2], lo[a][3]);
             nd[2 * a + 1] = make_float4(hi[a][0], hi[a][1], hi[a][2], hi[a][3]);
         }
-        std::memcpy(&nd[6], word, 16);  // the child words' bits, never through float registers
+        std::memcpy(&nd[6], w, 16);  // the child words' bits, never through float registers
         nd[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // depth-first: the 4-wide node for binary node n2 and its subtree, appended; returns its index
+    int emit(int n2, int depth) {
+        depth_max = std::max(depth_max, depth);
+        const int me = reserve();
+        const std::vector<int> ch = children4(n2);
+        int word[4] = {-1, -1, -1, -1};
+        for (size_t k = 0; k < ch.size(); ++k)
+            word[k] = B.nodes[ch[k]].left < 0 ? leaf_word(B.nodes[ch[k]]) : emit(ch[k], depth + 1);
+        write_node(me, ch, word);
         return me;
+    }
+    // the top kBvhTopLevels levels breadth-first (nodes 0 .. kBvhTopNodes - 1 at most, which the kernels stage in
+    // LDS), every deeper subtree depth-first after them
+    void emit_root(int root) {
+        std::vector<std::pair<int, int>> level = {{root, reserve()}};
+        for (int depth = 0; depth < kBvhTopLevels && !level.empty(); ++depth) {
+            depth_max = std::max(depth_max, depth);
+            std::vector<std::pair<int, int>> next;
+            std::vector<std::pair<int, std::vector<int>>> pend;  // (node index, children) of this level
+            for (const auto& [n2, me] : level) {
+                std::vector<int> ch = children4(n2);
+                pend.emplace_back(me, ch);
+            }
+            // indices of the next level first (contiguous), then leaves / deeper subtrees
+            std::vector<std::vector<int>> words(pend.size(), std::vector<int>(4, -1));
+            for (size_t i = 0; i < pend.size(); ++i)
+                for (size_t k = 0; k < pend[i].second.size(); ++k) {
+                    const int c = pend[i].second[k];
+                    if (B.nodes[c].left >= 0 && depth + 1 < kBvhTopLevels) {
+                        words[i][k] = reserve();
+                        next.emplace_back(c, words[i][k]);
+                    }
+                }
+            for (size_t i = 0; i < pend.size(); ++i) {
+                for (size_t k = 0; k < pend[i].second.size(); ++k) {
+                    const int c = pend[i].second[k];
+                    if (B.nodes[c].left < 0) words[i][k] = leaf_word(B.nodes[c]);
+                    else if (depth + 1 >= kBvhTopLevels) words[i][k] = emit(c, depth + 1);
+                }
+                write_node(pend[i].first, pend[i].second, words[i].data());
+            }
+            level = std::move(next);
+        }
     }
 };
 
@@ -232,7 +279,7 @@ void build_bvh4(const float* tri9, const int* ids, int n, float pad, float node_
     Collapse C{B, tri9, ids, pad, out};
     out.nodes.reserve(8 * (size_t)(n / 2 + 1));
     out.tiles.reserve(3 * (size_t)n);
-    C.emit(0, 0);
+    C.emit_root(0);
     out.depth = C.depth_max;
 }
 

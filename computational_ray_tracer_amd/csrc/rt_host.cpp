@@ -1889,17 +1889,22 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         return rc;
     void* pbv[2] = {nullptr, nullptr};
     void* pbt[2] = {nullptr, nullptr};
-    for (int st = 0; st < 2; ++st)
-        if (!bvh[st].nodes.empty() && ((rc = up(bvh[st].nodes.data(), bvh[st].nodes.size() * 16, &pbv[st])) ||
-                                        (rc = up(bvh[st].tiles.data(), bvh[st].tiles.size() * 16, &pbt[st]))))
+    const int bvh_nodes0 = (int)(bvh[0].nodes.size() / 8);
+    for (int st = 0; st < 2; ++st) {
+        if (bvh[st].nodes.empty()) continue;
+        // the kernels stage nodes [0, kBvhTopNodes) in LDS unconditionally: pad with empty nodes
+        if (bvh[st].nodes.size() < 8 * (size_t)kBvhTopNodes) bvh[st].nodes.resize(8 * (size_t)kBvhTopNodes, make_float4(0.f, 0.f, 0.f, 0.f));
+        if ((rc = up(bvh[st].nodes.data(), bvh[st].nodes.size() * 16, &pbv[st])) ||
+            (rc = up(bvh[st].tiles.data(), bvh[st].tiles.size() * 16, &pbt[st])))
             return rc;
+    }
     DevScene& d = c->dsc;
     for (int st = 0; st < 2; ++st) {
         d.bvh[st] = (const float4*)(pbv[st] ? pbv[st] : pbv[0]);
         d.btiles[st] = (const float4*)(pbt[st] ? pbt[st] : pbt[0]);
     }
     d.wabs = wabs;
-    c->info.bvh_nodes = (int)(bvh[0].nodes.size() / 8);
+    c->info.bvh_nodes = bvh_nodes0;
     c->info.bvh_depth = bvh[0].depth;
     d.clusters[0] = (const float4*)pc0; d.clusters[1] = (const float4*)pc1;
     if (qcap != 1) d.n_clusters[0] = d.n_clusters[1] = 0;

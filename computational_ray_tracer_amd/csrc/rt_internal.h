@@ -149,6 +149,9 @@ constexpr size_t kCtrWords = (size_t)C_NCOUNTERS * kCtrSubs * kCtrLine;
 __host__ __device__ inline size_t ctr_word(int slot, int sub) { return ((size_t)slot * kCtrSubs + sub) * kCtrLine; }
 
 // host: 4-wide BVH build (rt_bvh.cpp)
+// the top levels of every BVH are laid out breadth-first: nodes [0, kBvhTopNodes) (1 + 4 + 16), staged in LDS by
+// the multi-level traversal kernels
+static const int kBvhTopLevels = 3, kBvhTopNodes = 21;
 struct BvhData {
     std::vector<float4> nodes, tiles;
     int depth = 0, max_leaf = 0;

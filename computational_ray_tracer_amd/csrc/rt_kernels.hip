@@ -50,6 +50,37 @@ __device__ __forceinline__ void stage_leaf1(const DevScene& sc, int set) {
     __syncthreads();
 }
 #define RT_LEAF1(tiles, base, j) (g_leaf1 + 3 * (j))
+// multi-level scenes: the BVH's breadth-first top levels (kBvhTopNodes nodes, 2.6 KB; rt_bvh.cpp emit_root), which
+// every ray opens, staged in LDS at kernel start by every kernel that traverses the BVH
+#ifndef RT_BVH_TOP
+#define RT_BVH_TOP 1
+#endif
+__shared__ float4 g_top[8 * kBvhTopNodes];
+template <int QCAP>
+__device__ __forceinline__ void stage_scene(const DevScene& sc, int set) {
+    if constexpr (QCAP == 1) {
+        stage_leaf1(sc, set);
+    } else if constexpr (RT_BVH_TOP) {
+        // (the host pads every node array to at least kBvhTopNodes nodes)
+        if (sc.bvh[set])
+            for (int i = threadIdx.x; i < 8 * kBvhTopNodes; i += blockDim.x) g_top[i] = sc.bvh[set][i];
+        __syncthreads();
+    }
+}
+struct BvhNode {
+    float4 LX, HX, LY, HY, LZ, HZ, CW;
+};
+__device__ __forceinline__ BvhNode load_node(const float4* __restrict__ nodes, int node) {
+    BvhNode b;
+    if (RT_BVH_TOP && node < kBvhTopNodes) {
+        const float4* N = g_top + 8 * node;
+        b = {N[0], N[1], N[2], N[3], N[4], N[5], N[6]};
+    } else {
+        const float4* N = nodes + 8 * (size_t)node;
+        b = {N[0], N[1], N[2], N[3], N[4], N[5], N[6]};
+    }
+    return b;
+}
 // the simple path's per-triangle shading inputs on single-leaf scenes (<= 64 triangles): world vertices and the
 // material's (c0, c1, c2, emission), staged in LDS by k_path_shade<1>
 __shared__ float4 g_tri1[4 * 64];
@@ -928,8 +959,8 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
                 else decode_leaf(w, lf, lc);
                 continue;
             }
-            const float4* N = nodes + 8 * (size_t)node;
-            const float4 LX = N[0], HX = N[1], LY = N[2], HY = N[3], LZ = N[4], HZ = N[5], CW = N[6];
+            const BvhNode bn = load_node(nodes, node);
+            const float4 LX = bn.LX, HX = bn.HX, LY = bn.LY, HY = bn.HY, LZ = bn.LZ, HZ = bn.HZ, CW = bn.CW;
             nn += 4;
             float e0 = child_entry(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, inv, oi, cut);
             float e1 = child_entry(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, inv, oi, cut);
@@ -1001,8 +1032,8 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
                 else decode_leaf(w, lf, lc);
                 continue;
             }
-            const float4* N = nodes + 8 * (size_t)node;
-            const float4 LX = N[0], HX = N[1], LY = N[2], HY = N[3], LZ = N[4], HZ = N[5], CW = N[6];
+            const BvhNode bn = load_node(nodes, node);
+            const float4 LX = bn.LX, HX = bn.HX, LY = bn.LY, HY = bn.HY, LZ = bn.LZ, HZ = bn.HZ, CW = bn.CW;
             nn += 4;
             const int w[4] = {__float_as_int(CW.x), __float_as_int(CW.y), __float_as_int(CW.z), __float_as_int(CW.w)};
             const bool h[4] = {w[0] != -1 && child_entry(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, inv, oi, tMax) < __builtin_inff(),
@@ -1075,7 +1106,7 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
-    if constexpr (QCAP == 1) stage_leaf1(sc, io.set);
+    stage_scene<QCAP>(sc, io.set);
     ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
     // one ray at queue position p: octree (BVH / BFS), then the analytic shapes with the running tMax (DESIGN.md §5;
     // hitB = object-space point for a shape)
@@ -1277,10 +1308,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                                                                          unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
     bool lds_tris = false;
-    if constexpr (QCAP == 1) {
-        stage_leaf1(sc, 0);
-        lds_tris = stage_tris1(sc);
-    }
+    stage_scene<QCAP>(sc, 0);
+    if constexpr (QCAP == 1) lds_tris = stage_tris1(sc);
     __shared__ int lds[kBlock / 64 + 1];
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
@@ -1440,6 +1469,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
 // between this bounce's shade and the next one's, so every L sees its additions in the same order.
 template <int QCAP, bool DFS>
 __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
+    stage_scene<QCAP>(sc, 0);
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     WaveTickets tk(shq.shTicket, QueueView{shq.shCount, io.q.S, 0, io.q.ns});
     int qj, base;
@@ -1492,7 +1522,7 @@ template <int QCAP>
 __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const float4* o, const float4* d, int* out,
                                                      unsigned long long* ctr) {
     ctr_t nn = 0, nt = 0, ns = 0, nfb = 0;
-    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
+    stage_scene<QCAP>(sc, 0);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         float4 o4 = o[k], d4 = d[k];
         out[k] = scene_occluded<QCAP>(sc, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, nn, nt, nfb) ? 1 : 0;
@@ -1733,7 +1763,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_nee(DevScene sc, const DevSpectra* sp, PathIO io,
                                                                        NeeIO nee, unsigned long long* ctr) {
-    if constexpr (QCAP == 1) stage_leaf1(sc, 0);
+    stage_scene<QCAP>(sc, 0);
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     const int nl = sc.n_lights, nf4 = nee_stride(nl);
     const QueueView q{nee.len, io.q.S, 0, io.q.ns};
