@@ -1454,7 +1454,10 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
             rstore8(io.rec, slot, R_L, z);
         }
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
-        if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
+        if (wantNext) {
+            nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
+            io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot;
+        }
     }
     count_add(ctr, C_SNODES, snn);
     count_add(ctr, C_STRIS, snt);
@@ -1753,7 +1756,10 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
         const int pe = queue_append<WAVE>(nee.len + qj * kQStride, wantNee, lds) + qj * io.q.S;
         if (wantNee) nee.slot[pe] = slot;
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
-        if (wantNext) { io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot; }
+        if (wantNext) {
+            nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
+            io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot;
+        }
     }
 }
 

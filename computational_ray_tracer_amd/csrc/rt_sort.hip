@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const int* _
 __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int* __restrict__ perm, int S, int S2,
                                                                 const float4* __restrict__ o,
                                                                 const float4* __restrict__ d,
-                                                                const int* __restrict__ slot, float4* __restrict__ so,
+                                                                float4* __restrict__ so,
                                                                 float4* __restrict__ sd, int* __restrict__ ss,
                                                                 int* __restrict__ len) {
     if (blockIdx.x == 0 && threadIdx.x < kShards) {
@@ -74,9 +74,10 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int*
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const int j = perm[k];
         const int pos = (k / S2) * S + k % S2;
-        so[pos] = o[j];
+        const float4 oj = o[j];
+        so[pos] = oj;
         sd[pos] = d[j];
-        ss[pos] = slot[j];
+        ss[pos] = __float_as_int(oj.w);  // bounce rays carry their slot in o.w: two scattered reads per ray, not three
     }
 }
 
@@ -101,7 +102,7 @@ hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
                                                       key_bits, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.S, shard_stride(n, kShards),
-                       io.o, io.d, io.slot, io.so, io.sd, io.ss, io.len);
+                       io.o, io.d, io.so, io.sd, io.ss, io.len);
     return hipGetLastError();
 }
 
