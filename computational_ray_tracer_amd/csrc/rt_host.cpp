@@ -600,7 +600,7 @@ int ensure_shadow_workspace(rt_ctx* c, Work& w, size_t n) {
 }
 
 void free_sort_workspace(Work& w) {
-    void* ptrs[] = {w.sO, w.sD, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sTemp};
+    void* ptrs[] = {w.sO, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sTemp};  // (sD = sO + 1)
     for (void* p : ptrs)
         if (p) hipFree(p);
     w.sO = w.sD = nullptr;
@@ -613,7 +613,8 @@ void free_sort_workspace(Work& w) {
 int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
     if (w.sCap >= n) return RT_OK;
     free_sort_workspace(w);
-    HIPCHK(c, dalloc(&w.sO, n)); HIPCHK(c, dalloc(&w.sD, n)); HIPCHK(c, dalloc(&w.sS, n));
+    // the side queue's rays as interleaved (o, d) pairs like the queues' (sD = sO + 1)
+    HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1; HIPCHK(c, dalloc(&w.sS, n));
     HIPCHK(c, dalloc(&w.sVals, n)); HIPCHK(c, dalloc(&w.sValsAlt, n));
     HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n));
     w.sTempBytes = sort_rays_temp_bytes((int)n);
@@ -626,7 +627,7 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
 void free_workspace(Work& w) {
     free_sort_workspace(w);
     free_shadow_workspace(w);
-    void* ptrs[] = {w.rayO, w.rayD, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.rec, w.slot, w.hitPrim};
+    void* ptrs[] = {w.rayO, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.rec, w.slot, w.hitPrim};  // (rayD = rayO + 1)
     for (void* p : ptrs)
         if (p) hipFree(p);
     w.rayO = w.rayD = w.lamA = w.lamB = w.pdfA = w.pdfB = w.hitB = w.rec = nullptr;
@@ -677,7 +678,9 @@ int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
     free_workspace(w);
     // path mode: queue arrays hold 2 ping-pong queues of n entries each
     size_t nq = path ? 2 * n : n;
-    HIPCHK(c, dalloc(&w.rayO, nq)); HIPCHK(c, dalloc(&w.rayD, nq)); HIPCHK(c, dalloc(&w.slot, nq));
+    // rays as interleaved (o, d) pairs, 32 B per ray (rayD = rayO + 1, kernels index [k << rsh] with rsh = 1): a
+    // scattered read of one ray (the coherence sort's gather) touches one line instead of two
+    HIPCHK(c, dalloc(&w.rayO, 2 * nq)); w.rayD = w.rayO + 1; HIPCHK(c, dalloc(&w.slot, nq));
     HIPCHK(c, dalloc(&w.pdfA, n)); HIPCHK(c, dalloc(&w.pdfB, n));
     HIPCHK(c, dalloc(&w.hitB, n)); HIPCHK(c, dalloc(&w.hitPrim, n));
     if (path) {
@@ -961,6 +964,7 @@ DevFilm dev_film(const rt_ctx* c) {
 
 ShadeRefIO shade_ref_io(rt_ctx* c) {
     ShadeRefIO io{};
+    io.rsh = 1;  // the workspace's interleaved rays
     float a = c->integ.albedo_rgb[0];
     io.albedo_c2 = (a - .5f) / std::sqrt(a * (1 - a));  // color.cpp:35-37
     float g = 1.0f / (2.0f * 1.0f);                      // RGBIlluminant(1,1,1): scale = 2*max = 2, rgb/scale = .5
@@ -1028,11 +1032,12 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             int nIdx = std::min(B, ie - b0);
             int nS = nIdx * c->n_work;
             SampleIds ids = sample_ids(c, b0);
-            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, RecView{nullptr, 0, 0}, 0};
+            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, RecView{nullptr, 0, 0}, 0, 1};
             hipEvent_t e0 = ev_start(c, st);
             HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, st, ST_GEN, e0);
-            TraceIO tio{w.rayO, w.rayD, QueueView{nullptr, shard_stride(nS, nsh), nS, nsh}, c->cull ? 1 : 0, w.hitB, w.hitPrim};
+            TraceIO tio{w.rayO, w.rayD, QueueView{nullptr, shard_stride(nS, nsh), nS, nsh}, c->cull ? 1 : 0, w.hitB, w.hitPrim,
+                        nullptr, 1};
             e0 = ev_start(c, st);
             HIPCHK(c, launch_trace_closest(st, 0, c->dsc.qcap, lane_scene(c, w), tio, c->d_ctr));
             ev_mark(c, st, ST_TRACE, e0);
@@ -1103,7 +1108,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             nSq[l] = nS;
             Sq[l] = shard_stride(nS, nsh);  // every queue of this batch: shard j at [j S, j S + len_j)
             SampleIds ids = sample_ids(c, b0);
-            GenOut go{w.rayO, w.rayD, w.slot, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0};
+            GenOut go{w.rayO, w.rayD, w.slot, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0, 1};
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, s, ST_GEN, e0);
@@ -1120,8 +1125,8 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 const RecView rv{w.rec, rec_fs, rec_ss, rec_rng8};
                 SampleIds ids = sample_ids(c, g0 + l * B);
                 int nxt = cur[l] ^ 1;
-                const float4* cO = w.rayO + (size_t)cur[l] * qs;
-                const float4* cD = w.rayD + (size_t)cur[l] * qs;
+                const float4* cO = w.rayO + 2 * (size_t)cur[l] * qs;
+                const float4* cD = cO + 1;
                 const int* cS = w.slot + (size_t)cur[l] * qs;
                 int* qc_cur = w.d_qcount + kQRegion * cur[l];
                 int* qc_nxt = w.d_qcount + kQRegion * nxt;
@@ -1148,7 +1153,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     cO = w.sO; cD = w.sD; cS = w.sS;
                 }
                 const DevScene dsl = lane_scene(c, w);
-                TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr};
+                TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
                 ev_mark(c, s, ST_TRACE, e0);
@@ -1156,7 +1161,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 pio.lean = lean ? 1 : 0;
                 pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.q = qv;
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
-                pio.nO = w.rayO + (size_t)nxt * qs; pio.nD = w.rayD + (size_t)nxt * qs;
+                pio.nO = w.rayO + 2 * (size_t)nxt * qs; pio.nD = pio.nO + 1; pio.rsh = 1;
                 pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt + kQLen;
                 pio.rec = rv; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
@@ -2213,14 +2218,14 @@ static int impl_rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, con
         hipMemcpy(di, indices, 4 * (size_t)n, hipMemcpyHostToDevice);
         SampleIds ids{nullptr, 1, 0, dp, di};
         GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].slot, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA,
-                  c->ws[0].pdfB, RecView{nullptr, 0, 0}, 0};
+                  c->ws[0].pdfB, RecView{nullptr, 0, 0}, 0, 1};
         DevFilm fd = dev_film(c);
         TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, QueueView{nullptr, shard_stride(n, 1), n, 1}, c->cull ? 1 : 0, c->ws[0].hitB,
-                    c->ws[0].hitPrim};
+                    c->ws[0].hitPrim, nullptr, 1};
         ShadeRefIO sio = shade_ref_io(c);
         sio.rayD = c->ws[0].rayD; sio.lamA = c->ws[0].lamA; sio.lamB = c->ws[0].lamB; sio.pdfA = c->ws[0].pdfA; sio.pdfB = c->ws[0].pdfB;
         sio.hitB = c->ws[0].hitB; sio.hitPrim = c->ws[0].hitPrim;
-        RecordIO rio{n, c->ws[0].rayO, c->ws[0].rayD, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA, c->ws[0].pdfB, c->ws[0].hitB, c->ws[0].hitPrim, dout, 39};
+        RecordIO rio{n, c->ws[0].rayO, c->ws[0].rayD, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA, c->ws[0].pdfB, c->ws[0].hitB, c->ws[0].hitPrim, dout, 39, 1};
         if (launch_generate(c->stream, 0, n, ids, dev_camera(c->cam), smp, fd, go) != hipSuccess ||
             launch_trace_closest(c->stream, 0, c->dsc.qcap, lane_scene(c, c->ws[0]), tio, c->d_ctr) != hipSuccess ||
             launch_records(c->stream, c->dsc, c->d_spec, fd, sio, rio) != hipSuccess ||

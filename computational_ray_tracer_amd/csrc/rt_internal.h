@@ -196,6 +196,7 @@ struct GenOut {
     RecView rec;                                             // path mode: the slot state (λ, sampler, β, L, ...)
     int lean;  // simple path kernel: no β = 1 / L = 0 / pdf / dimension stores (depth 0, the film kernel and the
                // host's per-depth dimension derive them)
+    int rsh = 0;  // ray k at rayO[k << rsh] / rayD[k << rsh] (1: the workspace's interleaved (o, d) pairs)
 };
 
 // Ray queues are split into kShards shards, each with its own length and chunk-ticket counters: one returning
@@ -237,6 +238,7 @@ struct TraceIO {
     float4* hitB;             // (b0, b1, b2, t) at the ray's queue position
     int* hitPrim;
     int* ticket = nullptr;    // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
+    int rsh = 0;              // ray k at rayO[k << rsh] (1: the workspace's interleaved (o, d) pairs; 0: caller arrays)
 };
 
 struct ShadeRefIO {
@@ -245,6 +247,7 @@ struct ShadeRefIO {
     const float4* hitB; const int* hitPrim;
     float4* film;
     float albedo_c2, illum_c2, illum_scale;
+    int rsh;  // ray k at rayD[k << rsh]
 };
 
 struct PathIO {
@@ -254,6 +257,7 @@ struct PathIO {
     RecView rec;                                                          // slot state (R_LAM ...)
     float4* pdfA; float4* pdfB;                                           // TerminateSecondary writes them
     int depth, max_depth;
+    int rsh;  // queue ray k at rayO[k << rsh] / nO[k << rsh] (1: interleaved (o, d) pairs, 32 B per ray)
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
     int dim;    // >= 0: the sampler dimension every path of this depth starts from (simple path: each bounce takes
                 // two Get2D); -1: per slot in R_MISC
@@ -297,6 +301,7 @@ struct RecordIO {
     const float4* rayO; const float4* rayD; const float4* lamA; const float4* lamB; const float4* pdfA;
     const float4* pdfB; const float4* hitB; const int* hitPrim;
     float* out; int stride;  // rt_sample_record (floats)
+    int rsh = 0;             // ray k at rayO[k << rsh]
 };
 
 hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& ids, const DevCamera& cam,
@@ -306,8 +311,8 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
                            int* out, unsigned long long* ctr);
 struct SortRaysIO {
-    const float4* o; const float4* d; const int* slot;   // the queue
-    float4* so; float4* sd; int* ss;                      // the sorted side queue
+    const float4* o; const float4* d; const int* slot;   // the queue (interleaved (o, d) pairs: d = o + 1, ray k at 2k)
+    float4* so; float4* sd; int* ss;                      // the sorted side queue (interleaved the same way)
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp; size_t temp_bytes;
     float4 lo, scale;                                     // origin quantisation: (p - lo) * scale in [0, 512)

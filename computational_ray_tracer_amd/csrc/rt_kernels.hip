@@ -427,8 +427,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         mat4_mul(cam.c2w, o.x, o.y, o.z, 1.f, wo);
         mat4_mul(cam.c2w, d.x, d.y, d.z, 0.f, wd);
         float inv = 1.0f / sqrtf((wd[0] * wd[0] + wd[1] * wd[1]) + (wd[2] * wd[2] + wd[3] * wd[3]));  // glm dot vec4
-        out.rayO[s] = make_float4(wo[0], wo[1], wo[2], 0.f);
-        out.rayD[s] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
+        out.rayO[s << out.rsh] = make_float4(wo[0], wo[1], wo[2], 0.f);
+        out.rayD[s << out.rsh] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
         out.slot[s] = s;
         if (!out.lean) store8(out.pdfA, out.pdfB, s, pdf);
         if (out.rec.p) {  // path mode: the slot's state
@@ -1141,11 +1141,11 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
         };
         int k = item(0);
         float4 o4 = make_float4(0, 0, 0, 0), d4 = o4;
-        if (k < n) { o4 = io.rayO[k]; d4 = io.rayD[k]; }
+        if (k < n) { o4 = io.rayO[k << io.rsh]; d4 = io.rayD[k << io.rsh]; }
         for (int i = 1; k < n; ++i) {
             const int kn = item(i);
             float4 on = o4, dn = d4;
-            if (kn < n) { on = io.rayO[kn]; dn = io.rayD[kn]; }
+            if (kn < n) { on = io.rayO[kn << io.rsh]; dn = io.rayD[kn << io.rsh]; }
             trace_one(k, o4, d4);
             k = kn; o4 = on; d4 = dn;
         }
@@ -1158,7 +1158,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                 const int idx = base + r * kBlock + (int)threadIdx.x;
                 if (idx < ch.len) {
                     const int p = ch.j * io.q.S + idx;
-                    trace_one(p, io.rayO[p], io.rayD[p]);
+                    trace_one(p, io.rayO[p << io.rsh], io.rayD[p << io.rsh]);
                 }
             }
         }
@@ -1169,7 +1169,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
             const int idx = base + lane_id();
             if (idx < tk.len) {
                 const int p = j * io.q.S + idx;
-                trace_one(p, io.rayO[p], io.rayD[p]);
+                trace_one(p, io.rayO[p << io.rsh], io.rayD[p << io.rsh]);
             }
         }
     }
@@ -1193,7 +1193,7 @@ __device__ __forceinline__ void li_reference(const DevScene& sc, const DevSpectr
     float4 n1 = sc.triNormal[3 * prim], n2 = sc.triNormal[3 * prim + 1], n3 = sc.triNormal[3 * prim + 2];
     V3 n = vnorm(vadd(vadd(vmul(v3(n1.x, n1.y, n1.z), bb.x), vmul(v3(n2.x, n2.y, n2.z), bb.y)),
                       vmul(v3(n3.x, n3.y, n3.z), bb.z)));
-    float4 d4 = io.rayD[s];
+    float4 d4 = io.rayD[s << io.rsh];
     V3 rd = vnorm(v3(d4.x, d4.y, d4.z));  // TriangleIntersect::rayd (Shapes.h:1259)
     if (vdot(n, rd) > 0) n = v3(-n.x, -n.y, -n.z);
     float cosv = gclamp(vdot(n, v3(0, 0, -1)), 0.0f, 1.0f);
@@ -1245,7 +1245,7 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
     to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
     float* r = io.out + (size_t)s * io.stride;
     for (int i = 0; i < 8; ++i) { r[i] = lam[i]; r[8 + i] = pdf[i]; }
-    float4 o = io.rayO[s], d = io.rayD[s];
+    float4 o = io.rayO[s << io.rsh], d = io.rayD[s << io.rsh];
     r[16] = o.x; r[17] = o.y; r[18] = o.z; r[19] = d.x; r[20] = d.y; r[21] = d.z;
     int prim = io.hitPrim[s];
     ((int*)r)[22] = prim;
@@ -1350,7 +1350,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                 }
                 V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
                 V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
-                const float4 d4 = io.rayD[k];
+                const float4 d4 = io.rayD[k << io.rsh];
                 V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
                 if (mt.w > 0) {
                     if (io.depth == 0 && vdot(ng, rayd) < 0) {
@@ -1456,7 +1456,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
-            io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot;
+            io.nO[pn << io.rsh] = nO; io.nD[pn << io.rsh] = nD; io.nSlot[pn] = slot;
         }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1563,7 +1563,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                 float lam[8], beta[8];
                 rload8(io.rec, slot, R_LAM, lam);
                 rload8(io.rec, slot, R_BETA, beta);
-                float4 o4 = io.rayO[k], d4 = io.rayD[k];
+                float4 o4 = io.rayO[k << io.rsh], d4 = io.rayD[k << io.rsh];
                 V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
                 V3 rayd = vnorm(rdw);
                 float4 hb = io.hitB[k];
@@ -1758,7 +1758,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
-            io.nO[pn] = nO; io.nD[pn] = nD; io.nSlot[pn] = slot;
+            io.nO[pn << io.rsh] = nO; io.nD[pn << io.rsh] = nD; io.nSlot[pn] = slot;
         }
     }
 }

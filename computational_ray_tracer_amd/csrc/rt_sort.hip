@@ -21,6 +21,7 @@ __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every th
     return v;
 }
 
+// (both queues hold interleaved (o, d) pairs: ray k at o[2k], d[2k] with d = o + 1, one 32-B line per ray)
 // key = direction octant, then the octahedral position of the direction on a 2^B x 2^B grid, then a Morton code of
 // the origin with O bits per axis (DESIGN.md §6 key table).  Entry k of the sort is the k-th live ray of the sharded
 // queue (shards in order); its value is the ray's queue position.
@@ -41,7 +42,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const int* _
 #pragma unroll
         for (int u = 1; u < kShards; ++u) base = j == u ? pre[u] : base;
         const int pos = j * S + (k - base);
-        float4 p = o[pos], v = d[pos];
+        float4 p = o[2 * pos], v = d[2 * pos];
         auto q = [](float x) {
             x = x < 0.f ? 0.f : (x > 511.f ? 511.f : x);
             return (unsigned)x;
@@ -74,9 +75,9 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int*
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
         const int j = perm[k];
         const int pos = (k / S2) * S + k % S2;
-        const float4 oj = o[j];
-        so[pos] = oj;
-        sd[pos] = d[j];
+        const float4 oj = o[2 * j];
+        so[2 * pos] = oj;
+        sd[2 * pos] = d[2 * j];
         ss[pos] = __float_as_int(oj.w);  // bounce rays carry their slot in o.w: two scattered reads per ray, not three
     }
 }
