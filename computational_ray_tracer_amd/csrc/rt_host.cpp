@@ -1068,8 +1068,9 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
     const bool dyn = c->dsc.qcap != 1;
     const bool lean = !c->dsc.full;  // simple path kernel: no β / L / pdf streams (+4.5 %)
-    // multi-level simple scenes: NEE shadow rays queued and traced by their own kernel (no path state live)
-    const bool shq = c->shadow_queue && c->dsc.qcap != 1 && !c->dsc.full;
+    // multi-level simple scenes: the NEE shadow rays the BVH alone cannot decide (or, with RTMI_SHADOW_QUEUE=1,
+    // all of them) are queued and traced exactly by their own kernel
+    const bool shq = c->dsc.qcap != 1 && !c->dsc.full;
     if (shq)
         for (int l = 0; l < lanes; ++l)
             if ((rc = ensure_shadow_workspace(c, c->ws[l], ncap))) return rc;
@@ -1077,7 +1078,8 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const bool nee = c->dsc.full && c->dsc.n_lights > 0;
     if (nee)
         for (int l = 0; l < lanes; ++l)
-            if ((rc = ensure_nee_workspace(c, c->ws[l], nmax * (size_t)nee_stride(c->dsc.n_lights), ncap))) return rc;
+            if ((rc = ensure_nee_workspace(c, c->ws[l], nmax * (size_t)nee_stride(c->dsc.n_lights), 2 * (size_t)ncap)))
+                return rc;  // (the NEE queue, then the fallback list: rt_internal.h NeeIO)
     // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
     // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
     // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
@@ -1161,7 +1163,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 pio.lean = lean ? 1 : 0;
                 pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.q = qv;
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
-                pio.nO = w.rayO + 2 * (size_t)nxt * qs; pio.nD = pio.nO + 1; pio.rsh = 1;
+                pio.nO = w.rayO + 2 * (size_t)nxt * qs; pio.nD = pio.nO + 1;
                 pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt + kQLen;
                 pio.rec = rv; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
@@ -1176,15 +1178,20 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     sqio.shO = w.shO; sqio.shD = w.shD; sqio.shLA = w.shLA; sqio.shLB = w.shLB;
                     sqio.shCount = qc_cur + kQShadowLen;
                     sqio.shTicket = qc_cur + kQShadowTicket;
+                    sqio.defer = c->shadow_queue ? 0 : 1;
                 }
                 NeeIO nio{};
-                if (nee) nio = NeeIO{w.neeRec, w.neeSlot, qc_cur + kQShadowLen, qc_cur + kQShadowTicket};
+                if (nee)
+                    nio = NeeIO{w.neeRec, w.neeSlot, qc_cur + kQShadowLen, qc_cur + kQShadowTicket, w.neeSlot + ncap,
+                                qc_cur + kQNeeFallback};
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio, nio));
                 ev_mark(c, s, ST_SHADE, e0);
                 if (nee) {  // this bounce's shadow rays, before the next bounce reads L
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_path_nee(s, grid, c->dsc.qcap, dsl, c->d_spec, pio, nio, c->d_ctr));
+                    if (c->dsc.qcap != 1)
+                        HIPCHK(c, launch_path_nee_fallback(s, grid, c->dsc.qcap, dsl, c->d_spec, pio, nio, c->d_ctr));
                     ev_mark(c, s, ST_SHADOW, e0);
                 }
                 if (shq) {

@@ -212,7 +212,7 @@ static const int kShards = 8;
 static const int kQStride = 64;
 enum { kQLen = 0, kQTraceTicket = 1 * kShards * kQStride, kQShadeTicket = 2 * kShards * kQStride,
        kQShadowLen = 3 * kShards * kQStride, kQShadowTicket = 4 * kShards * kQStride,
-       kQRegion = 5 * kShards * kQStride };
+       kQNeeFallback = 5 * kShards * kQStride, kQRegion = 6 * kShards * kQStride };
 // Shard stride of a queue of ns shards for n items (a multiple of 64, so wave chunks stay line-aligned); capacity
 // ns * S.  Single-leaf scenes (static chunks, one block append per 256 rays) keep one shard: sharding their queues
 // cost the Cornell box 3 %; multi-level scenes (per-wave tickets and appends) use kShards (CFG3 +5.5 %).
@@ -251,13 +251,13 @@ struct ShadeRefIO {
 };
 
 struct PathIO {
+    // queue rays are interleaved (o, d) pairs, 32 B per ray: ray k at rayO[2k] / rayD[2k] (rayD = rayO + 1), nO / nD too
     const float4* rayO; const float4* rayD; const int* slot; QueueView q;       // current queue
     const float4* hitB; const int* hitPrim;                                     // at queue position
     float4* nO; float4* nD; int* nSlot; int* nCount;  // next queue: same shard stride, lengths at nCount + j kQStride
     RecView rec;                                                          // slot state (R_LAM ...)
     float4* pdfA; float4* pdfB;                                           // TerminateSecondary writes them
     int depth, max_depth;
-    int rsh;  // queue ray k at rayO[k << rsh] / nO[k << rsh] (1: interleaved (o, d) pairs, 32 B per ray)
     int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
     int dim;    // >= 0: the sampler dimension every path of this depth starts from (simple path: each bounce takes
                 // two Get2D); -1: per slot in R_MISC
@@ -271,6 +271,10 @@ struct PathIO {
 struct ShadowQueueIO {
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
     int *shCount = nullptr, *shTicket = nullptr;
+    // 1: the shade kernel traces its NEE shadow rays inline over the BVH and queues only the ambiguous ones (the
+    // canonical rule could not decide: §6b) for k_path_shadow, which runs the exact traversal; 0: every shadow ray
+    // is queued (RTMI_SHADOW_QUEUE=1).  Multi-level simple-path scenes always have a queue.
+    int defer = 0;
 };
 
 // Deferred NEE of the mixed-scene shade: k_path_shade_full samples every light at a Lambert vertex (same sampler
@@ -287,6 +291,8 @@ struct NeeIO {
     int* slot;     // NEE queue: slot per position (same shard stride as the ray queues)
     int* len;      // shard lengths (zeroed with the queue's counter region)
     int* ticket;   // per-shard chunk tickets of k_path_nee
+    int* fb_slot;  // multi-level scenes: slots of the vertices whose shadow rays the BVH alone could not decide,
+    int* fb_len;   // re-run by k_path_nee<Q, true> with the exact traversal (their count: zeroed with the region)
 };
 
 struct PathFilmIO {
@@ -339,6 +345,8 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
                              const NeeIO& nee = NeeIO{});
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr);
+hipError_t launch_path_nee_fallback(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
+                                    const PathIO& io, const NeeIO& nee, unsigned long long* ctr);
 hipError_t launch_path_nee(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                            const PathIO& io, const NeeIO& nee, unsigned long long* ctr);
 hipError_t launch_resolve(hipStream_t st, int n, const float4* film, const float* m_xyz_from_sensor,

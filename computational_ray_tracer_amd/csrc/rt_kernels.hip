@@ -1077,6 +1077,9 @@ __device__ __forceinline__ int traverse_kz(const DevScene& sc, int set, V3 o, V3
         bool amb = false;
         const int r = ANYHIT ? bvh_anyhit<KZ>(sc, set, o, d, tMax, nn, nt, amb)
                              : bvh_closest<KZ>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, amb);
+#ifdef RT_TIMING_NO_FALLBACK
+        return r;  // timing experiment only: wrong on ambiguous rays
+#endif
         if (!amb) return r;
         ++nfb;  // ambiguous (rare): the reference BFS decides, with the wave's other lanes done with the BVH
     }
@@ -1094,6 +1097,23 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
     if (__ballot(kz == 0) == act) return traverse_kz<QCAP, ANYHIT, 0, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, nfb);
     if (__ballot(kz == 1) == act) return traverse_kz<QCAP, ANYHIT, 1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, nfb);
     return traverse_kz<QCAP, ANYHIT, -1, DFS>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, nfb);
+}
+
+// Multi-level scenes: the BVH walk alone (no reference-BFS fallback in the calling kernel, whose register budget it
+// would set: trace 128 VGPRs + spill with it, 106 without); amb = the canonical rule could not decide, and the caller
+// hands the ray (or its path vertex) to a kernel that runs the exact traversal.
+template <bool ANYHIT>
+__device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
+                                            float& b2, float& t, ctr_t& nn, ctr_t& nt, bool& amb) {
+    int kz = dominant_axis(d);
+    uint64_t act = __ballot(true);
+#define RT_BVH_KZ(K) \
+    return ANYHIT ? bvh_anyhit<K>(sc, set, o, d, tMax, nn, nt, amb) : bvh_closest<K>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, amb)
+    if (__ballot(kz == 2) == act) RT_BVH_KZ(2);
+    if (__ballot(kz == 0) == act) RT_BVH_KZ(0);
+    if (__ballot(kz == 1) == act) RT_BVH_KZ(1);
+    RT_BVH_KZ(-1);
+#undef RT_BVH_KZ
 }
 
 // Register budgets (amdgpu_waves_per_eu) of the multi-level instantiations: 4 waves/SIMD (128 VGPRs) on the trace,
@@ -1350,7 +1370,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
                 }
                 V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
                 V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
-                const float4 d4 = io.rayD[k << io.rsh];
+                const float4 d4 = io.rayD[2 * k];
                 V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
                 if (mt.w > 0) {
                     if (io.depth == 0 && vdot(ng, rayd) < 0) {
@@ -1421,7 +1441,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
             }
         }
         if constexpr (QCAP != 1) {  // shadow queue: the ray and its pending contribution go to k_path_shadow
-            if (shq.shO) {
+            if (!shq.defer) {
                 int sp = WAVE ? wave_append(shq.shCount + qj * kQStride, wantShadow)
                               : block_append(shq.shCount + qj * kQStride, wantShadow, lds);
                 sp += qj * io.q.S;
@@ -1436,17 +1456,33 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         }
         // NEE shadow ray, traced inline (any hit, fixed tMax) after the bounce state is written, so only the
         // pending contribution Ld stays live across the traversal.  No shadow queue in HBM.
+        // Multi-level octrees: the BVH alone; a ray it cannot decide goes to the shadow queue with its pending
+        // contribution (k_path_shadow runs the exact traversal and adds it in the same order).
+        bool deferShadow = false;
         if (wantShadow) {
             float b0, b1, b2, t;
-            int hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt, sfb);
-            ++nsh;
-            if (hit < 0) {
-                float L[8];
-                rload8_or_zero(io.rec, slot, R_L, L, d0);
+            int hit;
+            if constexpr (QCAP != 1) hit = traverse_bvh<true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt, deferShadow);
+            else hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt, sfb);
+            if (!deferShadow) {
+                ++nsh;
+                if (hit < 0) {
+                    float L[8];
+                    rload8_or_zero(io.rec, slot, R_L, L, d0);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) L[i] += Ld[i];
-                rstore8(io.rec, slot, R_L, L);
-                storedL = true;
+                    for (int i = 0; i < 8; ++i) L[i] += Ld[i];
+                    rstore8(io.rec, slot, R_L, L);
+                    storedL = true;
+                }
+            }
+        }
+        if constexpr (QCAP != 1) {
+            const int sp = wave_append(shq.shCount + qj * kQStride, deferShadow) + qj * io.q.S;
+            if (deferShadow) {
+                shq.shO[sp] = make_float4(so.x, so.y, so.z, stmax);
+                shq.shD[sp] = make_float4(sd.x, sd.y, sd.z, __int_as_float(slot));
+                shq.shLA[sp] = make_float4(Ld[0], Ld[1], Ld[2], Ld[3]);
+                shq.shLB[sp] = make_float4(Ld[4], Ld[5], Ld[6], Ld[7]);
             }
         }
         if (d0 && slot >= 0 && !storedL) {
@@ -1456,7 +1492,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
-            io.nO[pn << io.rsh] = nO; io.nD[pn << io.rsh] = nD; io.nSlot[pn] = slot;
+            io.nO[2 * pn] = nO; io.nD[2 * pn] = nD; io.nSlot[pn] = slot;
         }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1563,7 +1599,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                 float lam[8], beta[8];
                 rload8(io.rec, slot, R_LAM, lam);
                 rload8(io.rec, slot, R_BETA, beta);
-                float4 o4 = io.rayO[k << io.rsh], d4 = io.rayD[k << io.rsh];
+                float4 o4 = io.rayO[2 * k], d4 = io.rayD[2 * k];
                 V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
                 V3 rayd = vnorm(rdw);
                 float4 hb = io.hitB[k];
@@ -1758,7 +1794,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
-            io.nO[pn << io.rsh] = nO; io.nD[pn << io.rsh] = nD; io.nSlot[pn] = slot;
+            io.nO[2 * pn] = nO; io.nD[2 * pn] = nD; io.nSlot[pn] = slot;
         }
     }
 }
@@ -1766,29 +1802,57 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
 // Deferred NEE (NeeIO): per queued Lambert vertex, the shadow rays of its lights in light order (any hit, fixed
 // tMax, then the analytic shapes: scene_occluded), then L += ((x (Le D65(λ))) wgt) for the visible lights in the
 // same order — the inline loop's arithmetic term for term.  Only the shadow rays and L are live here.
-template <int QCAP>
+// scene_occluded over the BVH alone (multi-level octrees): amb = the canonical rule could not decide
+__device__ __forceinline__ bool scene_occluded_bvh(const DevScene& sc, V3 o, V3 d, float tmax, ctr_t& nn, ctr_t& nt,
+                                                   bool& amb) {
+    float b0, b1, b2, t;
+    if (traverse_bvh<true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt, amb) >= 0) return true;
+    if (amb) return false;
+    for (int si = 0; si < sc.n_shapes; ++si) {
+        DevShape sh = ldconst(sc.shapes, si);
+        V3 ph;
+        float th;
+        if (shape_isect(sh, o, d, tmax, ph, th)) return true;
+    }
+    return false;
+}
+
+// FB = false: the NEE queue.  On multi-level octrees a vertex with a shadow ray the BVH alone cannot decide is not
+// accumulated but listed (nee.fb_slot); FB = true then re-runs the listed vertices with the exact traversal (the
+// reference BFS for the ambiguous rays), so this kernel never holds the BFS's registers (128 VGPRs + spill -> 108).
+// A vertex's lights are always accumulated together, in light order, by one of the two.
+template <int QCAP, bool FB>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_nee(DevScene sc, const DevSpectra* sp, PathIO io,
                                                                        NeeIO nee, unsigned long long* ctr) {
     stage_scene<QCAP>(sc, 0);
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     const int nl = sc.n_lights, nf4 = nee_stride(nl);
-    const QueueView q{nee.len, io.q.S, 0, io.q.ns};
-    std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<QCAP != 1>> items(nee.ticket, q);
-    int qj, qidx;
-    bool live;
-    while (items.next(qj, qidx, live)) {
-        if (!live) continue;  // (no block-level synchronisation in this kernel)
-        const int slot = nee.slot[qj * q.S + qidx];
+    // one path vertex: visibility of each sampled light, then the unoccluded lights' contributions in order
+    auto vertex = [&](int slot) __attribute__((always_inline)) {
         const float4* r = nee.rec + (size_t)slot * nf4;
         const float4 p4 = r[N_PO];
         const V3 po = v3(p4.x, p4.y, p4.z);
         uint64_t vis = 0;
+        ctr_t nv = 0;
+        bool defer = false;
         for (int li = 0; li < nl; ++li) {
             const float4 ray = r[N_RAY + li];
             if (ray.w < 0) continue;  // light not sampled (cos <= 0)
-            ++nsh;
-            if (!scene_occluded<QCAP>(sc, po, v3(ray.x, ray.y, ray.z), ray.w, snn, snt, sfb)) vis |= 1ull << li;
+            ++nv;
+            bool occ;
+            if constexpr (QCAP != 1 && !FB) {
+                occ = scene_occluded_bvh(sc, po, v3(ray.x, ray.y, ray.z), ray.w, snn, snt, defer);
+                if (defer) break;
+            } else {
+                occ = scene_occluded<QCAP>(sc, po, v3(ray.x, ray.y, ray.z), ray.w, snn, snt, sfb);
+            }
+            if (!occ) vis |= 1ull << li;
         }
+        if (defer) {  // (rare: vector atomics per lane)
+            nee.fb_slot[atomicAdd(nee.fb_len, 1)] = slot;
+            return;
+        }
+        nsh += nv;
         if (vis) {
             float lam[8], L[8];
             rload8(io.rec, slot, R_LAM, lam);
@@ -1808,6 +1872,19 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_nee(DevScen
                 }
             }
             rstore8(io.rec, slot, R_L, L);
+        }
+    };
+    if constexpr (FB) {
+        const int n = *nee.fb_len;
+        for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) vertex(nee.fb_slot[k]);
+    } else {
+        const QueueView q{nee.len, io.q.S, 0, io.q.ns};
+        std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<QCAP != 1>> items(nee.ticket, q);
+        int qj, qidx;
+        bool live;
+        while (items.next(qj, qidx, live)) {
+            if (!live) continue;  // (no block-level synchronisation in this kernel)
+            vertex(nee.slot[qj * q.S + qidx]);
         }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1968,9 +2045,15 @@ hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* 
     return hipGetLastError();
 }
 
+// The fallback passes (the few rays the BVH alone could not decide: 0-100 per launch on CFG3/CFG4) run on a small
+// grid, so their launch neither waits for nor occupies the whole GPU (a resident grid there: CFG3 +0.9 % instead of
+// the BFS-free kernels' full gain).
+static constexpr int kFallbackBlocks = 64;
+
 hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, const DevScene& sc, const PathIO& io,
                               const ShadowQueueIO& shq, unsigned long long* ctr) {
     int gb = grid > 0 ? grid : 1;
+    if (shq.defer) gb = std::min(gb, kFallbackBlocks);
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
 #define RT_SHADOW_CASE(Q)                                                                                        \
@@ -1998,6 +2081,7 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
     if (sc.full && sc.n_lights > 0 && !nee.rec) return hipErrorInvalidValue;  // NEE records are required
+    if (!sc.full && qcap != 1 && !shq.shO) return hipErrorInvalidValue;       // so is the shadow queue
 #define RT_SHADE_CASE(Q)                                                                                         \
     case Q:                                                                                                      \
         if (sc.full)                                                                                             \
@@ -2022,10 +2106,25 @@ hipError_t launch_path_nee(hipStream_t st, int grid, int qcap, const DevScene& s
     int gb = grid > 0 ? grid : 1;
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
+    if (qcap != 1 && (!nee.fb_slot || !nee.fb_len)) return hipErrorInvalidValue;  // the fallback list is required
     switch (qcap) {
-        case 0: hipLaunchKernelGGL(k_path_nee<0>, dim3(resident_grid(k_path_nee<0>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
-        case 1: hipLaunchKernelGGL(k_path_nee<1>, dim3(resident_grid(k_path_nee<1>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
-        case 16: hipLaunchKernelGGL(k_path_nee<16>, dim3(resident_grid(k_path_nee<16>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        case 0: hipLaunchKernelGGL((k_path_nee<0, false>), dim3(resident_grid(k_path_nee<0, false>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        case 1: hipLaunchKernelGGL((k_path_nee<1, false>), dim3(resident_grid(k_path_nee<1, false>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        case 16: hipLaunchKernelGGL((k_path_nee<16, false>), dim3(resident_grid(k_path_nee<16, false>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// the vertices k_path_nee listed (multi-level octrees only; a resident grid, the list's length read on the device)
+hipError_t launch_path_nee_fallback(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
+                                    const PathIO& io, const NeeIO& nee, unsigned long long* ctr) {
+    int gb = std::min(grid > 0 ? grid : 1, kFallbackBlocks);
+    if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
+    dim3 b(kBlock);
+    switch (qcap) {
+        case 0: hipLaunchKernelGGL((k_path_nee<0, true>), dim3(resident_grid(k_path_nee<0, true>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
+        case 16: hipLaunchKernelGGL((k_path_nee<16, true>), dim3(resident_grid(k_path_nee<16, true>, gb, grid)), b, 0, st, sc, sp, io, nee, ctr); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
