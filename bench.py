@@ -64,8 +64,18 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
         "k_path_shade": (st["ms_shade"], st["launches_shade"], 312 * st["rays"] + 32 * st["shadow_rays"],
                          32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"]),
     }
-    if st["ms_shadow"] > 0:  # shadow rays in a kernel of their own, one launch per shade launch: the §8(d) 32 B per
-        # shadow ray and the shadow scene terms move to it (k_path_nee: mixed scenes; k_path_shadow: shadow queue)
+    # Multi-level simple path without the shadow queue: k_path_shade traces its shadow rays inline and k_path_shadow
+    # only gets the few the BVH alone cannot decide (rt_kernels.hip k_path_shade), so the shadow bytes stay with the
+    # shade kernel and the fallback kernel is reported by time only (its ray count is not counted on its own).
+    fallback_only = shadow_kernel == "k_path_shadow" and os.environ.get("RTMI_SHADOW_QUEUE", "0") in ("", "0")
+    fallback = None
+    if st["ms_shadow"] > 0 and fallback_only:
+        fallback = {"kernel": shadow_kernel, "role": "exact traversal of the undecided shadow rays only",
+                    "launches": max(1, st["launches_shade"]),
+                    "avg_launch_ms": round(st["ms_shadow"] / max(1, st["launches_shade"]), 4),
+                    "total_ms": round(st["ms_shadow"], 3)}
+    elif st["ms_shadow"] > 0:  # shadow rays in a kernel of their own, one launch per shade launch: the §8(d) 32 B
+        # per shadow ray and the shadow scene terms move to it (k_path_nee: mixed scenes; k_path_shadow: shadow queue)
         ks[shadow_kernel] = (st["ms_shadow"], st["launches_shade"], 32 * st["shadow_rays"],
                              32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"])
         ks["k_path_shade"] = (st["ms_shade"], st["launches_shade"], 312 * st["rays"], 0)
@@ -88,6 +98,8 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
             res[name]["valu"] = {"achieved": round(g, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
                                  "frac": round(g / VALU_PEAK_GINST, 4),
                                  "insts_per_launch": int(kc["valu_insts_per_launch"])}
+    if fallback:
+        res[shadow_kernel] = fallback
     return res
 
 

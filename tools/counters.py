@@ -17,14 +17,16 @@ import glob
 import json
 from pathlib import Path
 
-KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_nee", "k_path_shadow", "k_generate",
+KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_nee", "k_path_nee_fb", "k_path_shadow", "k_generate",
            "k_path_film", "k_ref_shade_film", "k_sort_keys", "k_sort_gather")
 
 
 def kname(raw):
-    base = raw.split("(")[0].replace("void ", "")
-    base = base.split("<")[0]
-    return base.split("::")[-1]
+    full = raw.split("(")[0].replace("void ", "")
+    base = full.split("<")[0].split("::")[-1]
+    if base == "k_path_nee" and full.replace(" ", "").endswith(",true>"):
+        return "k_path_nee_fb"  # the exact-traversal fallback instantiation (undecided vertices), not the NEE pass
+    return base
 
 
 def per_dispatch(d, counter):
