@@ -500,6 +500,9 @@ struct rt_ctx {
     int sort_rays = 1;         // RTMI_SORT=0: no coherence sort (A/B)
     float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
     int sort_dir_bits = 3, sort_org_bits = 4;  // sort key widths (RTMI_SORT_BITS="dir/org"; 3/7 3/2 2/5 within 2 %)
+    // Morton sort of the NEE queue (mixed multi-level scenes; RTMI_SORT_NEE="on[/bits]"): CFG4 337 -> 364 at 9 bits
+    // per axis (6 / 7 bits: 353 / 356; CFG5 334 -> 355 at 7)
+    int sort_nee = 1, sort_nee_bits = 9;
     hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
     size_t batch_samples = 0;  // samples in flight per batch (0: 16 Mi; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
@@ -1187,6 +1190,19 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio, nio));
                 ev_mark(c, s, ST_SHADE, e0);
+                if (nee && sort_rays && c->sort_nee) {  // NEE vertices in Morton order of their shading points
+                    int lens[kShards * kQStride];
+                    HIPCHK(c, hipMemcpyAsync(lens, qc_cur + kQShadowLen, sizeof(lens), hipMemcpyDeviceToHost, s));
+                    HIPCHK(c, hipStreamSynchronize(s));
+                    int nq = 0;
+                    for (int j = 0; j < kShards; ++j) nq += lens[j * kQStride];
+                    SortNeeIO so{w.neeSlot, qc_cur + kQShadowLen, Sq[l], w.neeRec, nee_stride(c->dsc.n_lights),
+                                 w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp, w.sTempBytes, c->sort_lo,
+                                 c->sort_scale, c->sort_nee_bits};
+                    e0 = ev_start(c, s);
+                    HIPCHK(c, launch_sort_nee(s, nq, so));
+                    ev_mark(c, s, ST_SORT, e0);
+                }
                 if (nee) {  // this bounce's shadow rays, before the next bounce reads L
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_path_nee(s, grid, c->dsc.qcap, dsl, c->d_spec, pio, nio, c->d_ctr));
@@ -1484,6 +1500,8 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_SORT")) c->sort_rays = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BVH_CI")) c->bvh_node_cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) std::sscanf(e, "%d/%d", &c->sort_dir_bits, &c->sort_org_bits);
+    if (const char* e = std::getenv("RTMI_SORT_NEE")) std::sscanf(e, "%d/%d", &c->sort_nee, &c->sort_nee_bits);
+    c->sort_nee_bits = std::max(1, std::min(9, c->sort_nee_bits));
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
     c->hs.init();
     if (dalloc(&c->d_spec, 1) != hipSuccess || dalloc(&c->ws[0].d_qcount, 2 * kQRegion) != hipSuccess ||

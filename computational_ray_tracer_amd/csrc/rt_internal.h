@@ -329,6 +329,16 @@ struct SortRaysIO {
 size_t sort_rays_temp_bytes(int nmax);
 // n = total length of the queue's shards (read back by the host)
 hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io);
+struct SortNeeIO {
+    int* slot; int* len; int S;                          // the NEE queue (NeeIO slot / len), sorted in place
+    const float4* rec; int nf4;                          // NEE records: the shading point at rec[slot * nf4 + N_PO]
+    unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
+    void* temp; size_t temp_bytes;
+    float4 lo, scale;                                    // as SortRaysIO
+    int org_bits;                                        // key: 3 x org_bits Morton code of the shading point
+};
+// n = total length of the NEE queue's shards (read back by the host)
+hipError_t launch_sort_nee(hipStream_t st, int n, const SortNeeIO& io);
 hipError_t launch_oct_classify(hipStream_t st, int nnodes, const float* cbox, const int* seg, const int* ent,
                                const float* tri9, unsigned char* mask, int* stats);
 hipError_t launch_oct_scatter(hipStream_t st, int njobs, int nchild, const int* job, const int* ent,

@@ -82,6 +82,52 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int*
     }
 }
 
+// NEE queue coherence sort (mixed scenes, RTMI_SORT_NEE): the deferred NEE vertices of one bounce reordered by the
+// Morton code of their shading point (org_bits per axis), so the shadow rays of a wave start close together and walk
+// the same BVH nodes toward each light.  k_path_nee still traces and adds a vertex's lights in light order, and the
+// vertices are independent of each other (one slot each), so the film is unchanged.  Entry k is the k-th queued
+// vertex (shards in order); its value is the vertex's slot.
+__global__ void __launch_bounds__(kBlockThreads) k_nee_keys(int n, const int* __restrict__ len, int S,
+                                                             const int* __restrict__ slot,
+                                                             const float4* __restrict__ rec, int nf4, float4 lo,
+                                                             float4 scale, int kOrgB, unsigned* __restrict__ keys,
+                                                             int* __restrict__ vals) {
+    int pre[kShards + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int j = 0; j < kShards; ++j) pre[j + 1] = pre[j] + len[j * kQStride];
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        int j = 0;
+#pragma unroll
+        for (int u = 1; u < kShards; ++u) j += k >= pre[u] ? 1 : 0;
+        int base = pre[0];
+#pragma unroll
+        for (int u = 1; u < kShards; ++u) base = j == u ? pre[u] : base;
+        const int s = slot[j * S + (k - base)];
+        const float4 p = rec[(size_t)s * nf4 + N_PO];
+        auto q = [](float x) {
+            x = x < 0.f ? 0.f : (x > 511.f ? 511.f : x);
+            return (unsigned)x;
+        };
+        keys[k] = spread3(q((p.x - lo.x) * scale.x) >> (9 - kOrgB)) << 2 |
+                  spread3(q((p.y - lo.y) * scale.y) >> (9 - kOrgB)) << 1 |
+                  spread3(q((p.z - lo.z) * scale.z) >> (9 - kOrgB));
+        vals[k] = s;
+    }
+}
+
+// sorted entry k -> shard k / S2 of the NEE queue (in place: the slots were copied into the sort's values), and the
+// shard lengths rewritten for that split
+__global__ void __launch_bounds__(kBlockThreads) k_nee_scatter(int n, const int* __restrict__ sorted, int S, int S2,
+                                                                int* __restrict__ slot, int* __restrict__ len) {
+    if (blockIdx.x == 0 && threadIdx.x < kShards) {
+        const int c = n - (int)threadIdx.x * S2;
+        len[threadIdx.x * kQStride] = c < 0 ? 0 : (c > S2 ? S2 : c);
+    }
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+        slot[(k / S2) * S + k % S2] = sorted[k];
+}
+
 }  // namespace
 
 size_t sort_rays_temp_bytes(int nmax) {
@@ -104,6 +150,21 @@ hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.S, shard_stride(n, kShards),
                        io.o, io.d, io.so, io.sd, io.ss, io.len);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_nee(hipStream_t st, int n, const SortNeeIO& io) {
+    if (n <= 0) return hipSuccess;
+    int g = (n + kBlockThreads - 1) / kBlockThreads;
+    g = g < 8192 ? g : 8192;
+    hipLaunchKernelGGL(k_nee_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.len, io.S, io.slot, io.rec, io.nf4,
+                       io.lo, io.scale, io.org_bits, io.keys, io.vals);
+    size_t bytes = io.temp_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
+                                                      3 * io.org_bits, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nee_scatter, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.S,
+                       shard_stride(n, kShards), io.slot, io.len);
     return hipGetLastError();
 }
 
