@@ -499,7 +499,11 @@ struct rt_ctx {
     int shadow_dfs = 1;
     int sort_rays = 1;         // RTMI_SORT=0: no coherence sort (A/B)
     float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
-    int sort_dir_bits = 3, sort_org_bits = 4;  // sort key widths (RTMI_SORT_BITS="dir/org"; 3/7 3/2 2/5 within 2 %)
+    int sort_dir_bits = 3, sort_org_bits = 4;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; 3/7 3/2 2/5 within 2 %)
+    // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
+    // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
+    // queue has a sort of its own (CFG4 372 vs 367)
+    int sort_org_major = -1;
     // Morton sort of the NEE queue (mixed multi-level scenes; RTMI_SORT_NEE="on[/bits]"): CFG4 337 -> 364 at 9 bits
     // per axis (6 / 7 bits: 353 / 356; CFG5 334 -> 355 at 7)
     int sort_nee = 1, sort_nee_bits = 9;
@@ -1146,6 +1150,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 if (sort_rays && depth > 0) {
                     SortRaysIO so{cO, cD, cS, w.sO, w.sD, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt,
                                   w.sTemp, w.sTempBytes, c->sort_lo, c->sort_scale, c->sort_dir_bits, c->sort_org_bits,
+                                  c->sort_org_major >= 0 ? c->sort_org_major : (c->dsc.full ? 0 : 1),
                                   qc_cur + kQLen, Sq[l]};
                     int lens[kShards * kQStride];
                     HIPCHK(c, hipMemcpyAsync(lens, qc_cur + kQLen, sizeof(lens), hipMemcpyDeviceToHost, s));
@@ -1499,7 +1504,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_SHADOW_DFS")) c->shadow_dfs = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT")) c->sort_rays = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BVH_CI")) c->bvh_node_cost = (float)std::atof(e);
-    if (const char* e = std::getenv("RTMI_SORT_BITS")) std::sscanf(e, "%d/%d", &c->sort_dir_bits, &c->sort_org_bits);
+    if (const char* e = std::getenv("RTMI_SORT_BITS")) std::sscanf(e, "%d/%d/%d", &c->sort_dir_bits, &c->sort_org_bits, &c->sort_org_major);
     if (const char* e = std::getenv("RTMI_SORT_NEE")) std::sscanf(e, "%d/%d", &c->sort_nee, &c->sort_nee_bits);
     c->sort_nee_bits = std::max(1, std::min(9, c->sort_nee_bits));
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));

@@ -323,6 +323,7 @@ struct SortRaysIO {
     void* temp; size_t temp_bytes;
     float4 lo, scale;                                     // origin quantisation: (p - lo) * scale in [0, 512)
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin
+    int org_major;                                        // 1: origin Morton code in the high bits instead
     int* len;     // the queue's shard lengths (kQLen region): read, then rewritten for the sorted queue
     int S;        // shard stride (the sorted queue keeps it; its shards split the sorted order evenly)
 };

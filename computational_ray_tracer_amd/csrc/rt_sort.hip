@@ -28,8 +28,8 @@ __device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every th
 __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const int* __restrict__ len, int S,
                                                               const float4* __restrict__ o,
                                                               const float4* __restrict__ d, float4 lo, float4 scale,
-                                                              int kDirB, int kOrgB, unsigned* __restrict__ keys,
-                                                              int* __restrict__ vals) {
+                                                              int kDirB, int kOrgB, int org_major,
+                                                              unsigned* __restrict__ keys, int* __restrict__ vals) {
     int pre[kShards + 1];
     pre[0] = 0;
 #pragma unroll
@@ -54,7 +54,8 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const int* _
         unsigned mo = spread3(q((p.x - lo.x) * scale.x) >> (9 - kOrgB)) << 2 |
                       spread3(q((p.y - lo.y) * scale.y) >> (9 - kOrgB)) << 1 |
                       spread3(q((p.z - lo.z) * scale.z) >> (9 - kOrgB));
-        keys[k] = ((oct << (2 * kDirB) | ux << kDirB | uy) << (3 * kOrgB)) | mo;
+        const unsigned dk = oct << (2 * kDirB) | ux << kDirB | uy;
+        keys[k] = org_major ? (mo << (3 + 2 * kDirB)) | dk : (dk << (3 * kOrgB)) | mo;
         vals[k] = pos;
     }
 }
@@ -143,7 +144,7 @@ hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
     g = g < 8192 ? g : 8192;
     const int key_bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
     hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.len, io.S, io.o, io.d, io.lo, io.scale,
-                       io.dir_bits, io.org_bits, io.keys, io.vals);
+                       io.dir_bits, io.org_bits, io.org_major, io.keys, io.vals);
     size_t bytes = io.temp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
                                                       key_bits, st);
