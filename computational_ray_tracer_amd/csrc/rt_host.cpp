@@ -1085,8 +1085,8 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const bool nee = c->dsc.full && c->dsc.n_lights > 0;
     if (nee)
         for (int l = 0; l < lanes; ++l)
-            if ((rc = ensure_nee_workspace(c, c->ws[l], nmax * (size_t)nee_stride(c->dsc.n_lights), 2 * (size_t)ncap)))
-                return rc;  // (the NEE queue, then the fallback list: rt_internal.h NeeIO)
+            if ((rc = ensure_nee_workspace(c, c->ws[l], nmax * (size_t)nee_stride(c->dsc.n_lights), 3 * (size_t)ncap)))
+                return rc;  // (the NEE queue, the fallback list, the NEE sort keys: rt_internal.h NeeIO)
     // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
     // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
     // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
@@ -1189,21 +1189,23 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     sqio.defer = c->shadow_queue ? 0 : 1;
                 }
                 NeeIO nio{};
+                const bool sort_nee = nee && sort_rays && c->sort_nee;
+                unsigned* nee_key = reinterpret_cast<unsigned*>(w.neeSlot + 2 * ncap);
                 if (nee)
                     nio = NeeIO{w.neeRec, w.neeSlot, qc_cur + kQShadowLen, qc_cur + kQShadowTicket, w.neeSlot + ncap,
-                                qc_cur + kQNeeFallback};
+                                qc_cur + kQNeeFallback, sort_nee ? nee_key : nullptr, c->sort_lo, c->sort_scale,
+                                c->sort_nee_bits};
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio, nio));
                 ev_mark(c, s, ST_SHADE, e0);
-                if (nee && sort_rays && c->sort_nee) {  // NEE vertices in Morton order of their shading points
+                if (sort_nee) {  // NEE vertices in Morton order of their shading points
                     int lens[kShards * kQStride];
                     HIPCHK(c, hipMemcpyAsync(lens, qc_cur + kQShadowLen, sizeof(lens), hipMemcpyDeviceToHost, s));
                     HIPCHK(c, hipStreamSynchronize(s));
                     int nq = 0;
                     for (int j = 0; j < kShards; ++j) nq += lens[j * kQStride];
-                    SortNeeIO so{w.neeSlot, qc_cur + kQShadowLen, Sq[l], w.neeRec, nee_stride(c->dsc.n_lights),
-                                 w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp, w.sTempBytes, c->sort_lo,
-                                 c->sort_scale, c->sort_nee_bits};
+                    SortNeeIO so{w.neeSlot, qc_cur + kQShadowLen, Sq[l], nee_key, w.sKeys, w.sKeysAlt, w.sVals,
+                                 w.sValsAlt, w.sTemp, w.sTempBytes, c->sort_nee_bits};
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_nee(s, nq, so));
                     ev_mark(c, s, ST_SORT, e0);

@@ -293,7 +293,28 @@ struct NeeIO {
     int* ticket;   // per-shard chunk tickets of k_path_nee
     int* fb_slot;  // multi-level scenes: slots of the vertices whose shadow rays the BVH alone could not decide,
     int* fb_len;   // re-run by k_path_nee<Q, true> with the exact traversal (their count: zeroed with the region)
+    unsigned* key; // NEE sort (nullptr: none): the Morton code of the shading point per NEE queue position
+    float4 lo, scale; int key_bits;  // its quantisation (SortRaysIO lo / scale) and bits per axis
 };
+
+// 9 bits -> every third bit of 27
+__device__ __forceinline__ unsigned spread3_9(unsigned v) {
+    v &= 0x1ffu;
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+// Morton code of p quantised as (p - lo) * scale in [0, 512), `bits` per axis (the coherence sorts' origin keys)
+__device__ __forceinline__ unsigned morton_key(float x, float y, float z, float4 lo, float4 scale, int bits) {
+    auto q = [](float v) {
+        v = v < 0.f ? 0.f : (v > 511.f ? 511.f : v);
+        return (unsigned)v;
+    };
+    return spread3_9(q((x - lo.x) * scale.x) >> (9 - bits)) << 2 | spread3_9(q((y - lo.y) * scale.y) >> (9 - bits)) << 1 |
+           spread3_9(q((z - lo.z) * scale.z) >> (9 - bits));
+}
 
 struct PathFilmIO {
     const int* work_pixels; int n_pixels; int n_index;
@@ -332,10 +353,9 @@ size_t sort_rays_temp_bytes(int nmax);
 hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io);
 struct SortNeeIO {
     int* slot; int* len; int S;                          // the NEE queue (NeeIO slot / len), sorted in place
-    const float4* rec; int nf4;                          // NEE records: the shading point at rec[slot * nf4 + N_PO]
+    const unsigned* key;                                 // per queue position, written by k_path_shade_full (NeeIO key)
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp; size_t temp_bytes;
-    float4 lo, scale;                                    // as SortRaysIO
     int org_bits;                                        // key: 3 x org_bits Morton code of the shading point
 };
 // n = total length of the NEE queue's shards (read back by the host)

@@ -1590,6 +1590,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
     while (items.next(qj, qidx, live)) {
         const int k = qj * io.q.S + qidx;  // queue position
         bool wantNext = false, wantNee = false;
+        unsigned neeKey = 0;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int slot = -1;
         if (live) {
@@ -1712,6 +1713,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                             float4* nr = nee.rec + (size_t)slot * nee_f4;
                             float* nwgt = reinterpret_cast<float*>(nr + N_RAY + sc.n_lights);
                             nr[N_PO] = make_float4(po.x, po.y, po.z, 0.f);
+                            if (nee.key) neeKey = morton_key(po.x, po.y, po.z, nee.lo, nee.scale, nee.key_bits);
                             for (int li = 0; li < sc.n_lights; ++li) {
                                 const DevLight Lt = ldconst(sc.lights, li);
                                 float u0, u1;
@@ -1790,7 +1792,10 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
             }
         }
         const int pe = queue_append<WAVE>(nee.len + qj * kQStride, wantNee, lds) + qj * io.q.S;
-        if (wantNee) nee.slot[pe] = slot;
+        if (wantNee) {
+            nee.slot[pe] = slot;
+            if (nee.key) nee.key[pe] = neeKey;
+        }
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)

@@ -84,15 +84,14 @@ __global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int*
 }
 
 // NEE queue coherence sort (mixed scenes, RTMI_SORT_NEE): the deferred NEE vertices of one bounce reordered by the
-// Morton code of their shading point (org_bits per axis), so the shadow rays of a wave start close together and walk
-// the same BVH nodes toward each light.  k_path_nee still traces and adds a vertex's lights in light order, and the
+// Morton code of their shading point (org_bits per axis; k_path_shade_full writes it beside the queue entry), so the
+// shadow rays of a wave start close together and walk the same BVH nodes toward each light.  k_path_nee still traces and adds a vertex's lights in light order, and the
 // vertices are independent of each other (one slot each), so the film is unchanged.  Entry k is the k-th queued
 // vertex (shards in order); its value is the vertex's slot.
 __global__ void __launch_bounds__(kBlockThreads) k_nee_keys(int n, const int* __restrict__ len, int S,
                                                              const int* __restrict__ slot,
-                                                             const float4* __restrict__ rec, int nf4, float4 lo,
-                                                             float4 scale, int kOrgB, unsigned* __restrict__ keys,
-                                                             int* __restrict__ vals) {
+                                                             const unsigned* __restrict__ key,
+                                                             unsigned* __restrict__ keys, int* __restrict__ vals) {
     int pre[kShards + 1];
     pre[0] = 0;
 #pragma unroll
@@ -104,16 +103,9 @@ __global__ void __launch_bounds__(kBlockThreads) k_nee_keys(int n, const int* __
         int base = pre[0];
 #pragma unroll
         for (int u = 1; u < kShards; ++u) base = j == u ? pre[u] : base;
-        const int s = slot[j * S + (k - base)];
-        const float4 p = rec[(size_t)s * nf4 + N_PO];
-        auto q = [](float x) {
-            x = x < 0.f ? 0.f : (x > 511.f ? 511.f : x);
-            return (unsigned)x;
-        };
-        keys[k] = spread3(q((p.x - lo.x) * scale.x) >> (9 - kOrgB)) << 2 |
-                  spread3(q((p.y - lo.y) * scale.y) >> (9 - kOrgB)) << 1 |
-                  spread3(q((p.z - lo.z) * scale.z) >> (9 - kOrgB));
-        vals[k] = s;
+        const int pos = j * S + (k - base);
+        keys[k] = key[pos];
+        vals[k] = slot[pos];
     }
 }
 
@@ -158,8 +150,8 @@ hipError_t launch_sort_nee(hipStream_t st, int n, const SortNeeIO& io) {
     if (n <= 0) return hipSuccess;
     int g = (n + kBlockThreads - 1) / kBlockThreads;
     g = g < 8192 ? g : 8192;
-    hipLaunchKernelGGL(k_nee_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.len, io.S, io.slot, io.rec, io.nf4,
-                       io.lo, io.scale, io.org_bits, io.keys, io.vals);
+    hipLaunchKernelGGL(k_nee_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.len, io.S, io.slot, io.key, io.keys,
+                       io.vals);
     size_t bytes = io.temp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
                                                       3 * io.org_bits, st);
