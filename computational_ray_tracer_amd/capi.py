@@ -125,7 +125,7 @@ EXPORTS = [
     "rt_create", "rt_destroy", "rt_last_error", "rt_abi_version",
     "rt_scene_upload", "rt_camera_set", "rt_sampler_set", "rt_film_set", "rt_integrator_set", "rt_set_shard",
     "rt_render_pass", "rt_render_pass_device", "rt_film_resolve",
-    "rt_get_stats", "rt_reset_stats", "rt_octree_get_info", "rt_octree_export",
+    "rt_get_stats", "rt_reset_stats", "rt_octree_get_info", "rt_octree_export", "rt_bvh_export", "rt_debug_bvh_build",
     "rt_debug_trace", "rt_debug_occluded", "rt_debug_samples",
     "rt_film_resolve_srgb", "rt_load_obj", "rt_mesh_free", "rt_image_write", "rt_rgb_to_sigmoid", "rt_rgb_fit_sigmoid",
     "rt_sensor_name", "rt_film_matrices",
@@ -169,6 +169,10 @@ def load_library(path=None):
         "rt_reset_stats": ([C.c_void_p], C.c_int),
         "rt_octree_get_info": ([C.c_void_p, P(rt_octree_info)], C.c_int),
         "rt_octree_export": ([C.c_void_p, P(C.c_float), P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32)], C.c_int),
+        "rt_bvh_export": ([C.c_void_p, C.c_int, P(C.c_int), P(C.c_int), P(C.c_float), P(C.c_float), P(C.c_float)],
+                          C.c_int),
+        "rt_debug_bvh_build": ([P(rt_scene_desc), C.c_int, P(C.c_int), P(C.c_int), P(C.c_float), P(C.c_float),
+                               P(C.c_float)], C.c_int),
         "rt_debug_trace": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), C.c_int, P(C.c_int32), P(C.c_float)], C.c_int),
         "rt_debug_occluded": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_int32)], C.c_int),
         "rt_debug_samples": ([C.c_void_p, C.c_int, P(C.c_int32), P(C.c_int32), P(rt_sample_record)], C.c_int),

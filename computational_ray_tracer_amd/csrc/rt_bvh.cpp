@@ -1,15 +1,27 @@
-// 4-wide BVH over a tile set's triangles (host build, uploaded with the scene) for the fast multi-level
+// 8-wide compressed BVH over a tile set's triangles (host build, uploaded with the scene) for the fast multi-level
 // traversal of rt_kernels.hip.  The BVH never decides a result on its own: the kernels apply the
 // canonical closest-hit / any-hit rule over the triangles it reaches and hand every ambiguous ray to the
 // reference-order octree BFS (Octtree_Model.h:66-127), so only the set of triangles reachable by a ray matters,
-// and every box is padded outwards (conservative: a triangle the watertight test hits at t lies in boxes the ray
+// and every box is rounded outwards (conservative: a triangle the watertight test hits at t lies in boxes the ray
 // enters before t).
 //
-// Build: binned SAH (16 bins per axis, leaves of <= 8 triangles) into a binary tree, collapsed to 4-wide nodes by
-// repeatedly opening the largest-area internal child.  Node layout (128 B, one cache line): float4 lo.x[4],
-// hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4], int4 child[4], pad.  Child words: >= 0 internal node, -1 empty,
-// otherwise a leaf 0x80000000 | first_tile << 4 | (count - 1) over the leaf-ordered tile array (3 float4 per
-// triangle, the octree tiles' format).
+// Build: binned SAH (16 bins per axis, leaves of <= kMaxLeaf triangles) into a binary tree, collapsed to 8-wide
+// nodes by repeatedly opening the largest-area internal child.
+//
+// Node (one 128-B cache line, 8 float4; the kernels read the first five):
+//   N0 = (origin.xyz, bits: ex | ey << 8 | ez << 16 | imask << 24)   origin = the node's padded box corner,
+//        e_a = the biased exponent of the axis' quantum 2^(e_a - 127); imask bit k = child slot k is a node
+//   N1 = (child_base, tile_base, counts, valid)   internal child k = child_base + popcount(imask below k); leaf
+//        child k = counts nibble k triangles (1..15) at tile_base + the sum of the nibbles below k; valid bit k =
+//        slot k is used
+//   N2..N4 = the x, y, z child planes: u8 lo[8] then u8 hi[8] per axis; the child's box along a is
+//        [origin_a + lo 2^(e_a-127), origin_a + hi 2^(e_a-127)] ⊇ its triangles' box padded by `pad` (exact:
+//        lo = floor, hi = ceil of the exact quotients, computed in double)
+//   N5..N7 = zero (line padding)
+// The top kBvhTopLevels levels are laid out breadth-first at the front (nodes [0, kBvhTopNodes), staged in LDS by
+// the kernels), every deeper subtree depth-first after them: a node's internal children are one contiguous block,
+// its leaf children's tiles one contiguous run, in the same depth-first order as the nodes (treelet-contiguous).
+// Tiles: 3 float4 per triangle in the octree tiles' format (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -46,11 +58,10 @@ struct Node2 {
 };
 
 constexpr int kBins = 16;
-constexpr int kMaxLeaf = 8;
 
 struct Builder {
-    const float* tri9;
     float node_cost = 1.f;       // SAH: cost of opening a node relative to one triangle test
+    int max_leaf = kBvhMaxLeaf;
     std::vector<Box> pbox;
     std::vector<float> cen;      // 3 per primitive
     std::vector<int> perm;
@@ -66,7 +77,7 @@ struct Builder {
         }
         nodes[id].box = bb;
         const int n = e - b;
-        if (n <= 2) {
+        if (n <= 2 && n <= max_leaf) {
             nodes[id].first = b; nodes[id].count = n;
             return id;
         }
@@ -104,11 +115,9 @@ struct Builder {
         }
         const double parea = std::max(bb.area(), 1e-30);
         const double split_cost = node_cost + best / parea;
-        if (bax < 0 || (n <= kMaxLeaf && (double)n <= split_cost)) {
-            if (n <= kMaxLeaf) {
-                nodes[id].first = b; nodes[id].count = n;
-                return id;
-            }
+        if (n <= max_leaf && (bax < 0 || (double)n <= split_cost)) {
+            nodes[id].first = b; nodes[id].count = n;
+            return id;
         }
         int mid;
         if (bax < 0) {  // coincident centroids: split by count
@@ -135,37 +144,20 @@ struct Collapse {
     const Builder& B;
     const float* tri9;
     const int* ids;
-    float pad;
+    double pad;
     BvhData& out;
     int depth_max = 0;
 
-    void push_tiles(const Node2& lf) {
-        for (int i = lf.first; i < lf.first + lf.count; ++i) {
-            const int p = B.perm[i];
-            const float* v = tri9 + 9 * (size_t)p;
-            float fid;
-            std::memcpy(&fid, &ids[p], 4);
-            out.tiles.push_back(make_float4(v[0], v[1], v[2], v[3]));
-            out.tiles.push_back(make_float4(v[4], v[5], v[6], v[7]));
-            out.tiles.push_back(make_float4(v[8], fid, 0.f, 0.f));
-        }
-    }
-    int leaf_word(const Node2& lf) {
-        const int first = (int)(out.tiles.size() / 3);
-        push_tiles(lf);
-        out.max_leaf = std::max(out.max_leaf, lf.count);
-        return (int)(0x80000000u | ((unsigned)first << 4) | (unsigned)(lf.count - 1));
-    }
-    // the up-to-4 binary nodes that become the children of the 4-wide node for binary node n2 (opening the
-    // largest-area internal child until there are 4)
-    std::vector<int> children4(int n2) const {
+    // the up-to-8 binary nodes that become the children of the 8-wide node for binary node n2 (opening the
+    // largest-area internal child until there are 8)
+    std::vector<int> children8(int n2) const {
         std::vector<int> ch;
         if (B.nodes[n2].left < 0) {
             ch.push_back(n2);  // a leaf root
             return ch;
         }
         ch = {B.nodes[n2].left, B.nodes[n2].right};
-        while (ch.size() < 4) {
+        while (ch.size() < 8) {
             int pick = -1;
             double pa = -1;
             for (size_t k = 0; k < ch.size(); ++k)
@@ -177,69 +169,128 @@ struct Collapse {
         }
         return ch;
     }
-    int reserve() {
-        const int me = (int)(out.nodes.size() / 8);
-        out.nodes.resize(out.nodes.size() + 8);
+    int reserve(int n) {
+        const int me = (int)(out.nodes.size() / kBvhNodeF4);
+        out.nodes.resize(out.nodes.size() + (size_t)n * kBvhNodeF4, make_float4(0.f, 0.f, 0.f, 0.f));
         return me;
     }
-    void write_node(int me, const std::vector<int>& ch, const int* word) {
-        float lo[3][4], hi[3][4];
-        for (int k = 0; k < 4; ++k)
-            for (int a = 0; a < 3; ++a) { lo[a][k] = 0.f; hi[a][k] = 0.f; }
-        int w[4] = {-1, -1, -1, -1};
+    int n_internal(const std::vector<int>& ch) const {
+        int k = 0;
+        for (int c : ch) k += B.nodes[c].left >= 0;
+        return k;
+    }
+    // Quantise the children of node `me` (binary ids ch, slot order) and write its header.  Internal children
+    // are the nodes child_base, child_base + 1, ... in slot order; leaf children's tiles are appended here.
+    void write_node(int me, const std::vector<int>& ch, int child_base) {
+        double lo[8][3], hi[8][3];
+        double plo[3] = {INFINITY, INFINITY, INFINITY}, phi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t k = 0; k < ch.size(); ++k) {
+            const Box& b = B.nodes[ch[k]].box;
+            for (int a = 0; a < 3; ++a) {
+                lo[k][a] = (double)b.lo[a] - pad;
+                hi[k][a] = (double)b.hi[a] + pad;
+                plo[a] = std::min(plo[a], lo[k][a]);
+                phi[a] = std::max(phi[a], hi[k][a]);
+            }
+        }
+        float org[3];
+        int ebias[3];
+        for (int a = 0; a < 3; ++a) {
+            // the float origin at or below the padded corner, then the smallest quantum 2^e with 255 2^e >= extent
+            float o = (float)plo[a];
+            if ((double)o > plo[a]) o = std::nextafter(o, -INFINITY);
+            org[a] = o;
+            const double ext = phi[a] - (double)o;
+            int e = -100;
+            if (ext > 0) {
+                e = (int)std::ceil(std::log2(ext / 255.0));
+                while (std::ldexp(255.0, e) < ext) ++e;
+                while (e > -100 && std::ldexp(255.0, e - 1) >= ext) --e;
+            }
+            ebias[a] = e + 127;
+        }
+        unsigned qlo[3][8] = {}, qhi[3][8] = {};
+        unsigned imask = 0, valid = 0, counts = 0;
+        const int tile_base = (int)(out.tiles.size() / 3);
+        int ci = 0;
         for (size_t k = 0; k < ch.size(); ++k) {
             const Node2& c = B.nodes[ch[k]];
-            for (int a = 0; a < 3; ++a) { lo[a][k] = c.box.lo[a] - pad; hi[a][k] = c.box.hi[a] + pad; }
-            w[k] = word[k];
+            for (int a = 0; a < 3; ++a) {
+                const double q = std::ldexp(1.0, ebias[a] - 127);
+                const double l = std::floor((lo[k][a] - (double)org[a]) / q);
+                const double h = std::ceil((hi[k][a] - (double)org[a]) / q);
+                qlo[a][k] = (unsigned)std::min(std::max(l, 0.0), 255.0);
+                qhi[a][k] = (unsigned)std::min(std::max(h, 0.0), 255.0);
+            }
+            valid |= 1u << k;
+            if (c.left >= 0) {
+                imask |= 1u << k;
+                ++ci;
+            } else {
+                counts |= (unsigned)c.count << (4 * k);
+                for (int i = c.first; i < c.first + c.count; ++i) {
+                    const int p = B.perm[i];
+                    const float* v = tri9 + 9 * (size_t)p;
+                    float fid;
+                    std::memcpy(&fid, &ids[p], 4);
+                    out.tiles.push_back(make_float4(v[0], v[1], v[2], v[3]));
+                    out.tiles.push_back(make_float4(v[4], v[5], v[6], v[7]));
+                    out.tiles.push_back(make_float4(v[8], fid, 0.f, 0.f));
+                }
+                out.max_leaf = std::max(out.max_leaf, c.count);
+            }
         }
-        float4* nd = &out.nodes[8 * (size_t)me];
+        (void)ci;
+        float4* nd = &out.nodes[(size_t)kBvhNodeF4 * me];
+        unsigned w0 = (unsigned)ebias[0] | (unsigned)ebias[1] << 8 | (unsigned)ebias[2] << 16 | imask << 24;
+        float fw0;
+        std::memcpy(&fw0, &w0, 4);
+        nd[0] = make_float4(org[0], org[1], org[2], fw0);
+        const unsigned h1[4] = {(unsigned)child_base, (unsigned)tile_base, counts, valid};
+        std::memcpy(&nd[1], h1, 16);
         for (int a = 0; a < 3; ++a) {
-            nd[2 * a] = make_float4(lo[a][0], lo[a][1], lo[a][2], lo[a][3]);
-            nd[2 * a + 1] = make_float4(hi[a][0], hi[a][1], hi[a][2], hi[a][3]);
+            unsigned w[4] = {0, 0, 0, 0};
+            for (int k = 0; k < 8; ++k) {
+                w[k >> 2] |= qlo[a][k] << (8 * (k & 3));
+                w[2 + (k >> 2)] |= qhi[a][k] << (8 * (k & 3));
+            }
+            std::memcpy(&nd[2 + a], w, 16);  // the bytes' bits, never through float registers
         }
-        std::memcpy(&nd[6], w, 16);  // the child words' bits, never through float registers
-        nd[7] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    // depth-first: the 4-wide node for binary node n2 and its subtree, appended; returns its index
-    int emit(int n2, int depth) {
+    // depth-first: node `me` for binary node n2, its children block, then each internal child's subtree
+    void emit(int n2, int me, int depth) {
         depth_max = std::max(depth_max, depth);
-        const int me = reserve();
-        const std::vector<int> ch = children4(n2);
-        int word[4] = {-1, -1, -1, -1};
-        for (size_t k = 0; k < ch.size(); ++k)
-            word[k] = B.nodes[ch[k]].left < 0 ? leaf_word(B.nodes[ch[k]]) : emit(ch[k], depth + 1);
-        write_node(me, ch, word);
-        return me;
+        const std::vector<int> ch = children8(n2);
+        const int ni = n_internal(ch);
+        const int base = ni ? reserve(ni) : 0;
+        write_node(me, ch, base);
+        int k = 0;
+        for (int c : ch)
+            if (B.nodes[c].left >= 0) emit(c, base + k++, depth + 1);
     }
-    // the top kBvhTopLevels levels breadth-first (nodes 0 .. kBvhTopNodes - 1 at most, which the kernels stage in
-    // LDS), every deeper subtree depth-first after them
+    // the top kBvhTopLevels levels breadth-first (nodes [0, kBvhTopNodes) at most, staged in LDS by the kernels),
+    // every deeper subtree depth-first after them
     void emit_root(int root) {
-        std::vector<std::pair<int, int>> level = {{root, reserve()}};
+        std::vector<std::pair<int, int>> level = {{root, reserve(1)}};
         for (int depth = 0; depth < kBvhTopLevels && !level.empty(); ++depth) {
             depth_max = std::max(depth_max, depth);
             std::vector<std::pair<int, int>> next;
-            std::vector<std::pair<int, std::vector<int>>> pend;  // (node index, children) of this level
+            std::vector<std::vector<int>> chs;
+            std::vector<int> bases;
             for (const auto& [n2, me] : level) {
-                std::vector<int> ch = children4(n2);
-                pend.emplace_back(me, ch);
+                chs.push_back(children8(n2));
+                const int ni = n_internal(chs.back());
+                bases.push_back(ni ? reserve(ni) : 0);
             }
-            // indices of the next level first (contiguous), then leaves / deeper subtrees
-            std::vector<std::vector<int>> words(pend.size(), std::vector<int>(4, -1));
-            for (size_t i = 0; i < pend.size(); ++i)
-                for (size_t k = 0; k < pend[i].second.size(); ++k) {
-                    const int c = pend[i].second[k];
-                    if (B.nodes[c].left >= 0 && depth + 1 < kBvhTopLevels) {
-                        words[i][k] = reserve();
-                        next.emplace_back(c, words[i][k]);
-                    }
-                }
-            for (size_t i = 0; i < pend.size(); ++i) {
-                for (size_t k = 0; k < pend[i].second.size(); ++k) {
-                    const int c = pend[i].second[k];
-                    if (B.nodes[c].left < 0) words[i][k] = leaf_word(B.nodes[c]);
-                    else if (depth + 1 >= kBvhTopLevels) words[i][k] = emit(c, depth + 1);
-                }
-                write_node(pend[i].first, pend[i].second, words[i].data());
+            for (size_t i = 0; i < level.size(); ++i) {
+                write_node(level[i].second, chs[i], bases[i]);
+                int k = 0;
+                for (int c : chs[i])
+                    if (B.nodes[c].left >= 0) next.emplace_back(c, bases[i] + k++);
+            }
+            if (depth + 1 >= kBvhTopLevels) {
+                for (const auto& [n2, me] : next) emit(n2, me, depth + 1);
+                break;
             }
             level = std::move(next);
         }
@@ -248,22 +299,18 @@ struct Collapse {
 
 }  // namespace
 
-void build_bvh4(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out) {
+void build_bvh8(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out, int max_leaf) {
     out.nodes.clear();
     out.tiles.clear();
     out.max_leaf = 0;
     out.depth = 0;
-    if (n == 0) {  // an empty root: every child word -1
-        out.nodes.assign(8, make_float4(0.f, 0.f, 0.f, 0.f));
-        float m1;
-        const int neg = -1;
-        std::memcpy(&m1, &neg, 4);
-        out.nodes[6] = make_float4(m1, m1, m1, m1);
+    if (n == 0) {  // an empty root: no valid child
+        out.nodes.assign(kBvhNodeF4, make_float4(0.f, 0.f, 0.f, 0.f));
         return;
     }
     Builder B;
-    B.tri9 = tri9;
     B.node_cost = node_cost;
+    B.max_leaf = std::min(std::max(max_leaf, 1), 15);
     B.pbox.resize(n);
     B.cen.resize(3 * (size_t)n);
     B.perm.resize(n);
@@ -276,8 +323,8 @@ void build_bvh4(const float* tri9, const int* ids, int n, float pad, float node_
     }
     B.nodes.reserve(2 * (size_t)n);
     B.build(0, n);
-    Collapse C{B, tri9, ids, pad, out};
-    out.nodes.reserve(8 * (size_t)(n / 2 + 1));
+    Collapse C{B, tri9, ids, (double)pad, out};
+    out.nodes.reserve((size_t)kBvhNodeF4 * (n / 4 + 1));
     out.tiles.reserve(3 * (size_t)n);
     C.emit_root(0);
     out.depth = C.depth_max;

@@ -499,6 +499,9 @@ struct rt_ctx {
     int shadow_dfs = 1;
     int sort_rays = 1;         // RTMI_SORT=0: no coherence sort (A/B)
     float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
+    int bvh_max_leaf = kBvhMaxLeaf;  // triangles per BVH leaf at most (RTMI_BVH_LEAF)
+    int bvh_count[2][2] = {};  // per tile set: BVH nodes, BVH tiles (rt_bvh_export)
+    int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
     int sort_dir_bits = 3, sort_org_bits = 4;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; 3/7 3/2 2/5 within 2 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
@@ -1506,7 +1509,18 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_SHADOW_DFS")) c->shadow_dfs = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT")) c->sort_rays = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BVH_CI")) c->bvh_node_cost = (float)std::atof(e);
-    if (const char* e = std::getenv("RTMI_SORT_BITS")) std::sscanf(e, "%d/%d/%d", &c->sort_dir_bits, &c->sort_org_bits, &c->sort_org_major);
+    if (const char* e = std::getenv("RTMI_BVH_LEAF")) c->bvh_max_leaf = std::max(1, std::min(15, std::atoi(e)));
+    if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
+    if (const char* e = std::getenv("RTMI_SORT_BITS")) {
+        int db = 3, ob = 4, om = -1;
+        const int got = std::sscanf(e, "%d/%d/%d", &db, &ob, &om);
+        // the key is 3 octant bits + 2 x db direction bits + 3 x ob origin bits in one u32, ob <= 9 (spread3_9)
+        if (got >= 2 && db >= 0 && db <= 9 && ob >= 0 && ob <= 9 && 3 + 2 * db + 3 * ob <= 32) {
+            c->sort_dir_bits = db;
+            c->sort_org_bits = ob;
+            if (got == 3) c->sort_org_major = om < 0 ? -1 : (om ? 1 : 0);
+        }
+    }
     if (const char* e = std::getenv("RTMI_SORT_NEE")) std::sscanf(e, "%d/%d", &c->sort_nee, &c->sort_nee_bits);
     c->sort_nee_bits = std::max(1, std::min(9, c->sort_nee_bits));
     if (const char* e = std::getenv("RTMI_BATCH_SAMPLES")) c->batch_samples = (size_t)std::max(0L, std::atol(e));
@@ -1566,6 +1580,72 @@ static void destroy_one(rt_ctx* c) {
 
 const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+// World-space triangles of a (validated) scene: ObjectToRender * vec4(p,1) per vertex (= the per-test transform,
+// Shapes.h:1117-1122), back-face flags (Shapes.h:1339-1380) and degenerate flags (Shapes.h:1131).
+struct SceneWorld {
+    std::vector<F3> wv, tri3;
+    std::vector<uint8_t> back, degen;
+};
+static void scene_world(const rt_scene_desc* s, SceneWorld& w) {
+    const int nt = s->n_triangles, nv = s->n_vertices;
+    w.wv.resize(nv);
+    for (int i = 0; i < nv; ++i) {
+        float o[4];
+        m4v(s->object_to_render, s->positions[3 * i], s->positions[3 * i + 1], s->positions[3 * i + 2], 1.f, o);
+        w.wv[i] = {o[0], o[1], o[2]};
+    }
+    w.tri3.resize(3 * (size_t)nt);
+    for (int t = 0; t < nt; ++t)
+        for (int k = 0; k < 3; ++k) w.tri3[3 * (size_t)t + k] = w.wv[s->indices[3 * t + k]];
+    w.back.assign(nt, 0);
+    w.degen.assign(nt, 0);
+    const bool cull = s->cull_backfaces != 0;
+    F3 look = f3norm({s->cull_look[0], s->cull_look[1], s->cull_look[2]});
+    for (int t = 0; t < nt; ++t) {
+        const F3* p = &w.tri3[3 * (size_t)t];
+        F3 cr = f3cross(f3sub(p[2], p[0]), f3sub(p[1], p[0]));
+        w.degen[t] = f3dot(cr, cr) == 0;
+        if (cull) {
+            F3 n[3];
+            for (int k = 0; k < 3; ++k) {
+                uint32_t v = s->indices[3 * t + k];
+                n[k] = {s->normals[3 * v], s->normals[3 * v + 1], s->normals[3 * v + 2]};
+            }
+            F3 sum = f3add(f3add(n[0], n[1]), n[2]);
+            F3 N = f3norm({sum.x / 3.0f, sum.y / 3.0f, sum.z / 3.0f});
+            N = f3norm(m3v(s->normal_to_render, N));
+            w.back[t] = f3dot(look, N) > 0;
+        }
+    }
+}
+// The fast traversal's BVH over tile set `set` (non-degenerate triangles; set 1 without the back-facing ones) and
+// the canonical rule's constants, from M = max |world vertex coordinate|:
+//   wabs = M 2^-20 (the window W(t) = t 2^-16 + wabs; the oracle's Octree::SetWindow computes the same value);
+//   pad = M 2^-18: every child box is padded by it before quantisation.  The slab test's rounding (box_entry in
+//     rt_kernels.hip: base = fma(origin, inv, -o inv), t = fma(q, inv 2^e, base)) moves a plane by at most a few
+//     ulp of max(|o|, M) along its axis, i.e. < 2^-21 max(|o|, M), well inside the pad while |o| <= 8 M;
+//   oguard = 8 M: rays whose origin lies farther out in some coordinate are declared ambiguous (exact BFS).
+static void scene_bvh(const SceneWorld& w, int set, float node_cost, int max_leaf, BvhData& out, float& wabs,
+                      float& oguard) {
+    float mc = 0.f;
+    for (const F3& p : w.wv) mc = std::max(mc, std::max(std::fabs(p.x), std::max(std::fabs(p.y), std::fabs(p.z))));
+    wabs = mc * 0x1p-20f;
+    oguard = mc * 8.f;
+    const float pad = mc * 0x1p-18f;
+    const int nt = (int)w.degen.size();
+    std::vector<float> t9;
+    std::vector<int> ids;
+    for (int t = 0; t < nt; ++t) {
+        if (w.degen[t] || (set == 1 && w.back[t])) continue;
+        for (int k = 0; k < 3; ++k) {
+            const F3& p = w.tri3[3 * (size_t)t + k];
+            t9.push_back(p.x); t9.push_back(p.y); t9.push_back(p.z);
+        }
+        ids.push_back(t);
+    }
+    build_bvh8(t9.data(), ids.data(), (int)ids.size(), pad, node_cost, out, max_leaf);
+}
+
 static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     if (!c || !s) return RT_E_ARG;
     if (s->n_triangles <= 0 || s->n_vertices <= 0 || !s->positions || !s->indices)
@@ -1618,36 +1698,11 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     hipStreamSynchronize(c->stream);
     free_scene(c);
     const int nt = s->n_triangles, nv = s->n_vertices;
-    // world vertices: ObjectToRender * vec4(p,1) per vertex (= the per-test transform, Shapes.h:1117-1122)
-    std::vector<F3> wv(nv);
-    for (int i = 0; i < nv; ++i) {
-        float o[4];
-        m4v(s->object_to_render, s->positions[3 * i], s->positions[3 * i + 1], s->positions[3 * i + 2], 1.f, o);
-        wv[i] = {o[0], o[1], o[2]};
-    }
-    std::vector<F3> tri3(3 * (size_t)nt);
-    for (int t = 0; t < nt; ++t)
-        for (int k = 0; k < 3; ++k) tri3[3 * (size_t)t + k] = wv[s->indices[3 * t + k]];
-    // back-face flags (Shapes.h:1339-1380) and degenerate flags (Shapes.h:1131)
-    std::vector<uint8_t> back(nt, 0), degen(nt, 0);
+    SceneWorld sw;
+    scene_world(s, sw);
+    const std::vector<F3>& tri3 = sw.tri3;
+    const std::vector<uint8_t>&back = sw.back, &degen = sw.degen;
     c->cull = s->cull_backfaces != 0;
-    F3 look = f3norm({s->cull_look[0], s->cull_look[1], s->cull_look[2]});
-    for (int t = 0; t < nt; ++t) {
-        const F3* p = &tri3[3 * (size_t)t];
-        F3 cr = f3cross(f3sub(p[2], p[0]), f3sub(p[1], p[0]));
-        degen[t] = f3dot(cr, cr) == 0;
-        if (c->cull) {
-            F3 n[3];
-            for (int k = 0; k < 3; ++k) {
-                uint32_t v = s->indices[3 * t + k];
-                n[k] = {s->normals[3 * v], s->normals[3 * v + 1], s->normals[3 * v + 2]};
-            }
-            F3 sum = f3add(f3add(n[0], n[1]), n[2]);
-            F3 N = f3norm({sum.x / 3.0f, sum.y / 3.0f, sum.z / 3.0f});
-            N = f3norm(m3v(s->normal_to_render, N));
-            back[t] = f3dot(look, N) > 0;
-        }
-    }
     // root bounds: TriModel::Bounds (Shapes.h:1390-1397): object-space min/max (max starts at FLT_MIN, :1292)
     // then Bounds3::Transform (Shapes.h:60-98, same FLT_MIN quirk)
     const float FMAX = std::numeric_limits<float>::max(), FMIN = std::numeric_limits<float>::min();
@@ -1778,26 +1833,10 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     // multi-level octrees: the fast traversal's BVH per tile set (non-degenerate triangles; set 1 without the
     // back-facing ones) and the canonical-rule window (rt_bvh.cpp)
     BvhData bvh[2];
-    float wabs = 0.f;
-    if (qcap != 1) {
-        float mc = 0.f;
-        for (const F3& p : wv) mc = std::max(mc, std::max(std::fabs(p.x), std::max(std::fabs(p.y), std::fabs(p.z))));
-        wabs = mc * 0x1p-20f;  // same value as the oracle's Octree::SetWindow
-        const float pad = mc * 0x1p-18f;
-        for (int st = 0; st < (c->cull ? 2 : 1); ++st) {
-            std::vector<float> t9;
-            std::vector<int> ids;
-            for (int t = 0; t < nt; ++t) {
-                if (degen[t] || (st == 1 && back[t])) continue;
-                for (int k = 0; k < 3; ++k) {
-                    const F3& p = tri3[3 * (size_t)t + k];
-                    t9.push_back(p.x); t9.push_back(p.y); t9.push_back(p.z);
-                }
-                ids.push_back(t);
-            }
-            build_bvh4(t9.data(), ids.data(), (int)ids.size(), pad, c->bvh_node_cost, bvh[st]);
-        }
-    }
+    float wabs = 0.f, oguard = 0.f;
+    if (qcap != 1)
+        for (int st = 0; st < (c->cull ? 2 : 1); ++st)
+            scene_bvh(sw, st, c->bvh_node_cost, c->bvh_max_leaf, bvh[st], wabs, oguard);
     c->info.n_nodes = nn;
     c->info.n_leaf_refs = (int)c->h_refs.size();
     c->info.max_queue_groups = bound;
@@ -1926,11 +1965,14 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         return rc;
     void* pbv[2] = {nullptr, nullptr};
     void* pbt[2] = {nullptr, nullptr};
-    const int bvh_nodes0 = (int)(bvh[0].nodes.size() / 8);
+    const int bvh_nodes0 = (int)(bvh[0].nodes.size() / kBvhNodeF4);
     for (int st = 0; st < 2; ++st) {
+        c->bvh_count[st][0] = (int)(bvh[st].nodes.size() / kBvhNodeF4);
+        c->bvh_count[st][1] = (int)(bvh[st].tiles.size() / 3);
         if (bvh[st].nodes.empty()) continue;
         // the kernels stage nodes [0, kBvhTopNodes) in LDS unconditionally: pad with empty nodes
-        if (bvh[st].nodes.size() < 8 * (size_t)kBvhTopNodes) bvh[st].nodes.resize(8 * (size_t)kBvhTopNodes, make_float4(0.f, 0.f, 0.f, 0.f));
+        if (bvh[st].nodes.size() < kBvhNodeF4 * (size_t)kBvhTopNodes)
+            bvh[st].nodes.resize(kBvhNodeF4 * (size_t)kBvhTopNodes, make_float4(0.f, 0.f, 0.f, 0.f));
         if ((rc = up(bvh[st].nodes.data(), bvh[st].nodes.size() * 16, &pbv[st])) ||
             (rc = up(bvh[st].tiles.data(), bvh[st].tiles.size() * 16, &pbt[st])))
             return rc;
@@ -1941,6 +1983,9 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         d.btiles[st] = (const float4*)(pbt[st] ? pbt[st] : pbt[0]);
     }
     d.wabs = wabs;
+    d.oguard = oguard;
+    d.amb_force = c->force_amb >= 0;
+    d.amb_mask = c->force_amb > 0 ? (1u << c->force_amb) - 1u : 0u;
     c->info.bvh_nodes = bvh_nodes0;
     c->info.bvh_depth = bvh[0].depth;
     d.clusters[0] = (const float4*)pc0; d.clusters[1] = (const float4*)pc1;
@@ -2163,6 +2208,48 @@ static int impl_rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32
     if (leaf_first) std::memcpy(leaf_first, c->h_leaf_first.data(), c->h_leaf_first.size() * 4);
     if (leaf_count) std::memcpy(leaf_count, c->h_leaf_count.data(), c->h_leaf_count.size() * 4);
     if (refs) std::memcpy(refs, c->h_refs.data(), c->h_refs.size() * 4);
+    return RT_OK;
+}
+
+// The fast traversal's BVH as uploaded (tile set `set`): counts always, arrays when the pointers are non-null.
+static int impl_rt_bvh_export(rt_ctx* c, int set, int* n_nodes, int* n_tiles, float* consts, float* nodes, float* tiles) {
+    if (!c || set < 0 || set > 1) return RT_E_ARG;
+    if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
+    if (set == 1 && !c->cull) set = 0;  // the kernels use set 0's arrays when there is no culled set
+    if (n_nodes) *n_nodes = c->bvh_count[set][0];
+    if (n_tiles) *n_tiles = c->bvh_count[set][1];
+    if (consts) { consts[0] = c->dsc.wabs; consts[1] = c->dsc.oguard; }
+    hipSetDevice(c->device);
+    if (nodes && c->bvh_count[set][0])
+        HIPCHK(c, hipMemcpy(nodes, c->dsc.bvh[set], (size_t)c->bvh_count[set][0] * kBvhNodeF4 * 16, hipMemcpyDeviceToHost));
+    if (tiles && c->bvh_count[set][1])
+        HIPCHK(c, hipMemcpy(tiles, c->dsc.btiles[set], (size_t)c->bvh_count[set][1] * 48, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+// The same BVH built on the host alone (no device): the upload's world transform, tile-set filter, padding and
+// build parameters (RTMI_BVH_CI / RTMI_BVH_LEAF as rt_create reads them).  For CPU tests of the traversal.
+static int impl_rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes, int* n_tiles, float* consts,
+                                   float* nodes, float* tiles) {
+    if (!s || set < 0 || set > 1 || s->n_triangles <= 0 || s->n_vertices <= 0 || !s->positions || !s->indices)
+        return RT_E_ARG;
+    if (s->cull_backfaces && !s->normals) return RT_E_ARG;
+    for (int t = 0; t < 3 * s->n_triangles; ++t)
+        if (s->indices[t] >= (uint32_t)s->n_vertices) return RT_E_ARG;
+    float cost = 3.f;
+    int leaf = kBvhMaxLeaf;
+    if (const char* e = std::getenv("RTMI_BVH_CI")) cost = (float)std::atof(e);
+    if (const char* e = std::getenv("RTMI_BVH_LEAF")) leaf = std::max(1, std::min(15, std::atoi(e)));
+    SceneWorld sw;
+    scene_world(s, sw);
+    BvhData b;
+    float wabs = 0.f, oguard = 0.f;
+    scene_bvh(sw, s->cull_backfaces ? set : 0, cost, leaf, b, wabs, oguard);
+    if (n_nodes) *n_nodes = (int)(b.nodes.size() / kBvhNodeF4);
+    if (n_tiles) *n_tiles = (int)(b.tiles.size() / 3);
+    if (consts) { consts[0] = wabs; consts[1] = oguard; }
+    if (nodes) std::memcpy(nodes, b.nodes.data(), b.nodes.size() * 16);
+    if (tiles) std::memcpy(tiles, b.tiles.data(), b.tiles.size() * 16);
     return RT_OK;
 }
 
@@ -2421,6 +2508,12 @@ int rt_octree_get_info(rt_ctx* c, rt_octree_info* out) {
 }
 int rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32_t* leaf_first, int32_t* leaf_count, int32_t* refs) {
     return guarded([&] { return impl_rt_octree_export(c, bounds, child, leaf_first, leaf_count, refs); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_bvh_export(rt_ctx* c, int set, int* n_nodes, int* n_tiles, float* consts, float* nodes, float* tiles) {
+    return guarded([&] { return impl_rt_bvh_export(c, set, n_nodes, n_tiles, consts, nodes, tiles); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes, int* n_tiles, float* consts, float* nodes, float* tiles) {
+    return guarded([&] { return impl_rt_debug_bvh_build(s, set, n_nodes, n_tiles, consts, nodes, tiles); }, [](const std::string&) {});
 }
 int rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* rd, int use_cull, int32_t* prim, float* bt) {
     return guarded([&] { return impl_rt_debug_trace(c, n, ro, rd, use_cull, prim, bt); }, [&](const std::string& m) { set_error(c, m); });

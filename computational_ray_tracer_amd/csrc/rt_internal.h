@@ -131,11 +131,16 @@ struct DevScene {
     int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
     int ring_mask;
     int ring_threads;               // launches with qcap == 0 are clamped to this many threads
-    // multi-level octrees (qcap != 1): the fast traversal's 4-wide BVH per tile set (rt_bvh.cpp: 8 float4 per
-    // node) and its leaf-ordered triangle tiles; rays it finds ambiguous fall back to the octree BFS
+    // multi-level octrees (qcap != 1): the fast traversal's 8-wide compressed BVH per tile set (rt_bvh.cpp:
+    // kBvhNodeF4 float4 per node) and its leaf-ordered triangle tiles; rays it finds ambiguous fall back to the
+    // octree BFS
     const float4* bvh[2];
     const float4* btiles[2];
     float wabs;                     // canonical-rule window W(t) = t 2^-16 + wabs
+    float oguard;                   // rays whose origin has a coordinate beyond +-oguard are ambiguous (the box
+                                    // padding covers the slab test's rounding only for origins inside 8 M)
+    unsigned amb_mask;              // test knob (RTMI_FORCE_AMB=k): with amb_force set, rays whose direction-bit hash
+    int amb_force;                  // has its low k bits zero are declared ambiguous (exercises every fallback path)
 };
 
 // device counter slots (u64).  Every wave of a persistent kernel adds its totals at the end, all at about the same
@@ -148,15 +153,18 @@ constexpr int kCtrLine = 32;   // u64 between words: 256 B
 constexpr size_t kCtrWords = (size_t)C_NCOUNTERS * kCtrSubs * kCtrLine;
 __host__ __device__ inline size_t ctr_word(int slot, int sub) { return ((size_t)slot * kCtrSubs + sub) * kCtrLine; }
 
-// host: 4-wide BVH build (rt_bvh.cpp)
-// the top levels of every BVH are laid out breadth-first: nodes [0, kBvhTopNodes) (1 + 4 + 16), staged in LDS by
-// the multi-level traversal kernels
-static const int kBvhTopLevels = 3, kBvhTopNodes = 21;
+// host: 8-wide compressed BVH build (rt_bvh.cpp; node layout there): kBvhNodeF4 float4 (128 B) per node.
+// The top levels of every BVH are laid out breadth-first: nodes [0, kBvhTopNodes) (1 + 8), staged in LDS by the
+// multi-level traversal kernels.
+static const int kBvhNodeF4 = 8, kBvhNodeRead = 5;  // float4 per node / float4 the kernels read (N0..N4)
+static const int kBvhTopLevels = 2, kBvhTopNodes = 9;
+static const int kBvhMaxLeaf = 8;                     // triangles per leaf (SAH may stop earlier)
 struct BvhData {
     std::vector<float4> nodes, tiles;
     int depth = 0, max_leaf = 0;
 };
-void build_bvh4(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out);
+void build_bvh8(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out,
+                int max_leaf = kBvhMaxLeaf);
 
 }  // namespace rtmi
 

@@ -50,36 +50,38 @@ __device__ __forceinline__ void stage_leaf1(const DevScene& sc, int set) {
     __syncthreads();
 }
 #define RT_LEAF1(tiles, base, j) (g_leaf1 + 3 * (j))
-// multi-level scenes: the BVH's breadth-first top levels (kBvhTopNodes nodes, 2.6 KB; rt_bvh.cpp emit_root), which
-// every ray opens, staged in LDS at kernel start by every kernel that traverses the BVH
-#ifndef RT_BVH_TOP
-#define RT_BVH_TOP 1
-#endif
-__shared__ float4 g_top[8 * kBvhTopNodes];
+// multi-level scenes: the BVH's breadth-first top levels (kBvhTopNodes 8-wide nodes, the 80 B the kernels read of
+// each; rt_bvh.cpp emit_root), which every ray opens, staged in LDS at kernel start by every kernel that traverses
+// the BVH
+__shared__ float4 g_top[kBvhNodeRead * kBvhTopNodes];
 template <int QCAP>
 __device__ __forceinline__ void stage_scene(const DevScene& sc, int set) {
     if constexpr (QCAP == 1) {
         stage_leaf1(sc, set);
-    } else if constexpr (RT_BVH_TOP) {
+    } else {
         // (the host pads every node array to at least kBvhTopNodes nodes)
         if (sc.bvh[set])
-            for (int i = threadIdx.x; i < 8 * kBvhTopNodes; i += blockDim.x) g_top[i] = sc.bvh[set][i];
+            for (int i = threadIdx.x; i < kBvhNodeRead * kBvhTopNodes; i += blockDim.x)
+                g_top[i] = sc.bvh[set][(i / kBvhNodeRead) * kBvhNodeF4 + i % kBvhNodeRead];
         __syncthreads();
     }
 }
-struct BvhNode {
-    float4 LX, HX, LY, HY, LZ, HZ, CW;
+// An 8-wide node as the kernels read it (rt_bvh.cpp): header N0, N1 and the quantised child planes per axis.
+struct BvhNode8 {
+    float4 N0;
+    uint4 N1, QX, QY, QZ;
 };
-__device__ __forceinline__ BvhNode load_node(const float4* __restrict__ nodes, int node) {
-    BvhNode b;
-    if (RT_BVH_TOP && node < kBvhTopNodes) {
-        const float4* N = g_top + 8 * node;
-        b = {N[0], N[1], N[2], N[3], N[4], N[5], N[6]};
-    } else {
-        const float4* N = nodes + 8 * (size_t)node;
-        b = {N[0], N[1], N[2], N[3], N[4], N[5], N[6]};
+__device__ __forceinline__ uint4 as_u4(float4 v) {
+    return make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w));
+}
+__device__ __forceinline__ BvhNode8 load_node8(const float4* __restrict__ nodes, int node) {
+    // two explicit paths (ds_read / global_load), not one generic pointer (flat loads)
+    if (node < kBvhTopNodes) {
+        const float4* N = g_top + kBvhNodeRead * node;
+        return BvhNode8{N[0], as_u4(N[1]), as_u4(N[2]), as_u4(N[3]), as_u4(N[4])};
     }
-    return b;
+    const float4* N = nodes + (size_t)kBvhNodeF4 * node;
+    return BvhNode8{N[0], as_u4(N[1]), as_u4(N[2]), as_u4(N[3]), as_u4(N[4])};
 }
 // the simple path's per-triangle shading inputs on single-leaf scenes (<= 64 triangles): world vertices and the
 // material's (c0, c1, c2, emission), staged in LDS by k_path_shade<1>
@@ -889,62 +891,110 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
 
 // ============================================================= fast multi-level traversal
 // The reference's unordered BFS (Octtree_Model.h:66-127) only shrinks tMax when its order happens to reach the
-// near leaf, and its answer depends on that order only through near-ties.  Multi-level scenes therefore walk a
-// 4-wide BVH (rt_bvh.cpp) nearest-child first and apply the canonical rule of oracle/rtcore.hpp
+// near leaf, and its answer depends on that order only through near-ties.  Multi-level scenes therefore walk an
+// 8-wide compressed BVH (rt_bvh.cpp) nearest-child first and apply the canonical rule of oracle/rtcore.hpp
 // (Octree::ClosestCanonical / OccludedCanonical), which tests/test_canonical_traversal.py checks against the BFS
-// on >= 10 M rays:
+// on >= 10 M rays (over this BVH: oracle Bvh8Walk restates this walk bit for bit):
 //   closest hit: keep the two smallest-t distinct triangles (t1, t2), prune with cut = t1 + 2 W(t1).  If
 //                t2 > t1 + W(t1) the BFS must end on t1's triangle with the same (b, t); otherwise (or on a stack
-//                overflow) the ray is ambiguous;
+//                overflow, or an origin beyond the guard) the ray is ambiguous;
 //   any hit:     a passing triangle with t < tMax - W(tMax) proves occlusion; hits only inside the window are
 //                ambiguous.
-// Ambiguous rays — rare: coplanar / touching surfaces, near-tMax occluders — run the reference BFS below.
+// Ambiguous rays — rare: coplanar / touching surfaces, near-tMax occluders — run the reference BFS.
 __device__ __forceinline__ float canon_window(float t, float wabs) { return t * 0x1p-16f + wabs; }
 
-// conservative slab test of one child box: entry distance in [0, tcut] or +inf.  (lo - o)/d is computed as
-// fma(lo, inv, -o inv), i.e. exactly for an origin perturbed by half an ulp; boxes are padded by 2^-18 of the
-// scene's extent at build, which covers that.  inv = 1 / d with |d| clamped to >= 2^-80 (bvh_inv): a zero
-// component then gives huge but finite plane distances of the right sign (no inf - inf), and the clamped ray
-// leaves a slab it starts in only after ~pad / 2^-80, far beyond any distance in a scene.
-__device__ __forceinline__ float child_entry(float lx, float hx, float ly, float hy, float lz, float hz, V3 inv, V3 oi,
-                                             float tcut) {
-    const float x0 = __builtin_fmaf(lx, inv.x, -oi.x), x1 = __builtin_fmaf(hx, inv.x, -oi.x);
-    const float y0 = __builtin_fmaf(ly, inv.y, -oi.y), y1 = __builtin_fmaf(hy, inv.y, -oi.y);
-    const float z0 = __builtin_fmaf(lz, inv.z, -oi.z), z1 = __builtin_fmaf(hz, inv.z, -oi.z);
-    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.f));
-    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tcut)) * 1.00000048f;
-    return tn <= tf ? tn : __builtin_inff();
-}
+// inv = 1 / d with |d| clamped to >= 2^-80: a zero component then gives huge but finite plane distances of the
+// right sign (no inf - inf), and the clamped ray leaves a slab it starts in only after ~pad / 2^-80, far beyond any
+// distance in a scene.
 __device__ __forceinline__ V3 bvh_inv(V3 d) {
     const float e = 0x1p-80f;
     return v3(1 / copysignf(fmaxf(fabsf(d.x), e), d.x), 1 / copysignf(fmaxf(fabsf(d.y), e), d.y),
               1 / copysignf(fmaxf(fabsf(d.z), e), d.z));
 }
-__device__ __forceinline__ void cswap(float& ea, int& wa, float& eb, int& wb) {
-    const bool s = eb < ea;
-    const float e = s ? eb : ea;
-    const int w = s ? wb : wa;
-    eb = s ? ea : eb; wb = s ? wa : wb;
-    ea = e; wa = w;
+// Rays the BVH may not decide: an origin beyond the padding's validity, or picked by the RTMI_FORCE_AMB test knob.
+__device__ __forceinline__ bool bvh_refuses(const DevScene& sc, V3 o, V3 d) {
+    if (!(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)) <= sc.oguard)) return true;
+    return sc.amb_force &&
+           (((__float_as_uint(d.x) ^ (__float_as_uint(d.y) >> 3) ^ (__float_as_uint(d.z) >> 7)) & sc.amb_mask) == 0);
 }
 __device__ __forceinline__ void decode_leaf(int w, int& lf, int& lc) {
     lf = (w >> 4) & 0x7ffffff;
     lc = (w & 15) + 1;
 }
+__device__ __forceinline__ void kswap(unsigned& a, unsigned& b) {
+    const unsigned lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo; b = hi;
+}
+static constexpr unsigned kNoChild = 0xffffffffu;
 
-// closest hit over the BVH: returns the triangle id (or -1) with (b0, b1, b2, t); amb = the BFS must decide
-template <int KZ>
-__device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0,
-                                           float& rb1, float& rb2, float& rt, ctr_t& nn, ctr_t& nt, bool& amb) {
-    const float4* __restrict__ nodes = sc.bvh[set];
-    const float4* __restrict__ tiles = sc.btiles[set];
-    const V3 inv = bvh_inv(d);
-    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-    const TriRay R = make_triray<KZ>(o, d);
+// One 8-wide node against the ray: the sorted child keys k[0] <= ... <= k[7].  Key of a child whose slab interval
+// [tn, tf] is non-empty within [0, tcut]: (bits(tn) with the low 3 bits cleared) | slot — tn >= 0, so the keys
+// order the children by entry distance (truncated: a smaller value, the cull on pop stays conservative); missed
+// and unused slots: kNoChild.  The slab test: the child's plane along axis a is origin_a + q 2^(e_a - 127), its
+// parametric distance (plane - o_a) inv_a is evaluated as fma(q, inv_a 2^(e_a - 127), fma(origin_a, inv_a,
+// -o_a inv_a)) — the scaling by a power of two is exact, so each plane moves by a few ulp of max(|o|, M) at
+// most, which the build's padding covers (rt_host.cpp scene_bvh).  The near plane along a is the lo plane when
+// inv_a >= 0, else the hi plane (the same interval as min / max of the two); tf is widened by 1.00000048 as the
+// reference's IntersectP widens tFar (Shapes.h:116, 1 + 2 gamma(3)).
+struct Bvh8Ray {
+    V3 inv, oi;
+};
+__device__ __forceinline__ void node_keys(const BvhNode8& n, const Bvh8Ray& r, float tcut, unsigned k[8]) {
+    const unsigned w0 = __float_as_uint(n.N0.w);
+    const float sx = ldexpf(r.inv.x, (int)(w0 & 255u) - 127), sy = ldexpf(r.inv.y, (int)((w0 >> 8) & 255u) - 127),
+                sz = ldexpf(r.inv.z, (int)((w0 >> 16) & 255u) - 127);
+    const float bx = __builtin_fmaf(n.N0.x, r.inv.x, -r.oi.x), by = __builtin_fmaf(n.N0.y, r.inv.y, -r.oi.y),
+                bz = __builtin_fmaf(n.N0.z, r.inv.z, -r.oi.z);
+    const bool px = r.inv.x >= 0.f, py = r.inv.y >= 0.f, pz = r.inv.z >= 0.f;
+    const unsigned nx0 = px ? n.QX.x : n.QX.z, nx1 = px ? n.QX.y : n.QX.w, fx0 = px ? n.QX.z : n.QX.x, fx1 = px ? n.QX.w : n.QX.y;
+    const unsigned ny0 = py ? n.QY.x : n.QY.z, ny1 = py ? n.QY.y : n.QY.w, fy0 = py ? n.QY.z : n.QY.x, fy1 = py ? n.QY.w : n.QY.y;
+    const unsigned nz0 = pz ? n.QZ.x : n.QZ.z, nz1 = pz ? n.QZ.y : n.QZ.w, fz0 = pz ? n.QZ.z : n.QZ.x, fz1 = pz ? n.QZ.w : n.QZ.y;
+    const unsigned valid = n.N1.w;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const int sh = 8 * (s & 3);
+        const unsigned nx = s < 4 ? nx0 : nx1, fx = s < 4 ? fx0 : fx1, ny = s < 4 ? ny0 : ny1, fy = s < 4 ? fy0 : fy1;
+        const unsigned nz = s < 4 ? nz0 : nz1, fz = s < 4 ? fz0 : fz1;
+        const float tnx = __builtin_fmaf((float)((nx >> sh) & 255u), sx, bx);
+        const float tny = __builtin_fmaf((float)((ny >> sh) & 255u), sy, by);
+        const float tnz = __builtin_fmaf((float)((nz >> sh) & 255u), sz, bz);
+        const float tfx = __builtin_fmaf((float)((fx >> sh) & 255u), sx, bx);
+        const float tfy = __builtin_fmaf((float)((fy >> sh) & 255u), sy, by);
+        const float tfz = __builtin_fmaf((float)((fz >> sh) & 255u), sz, bz);
+        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.f));
+        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tcut)) * 1.00000048f;
+        k[s] = (((valid >> s) & 1u) && tn <= tf) ? ((__float_as_uint(tn) & 0x7ffffff8u) | (unsigned)s) : kNoChild;
+    }
+    // Batcher's odd-even merge sort, 19 compare-exchanges
+    kswap(k[0], k[1]); kswap(k[2], k[3]); kswap(k[4], k[5]); kswap(k[6], k[7]);
+    kswap(k[0], k[2]); kswap(k[1], k[3]); kswap(k[4], k[6]); kswap(k[5], k[7]);
+    kswap(k[1], k[2]); kswap(k[5], k[6]);
+    kswap(k[0], k[4]); kswap(k[1], k[5]); kswap(k[2], k[6]); kswap(k[3], k[7]);
+    kswap(k[2], k[4]); kswap(k[3], k[5]);
+    kswap(k[1], k[2]); kswap(k[3], k[4]); kswap(k[5], k[6]);
+}
+// The child word of slot (key & 7): >= 0 an internal node, else a leaf 0x80000000 | first_tile << 4 | (count - 1)
+__device__ __forceinline__ int child_word(const BvhNode8& n, unsigned key) {
+    const unsigned s = key & 7u;
+    const unsigned imask = __float_as_uint(n.N0.w) >> 24;
+    const unsigned below = (1u << s) - 1u;
+    if ((imask >> s) & 1u) return (int)(n.N1.x + (unsigned)__popc(imask & below));
+    const unsigned cnt = (n.N1.z >> (4 * s)) & 15u;
+    unsigned m = n.N1.z & ((1u << (4 * s)) - 1u);  // s <= 7: shift <= 28
+    m = (m & 0x0f0f0f0fu) + ((m >> 4) & 0x0f0f0f0fu);
+    const unsigned first = n.N1.y + ((m * 0x01010101u) >> 24);
+    return (int)(0x80000000u | first << 4 | (cnt - 1u));
+}
+
+// The walk shared by both queries: nearest child first, the others pushed far-to-near on a per-lane LDS stack of
+// (child word, key) (an entry whose entry distance lies beyond the current cut is dropped when popped); leaves are
+// handed to `leaf(lf, lc)`, which may lower the cut and returns true to end the walk.  Returns false on a stack
+// overflow (the ray is then ambiguous).
+template <class LeafFn>
+__device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, const Bvh8Ray& r, float& cut, ctr_t& nn,
+                                          LeafFn&& leaf) {
     uint2* stk = g_bstk + threadIdx.x;
     int sp = 0;
-    float cut = tMaxInit, t2 = __builtin_inff();
-    int best = -1, second = -1;
     bool overflow = false;
     int node = 0, lf = 0, lc = 0;
     while (true) {
@@ -953,37 +1003,53 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
             if (node < 0) {
                 if (sp == 0) break;
                 const uint2 e = stk[--sp * kBlock];
-                if (__uint_as_float(e.y) > cut) continue;  // entered beyond the current cut: nothing to find there
+                if (__uint_as_float(e.y & 0x7ffffff8u) > cut) continue;  // entered beyond the current cut
                 const int w = (int)e.x;
                 if (w >= 0) node = w;
                 else decode_leaf(w, lf, lc);
                 continue;
             }
-            const BvhNode bn = load_node(nodes, node);
-            const float4 LX = bn.LX, HX = bn.HX, LY = bn.LY, HY = bn.HY, LZ = bn.LZ, HZ = bn.HZ, CW = bn.CW;
-            nn += 4;
-            float e0 = child_entry(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, inv, oi, cut);
-            float e1 = child_entry(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, inv, oi, cut);
-            float e2 = child_entry(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, inv, oi, cut);
-            float e3 = child_entry(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, inv, oi, cut);
-            int w0 = __float_as_int(CW.x), w1 = __float_as_int(CW.y), w2 = __float_as_int(CW.z), w3 = __float_as_int(CW.w);
-            e0 = w0 == -1 ? __builtin_inff() : e0;
-            e1 = w1 == -1 ? __builtin_inff() : e1;
-            e2 = w2 == -1 ? __builtin_inff() : e2;
-            e3 = w3 == -1 ? __builtin_inff() : e3;
-            cswap(e0, w0, e1, w1); cswap(e2, w2, e3, w3); cswap(e0, w0, e2, w2); cswap(e1, w1, e3, w3);
-            cswap(e1, w1, e2, w2);
+            const BvhNode8 bn = load_node8(nodes, node);
+            nn += __popc(bn.N1.w);
+            unsigned k[8];
+            node_keys(bn, r, cut, k);
             node = -1;
-            const float INF = __builtin_inff();
-            if (e3 < INF) { if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)w3, __float_as_uint(e3)); else overflow = true; }
-            if (e2 < INF) { if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)w2, __float_as_uint(e2)); else overflow = true; }
-            if (e1 < INF) { if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)w1, __float_as_uint(e1)); else overflow = true; }
-            if (e0 < INF) {
-                if (w0 >= 0) node = w0;
-                else decode_leaf(w0, lf, lc);
+#pragma unroll
+            for (int i = 7; i >= 1; --i)
+                if (k[i] != kNoChild) {
+                    if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)child_word(bn, k[i]), k[i]);
+                    else overflow = true;
+                }
+            if (k[0] != kNoChild) {
+                const int w = child_word(bn, k[0]);
+                if (w >= 0) node = w;
+                else decode_leaf(w, lf, lc);
             }
         }
         if (lc == 0) break;
+        const bool done = leaf(lf, lc);
+        lc = 0;
+        if (done) break;
+    }
+    return !overflow;
+}
+
+// closest hit over the BVH: returns the triangle id (or -1) with (b0, b1, b2, t); amb = the BFS must decide
+template <int KZ>
+__device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0,
+                                           float& rb1, float& rb2, float& rt, ctr_t& nn, ctr_t& nt, bool& amb) {
+    if (bvh_refuses(sc, o, d)) {
+        amb = true;
+        return -1;
+    }
+    const float4* __restrict__ tiles = sc.btiles[set];
+    Bvh8Ray r;
+    r.inv = bvh_inv(d);
+    r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    const TriRay R = make_triray<KZ>(o, d);
+    float cut = tMaxInit, t2 = __builtin_inff();
+    int best = -1, second = -1;
+    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, [&](int lf, int lc) {
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             const float4 A = tp[0], B = tp[1], Cc = tp[2];
@@ -1003,9 +1069,9 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
                 }
             }
         }
-        lc = 0;
-    }
-    amb = overflow || (second >= 0 && t2 <= rt + canon_window(rt, sc.wabs));
+        return false;
+    });
+    amb = !ok || (second >= 0 && t2 <= rt + canon_window(rt, sc.wabs));
     return best;
 }
 
@@ -1013,60 +1079,32 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
 template <int KZ>
 __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 d, float tMax, ctr_t& nn, ctr_t& nt,
                                           bool& amb) {
-    const float4* __restrict__ nodes = sc.bvh[set];
+    if (bvh_refuses(sc, o, d)) {
+        amb = true;
+        return -1;
+    }
     const float4* __restrict__ tiles = sc.btiles[set];
-    const V3 inv = bvh_inv(d);
-    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+    Bvh8Ray r;
+    r.inv = bvh_inv(d);
+    r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
     const TriRay R = make_triray<KZ>(o, d);
     const float sure = tMax - canon_window(tMax, sc.wabs);
-    uint2* stk = g_bstk + threadIdx.x;
-    int sp = 0;
-    bool window = false, overflow = false;
-    int node = 0, lf = 0, lc = 0;
-    while (true) {
-        while (lc == 0) {
-            if (node < 0) {
-                if (sp == 0) break;
-                const int w = (int)stk[--sp * kBlock].x;
-                if (w >= 0) node = w;
-                else decode_leaf(w, lf, lc);
-                continue;
-            }
-            const BvhNode bn = load_node(nodes, node);
-            const float4 LX = bn.LX, HX = bn.HX, LY = bn.LY, HY = bn.HY, LZ = bn.LZ, HZ = bn.HZ, CW = bn.CW;
-            nn += 4;
-            const int w[4] = {__float_as_int(CW.x), __float_as_int(CW.y), __float_as_int(CW.z), __float_as_int(CW.w)};
-            const bool h[4] = {w[0] != -1 && child_entry(LX.x, HX.x, LY.x, HY.x, LZ.x, HZ.x, inv, oi, tMax) < __builtin_inff(),
-                               w[1] != -1 && child_entry(LX.y, HX.y, LY.y, HY.y, LZ.y, HZ.y, inv, oi, tMax) < __builtin_inff(),
-                               w[2] != -1 && child_entry(LX.z, HX.z, LY.z, HY.z, LZ.z, HZ.z, inv, oi, tMax) < __builtin_inff(),
-                               w[3] != -1 && child_entry(LX.w, HX.w, LY.w, HY.w, LZ.w, HZ.w, inv, oi, tMax) < __builtin_inff()};
-            node = -1;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!h[k]) continue;
-                if (node < 0 && lc == 0) {  // the first passing child is opened next, the others wait
-                    if (w[k] >= 0) node = w[k];
-                    else decode_leaf(w[k], lf, lc);
-                } else if (sp < kBvhStack) {
-                    stk[sp++ * kBlock] = make_uint2((unsigned)w[k], 0u);
-                } else {
-                    overflow = true;
-                }
-            }
-        }
-        if (lc == 0) break;
+    bool window = false, occluded = false;
+    float cut = tMax;
+    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, [&](int lf, int lc) {
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             ++nt;
             float b0, b1, b2, t;
             if (tri_intersect<KZ>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax) {
-                if (t < sure) { amb = false; return 0; }
+                if (t < sure) { occluded = true; return true; }
                 window = true;
             }
         }
-        lc = 0;
-    }
-    amb = window || overflow;
+        return false;
+    });
+    if (occluded) { amb = false; return 0; }
+    amb = window || !ok;
     return -1;
 }
 
@@ -1077,9 +1115,6 @@ __device__ __forceinline__ int traverse_kz(const DevScene& sc, int set, V3 o, V3
         bool amb = false;
         const int r = ANYHIT ? bvh_anyhit<KZ>(sc, set, o, d, tMax, nn, nt, amb)
                              : bvh_closest<KZ>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, amb);
-#ifdef RT_TIMING_NO_FALLBACK
-        return r;  // timing experiment only: wrong on ambiguous rays
-#endif
         if (!amb) return r;
         ++nfb;  // ambiguous (rare): the reference BFS decides, with the wave's other lanes done with the BVH
     }

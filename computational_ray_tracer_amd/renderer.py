@@ -103,6 +103,11 @@ class Renderer:
         return dict(bounds=b, child=ch, leaf_first=lf, leaf_count=lc, refs=refs[:r], depth=info.depth,
                     max_queue_groups=info.max_queue_groups)
 
+    def bvh(self, tile_set=0):
+        """The fast traversal's BVH as uploaded (rt_bvh_export): nodes (n, 32) f32, tiles (m, 12) f32, consts."""
+        return _bvh_arrays(lambda nn, nt, cs, nd, tl: self.lib.rt_bvh_export(self.h, tile_set, nn, nt, cs, nd, tl),
+                           lambda rc: self._chk("rt_bvh_export", rc))
+
     def trace(self, ro, rd, use_cull=True):
         ro = np.ascontiguousarray(ro, np.float32)
         rd = np.ascontiguousarray(rd, np.float32)
@@ -151,3 +156,26 @@ def records_to_arrays(recs):
     return dict(lam=raw[:, 0:8], pdf=raw[:, 8:16], ro=raw[:, 16:19], rd=raw[:, 19:22],
                 prim=raw[:, 22].view(np.int32), b=raw[:, 23:26], t=raw[:, 26], L=raw[:, 27:35], rgb=raw[:, 35:38],
                 weight=raw[:, 38])
+
+
+def _bvh_arrays(call, check):
+    P = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
+    nn, nt = C.c_int(), C.c_int()
+    cs = np.zeros(2, np.float32)
+    check(call(C.byref(nn), C.byref(nt), P(cs), None, None))
+    nodes = np.zeros((max(nn.value, 1), 32), np.float32)
+    tiles = np.zeros((max(nt.value, 1), 12), np.float32)
+    check(call(C.byref(nn), C.byref(nt), P(cs), P(nodes), P(tiles)))
+    return dict(nodes=nodes[: nn.value], tiles=tiles[: nt.value], consts=cs)
+
+
+def build_bvh_host(model, tile_set=0):
+    """rt_debug_bvh_build: the upload's BVH built on the host from a scene.Model, without a device (CPU tests)."""
+    lib = capi.load_library()
+    sd = model.desc()
+
+    def check(rc):
+        if rc != capi.RT_OK:
+            raise capi.RTError("rt_debug_bvh_build", rc, "bad scene")
+    return _bvh_arrays(lambda nn, nt, cs, nd, tl: lib.rt_debug_bvh_build(C.byref(sd), tile_set, nn, nt, cs, nd, tl),
+                       check)

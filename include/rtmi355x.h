@@ -307,6 +307,14 @@ int rt_octree_get_info(rt_ctx* ctx, rt_octree_info* out);
  * node_leaf_first[n], node_leaf_count[n], leaf_refs[n_leaf_refs] (triangle ids incl. culled ones). */
 int rt_octree_export(rt_ctx* ctx, float* node_bounds, int32_t* node_child, int32_t* node_leaf_first,
                      int32_t* node_leaf_count, int32_t* leaf_refs);
+/* The fast multi-level traversal's 8-wide compressed BVH as uploaded for tile set `set` (0 all triangles, 1 without
+ * back faces), DESIGN.md §6b: *n_nodes nodes of 32 floats (128 B, layout in rt_bvh.cpp), *n_tiles triangle tiles of
+ * 12 floats, consts[2] = (wabs, oguard) of the canonical rule.  Counts always; arrays when non-NULL.  Not a
+ * reference structure (the reference traverses only its octree): exported so tests can replay the GPU's walk. */
+int rt_bvh_export(rt_ctx* ctx, int set, int* n_nodes, int* n_tiles, float* consts, float* nodes, float* tiles);
+/* The same BVH built on the host from a scene descriptor, without a context or a device (CPU tests). */
+int rt_debug_bvh_build(const rt_scene_desc* scene, int set, int* n_nodes, int* n_tiles, float* consts, float* nodes,
+                       float* tiles);
 
 /* ---- parity entry points (same kernels as the hot path, stage outputs exposed) ------------------ */
 /* K2 alone: closest hit of n world-space rays (ro, rd: 3n floats).  prim[n] (-1 = miss),

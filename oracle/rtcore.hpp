@@ -1069,6 +1069,176 @@ struct Octree {
     }
 };
 
+// ---- The GPU's fast multi-level walk restated (rt_kernels.hip bvh8_walk / bvh_closest / bvh_anyhit, DESIGN.md
+// §6b).  NOT the reference's algorithm and not the product's code: a CPU restatement, operation for operation
+// (std::fma where the kernel calls fma, the same IEEE min / max order, the same 19-comparator sorting network and
+// push order), over the BVH the product builds (exported through rt_bvh_export / rt_debug_bvh_build: 32 floats per
+// node, 12 per tile).  With it a CPU test checks, on millions of rays, that the canonical rule over THIS BVH returns
+// what Octree::Traverse / Occluded return, and a GPU test checks the device walk against it ray by ray.
+struct Bvh8 {
+    const float* nodes = nullptr;   // 32 floats per node (rt_bvh.cpp layout)
+    const float* tiles = nullptr;   // 12 floats per tile: (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0)
+    int n_nodes = 0, n_tiles = 0;
+    float wabs = 0, oguard = 0;
+    int stack_cap = 16;             // kBvhStack
+    static constexpr unsigned kNo = 0xffffffffu;
+    struct Stats { int64_t nodes = 0, boxes = 0, tris = 0; int max_sp = 0; };
+    struct Result { int tri = -1; TriIsect isect{}; bool amb = false; int occluded = 0; };
+
+    static uint32_t U(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+    static float F(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+    const float* N(int i) const { return nodes + 32 * (size_t)i; }
+    static float ClampInv(float d) { return 1 / std::copysign(std::max(std::fabs(d), 0x1p-80f), d); }
+
+    void Keys(int node, const vec3& inv, const vec3& oi, float tcut, unsigned k[8]) const {
+        const float* n = N(node);
+        const uint32_t w0 = U(n[3]);
+        const float s[3] = {std::ldexp(inv.x, (int)(w0 & 255u) - 127), std::ldexp(inv.y, (int)((w0 >> 8) & 255u) - 127),
+                            std::ldexp(inv.z, (int)((w0 >> 16) & 255u) - 127)};
+        const float b[3] = {std::fma(n[0], inv.x, -oi.x), std::fma(n[1], inv.y, -oi.y), std::fma(n[2], inv.z, -oi.z)};
+        const float iv[3] = {inv.x, inv.y, inv.z};
+        const uint32_t valid = U(n[7]);
+        for (int sl = 0; sl < 8; ++sl) {
+            float tnear[3], tfar[3];
+            for (int a = 0; a < 3; ++a) {
+                const float* q = n + 8 + 4 * a;  // lo bytes (words 0, 1), hi bytes (words 2, 3)
+                const uint32_t lo = (U(q[sl >> 2]) >> (8 * (sl & 3))) & 255u, hi = (U(q[2 + (sl >> 2)]) >> (8 * (sl & 3))) & 255u;
+                const bool pos = iv[a] >= 0.f;
+                tnear[a] = std::fma((float)(pos ? lo : hi), s[a], b[a]);
+                tfar[a] = std::fma((float)(pos ? hi : lo), s[a], b[a]);
+            }
+            const float tn = std::fmax(std::fmax(tnear[0], tnear[1]), std::fmax(tnear[2], 0.f));
+            const float tf = std::fmin(std::fmin(tfar[0], tfar[1]), std::fmin(tfar[2], tcut)) * 1.00000048f;
+            k[sl] = (((valid >> sl) & 1u) && tn <= tf) ? ((U(tn) & 0x7ffffff8u) | (unsigned)sl) : kNo;
+        }
+        auto sw = [&](int i, int j) { if (k[j] < k[i]) std::swap(k[i], k[j]); };
+        sw(0, 1); sw(2, 3); sw(4, 5); sw(6, 7);
+        sw(0, 2); sw(1, 3); sw(4, 6); sw(5, 7);
+        sw(1, 2); sw(5, 6);
+        sw(0, 4); sw(1, 5); sw(2, 6); sw(3, 7);
+        sw(2, 4); sw(3, 5);
+        sw(1, 2); sw(3, 4); sw(5, 6);
+    }
+    int Word(int node, unsigned key) const {
+        const float* n = N(node);
+        const unsigned s = key & 7u, imask = U(n[3]) >> 24;
+        if ((imask >> s) & 1u) return (int)(U(n[4]) + (unsigned)__builtin_popcount(imask & ((1u << s) - 1u)));
+        const unsigned counts = U(n[6]), cnt = (counts >> (4 * s)) & 15u;
+        unsigned first = U(n[5]);
+        for (unsigned j = 0; j < s; ++j) first += (counts >> (4 * j)) & 15u;
+        return (int)(0x80000000u | first << 4 | (cnt - 1u));
+    }
+    // the walk; leaf(first, count) returns true to stop; false on a stack overflow
+    template <class Leaf>
+    bool Walk(const Ray& ray, float& cut, Stats& st, Leaf&& leaf) const {
+        const vec3 inv = {ClampInv(ray.d.x), ClampInv(ray.d.y), ClampInv(ray.d.z)};
+        const vec3 oi = {ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z};
+        std::vector<std::pair<int, unsigned>> stk;
+        bool overflow = false;
+        int node = 0;
+        while (true) {
+            int lf = 0, lc = 0;
+            while (lc == 0) {
+                if (node < 0) {
+                    if (stk.empty()) break;
+                    auto e = stk.back();
+                    stk.pop_back();
+                    if (F(e.second & 0x7ffffff8u) > cut) continue;
+                    if (e.first >= 0) node = e.first;
+                    else { lf = (e.first >> 4) & 0x7ffffff; lc = (e.first & 15) + 1; }
+                    continue;
+                }
+                ++st.nodes;
+                st.boxes += __builtin_popcount(U(N(node)[7]));
+                unsigned k[8];
+                Keys(node, inv, oi, cut, k);
+                const int cur = node;
+                node = -1;
+                for (int i = 7; i >= 1; --i)
+                    if (k[i] != kNo) {
+                        if ((int)stk.size() < stack_cap) stk.emplace_back(Word(cur, k[i]), k[i]);
+                        else overflow = true;
+                    }
+                st.max_sp = std::max(st.max_sp, (int)stk.size());
+                if (k[0] != kNo) {
+                    const int w = Word(cur, k[0]);
+                    if (w >= 0) node = w;
+                    else { lf = (w >> 4) & 0x7ffffff; lc = (w & 15) + 1; }
+                }
+            }
+            if (lc == 0) break;
+            if (leaf(lf, lc)) break;
+        }
+        return !overflow;
+    }
+    void Tri(int i, vec3& p0, vec3& p1, vec3& p2, int& id) const {
+        const float* q = tiles + 12 * (size_t)i;
+        p0 = {q[0], q[1], q[2]}; p1 = {q[3], q[4], q[5]}; p2 = {q[6], q[7], q[8]};
+        id = (int)U(q[9]);
+    }
+    bool Guarded(const Ray& r) const {
+        return std::fmax(std::fmax(std::fabs(r.o.x), std::fabs(r.o.y)), std::fabs(r.o.z)) <= oguard;
+    }
+    // bvh_closest: the canonical closest hit (amb: the BFS decides)
+    Result Closest(const Ray& ray, Stats& st) const {
+        Result res;
+        if (!Guarded(ray)) { res.amb = true; return res; }
+        float cut = std::numeric_limits<float>::max(), t2 = std::numeric_limits<float>::infinity();
+        int best = -1, second = -1;
+        const bool ok = Walk(ray, cut, st, [&](int lf, int lc) {
+            for (int k = 0; k < lc; ++k) {
+                vec3 p0, p1, p2;
+                int id;
+                Tri(lf + k, p0, p1, p2, id);
+                ++st.tris;
+                TriIsect is;
+                if (BasicIntersect(p0, p1, p2, ray, cut, &is) && is.t < cut) {
+                    if (best < 0 || is.t < res.isect.t) {
+                        t2 = best < 0 ? t2 : res.isect.t;
+                        second = best;
+                        best = id;
+                        res.isect = is;
+                        const float c2 = is.t + 2.f * Octree::Window(is.t, wabs);
+                        cut = c2 < cut ? c2 : cut;
+                    } else if (is.t < t2) {
+                        second = id;
+                        t2 = is.t;
+                    }
+                }
+            }
+            return false;
+        });
+        res.tri = best;
+        res.amb = !ok || (second >= 0 && t2 <= res.isect.t + Octree::Window(res.isect.t, wabs));
+        return res;
+    }
+    // bvh_anyhit: occluded = 1 / 0 (amb: the BFS decides)
+    Result AnyHit(const Ray& ray, float tMax, Stats& st) const {
+        Result res;
+        if (!Guarded(ray)) { res.amb = true; return res; }
+        const float sure = tMax - Octree::Window(tMax, wabs);
+        bool window = false, occ = false;
+        float cut = tMax;
+        const bool ok = Walk(ray, cut, st, [&](int lf, int lc) {
+            for (int k = 0; k < lc; ++k) {
+                vec3 p0, p1, p2;
+                int id;
+                Tri(lf + k, p0, p1, p2, id);
+                ++st.tris;
+                TriIsect is;
+                if (BasicIntersect(p0, p1, p2, ray, tMax, &is) && is.t < tMax) {
+                    if (is.t < sure) { occ = true; return true; }
+                    window = true;
+                }
+            }
+            return false;
+        });
+        res.occluded = occ ? 1 : 0;
+        res.amb = !occ && (window || !ok);
+        return res;
+    }
+};
+
 // ------------------------------------------------------------------------------- camera
 // Cameras.h:273-297 PerspectiveCamera::generateRay; matrices are the values CameraBase holds
 struct Camera {

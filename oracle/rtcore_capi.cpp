@@ -464,6 +464,110 @@ int orc_canonical_check(void* h, int n, const float* ro, const float* rd, const 
     return 0;
 }
 
+// The GPU's walk over the product's exported 8-wide BVH (Bvh8) against the reference BFS: for every
+// ray the canonical closest hit (the BFS when ambiguous) against Traverse, and the canonical any hit against Occluded
+// with tMax = tmax[i].  stats[16]: closest mismatches, closest ambiguous, any-hit mismatches, any-hit ambiguous,
+// closest hits, occluded, rays, first mismatching ray (or -1), closest node visits, box tests, triangle tests, max
+// stack depth, any-hit node visits, box tests, triangle tests, stack overflows.
+static Bvh8 MakeBvh8(const float* nodes, int n_nodes, const float* tiles, int n_tiles, const float* consts) {
+    Bvh8 b;
+    b.nodes = nodes; b.n_nodes = n_nodes; b.tiles = tiles; b.n_tiles = n_tiles;
+    b.wabs = consts[0]; b.oguard = consts[1];
+    return b;
+}
+// The any-hit queries walk tile set 0's BVH (nodes_a / tiles_a: the path kernels' shadow rays never cull), the
+// closest-hit queries the BVH of the tile set use_cull selects.
+int orc_bvh_check(void* h, const float* nodes, int n_nodes, const float* tiles, int n_tiles, const float* nodes_a,
+                  int n_nodes_a, const float* tiles_a, int n_tiles_a, const float* consts, int n, const float* ro,
+                  const float* rd, const float* tmax, int use_cull, int nthreads, int64_t* stats) {
+    const Octree& T = static_cast<OracleScene*>(h)->S.octree;
+    const Bvh8 B = MakeBvh8(nodes, n_nodes, tiles, n_tiles, consts);
+    const Bvh8 BA = MakeBvh8(nodes_a, n_nodes_a, tiles_a, n_tiles_a, consts);
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::array<int64_t, 16>> part(nthreads);
+    std::vector<std::thread> pool;
+    for (int th = 0; th < nthreads; ++th)
+        pool.emplace_back([&, th] {
+            std::array<int64_t, 16>& st = part[th];
+            st.fill(0);
+            st[7] = -1;
+            const int i0 = (int)((int64_t)n * th / nthreads), i1 = (int)((int64_t)n * (th + 1) / nthreads);
+            for (int i = i0; i < i1; ++i) {
+                Ray r{{ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]}, {rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]}};
+                Octree::Hit b = T.Traverse(r, use_cull != 0);
+                Bvh8::Stats sc, sa;
+                Bvh8::Result c = B.Closest(r, sc);
+                bool same = true;
+                if (c.amb) ++st[1];
+                else same = c.tri == b.tri && (c.tri < 0 || std::memcmp(&c.isect, &b.isect, sizeof(TriIsect)) == 0);
+                if (!same) { ++st[0]; if (st[7] < 0) st[7] = i; }
+                st[4] += b.tri >= 0;
+                const bool occ = T.Occluded(r, tmax[i]);
+                Bvh8::Result a = BA.AnyHit(r, tmax[i], sa);
+                if (a.amb) ++st[3];
+                else if ((a.occluded == 1) != occ) { ++st[2]; if (st[7] < 0) st[7] = i; }
+                st[5] += occ;
+                ++st[6];
+                st[8] += sc.nodes; st[9] += sc.boxes; st[10] += sc.tris;
+                st[11] = std::max<int64_t>(st[11], std::max(sc.max_sp, sa.max_sp));
+                st[12] += sa.nodes; st[13] += sa.boxes; st[14] += sa.tris;
+                st[15] += (sc.max_sp >= B.stack_cap) + (sa.max_sp >= B.stack_cap);
+            }
+        });
+    for (auto& t : pool) t.join();
+    for (int k = 0; k < 16; ++k) stats[k] = 0;
+    stats[7] = -1;
+    for (auto& st : part) {
+        for (int k = 0; k < 16; ++k)
+            if (k == 11) stats[k] = std::max(stats[k], st[k]);
+            else if (k != 7) stats[k] += st[k];
+        if (stats[7] < 0 && st[7] >= 0) stats[7] = st[7];
+    }
+    return 0;
+}
+
+// What the GPU returns for each ray over the same BVH: the canonical closest hit / any hit, or — for an ambiguous
+// ray — the reference BFS's (Traverse / Occluded).  prim[n] (-1 miss), bt[4n] (0 on a miss), occluded[n], amb[n]
+// (bit 0 closest ambiguous, bit 1 any-hit ambiguous).
+int orc_bvh_query(void* h, const float* nodes, int n_nodes, const float* tiles, int n_tiles, const float* nodes_a,
+                  int n_nodes_a, const float* tiles_a, int n_tiles_a, const float* consts, int n, const float* ro,
+                  const float* rd, const float* tmax, int use_cull, int nthreads, int* prim, float* bt, int* occluded,
+                  int* amb) {
+    const Octree& T = static_cast<OracleScene*>(h)->S.octree;
+    const Bvh8 B = MakeBvh8(nodes, n_nodes, tiles, n_tiles, consts);
+    const Bvh8 BA = MakeBvh8(nodes_a, n_nodes_a, tiles_a, n_tiles_a, consts);
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> pool;
+    for (int th = 0; th < nthreads; ++th)
+        pool.emplace_back([&, th] {
+            const int i0 = (int)((int64_t)n * th / nthreads), i1 = (int)((int64_t)n * (th + 1) / nthreads);
+            for (int i = i0; i < i1; ++i) {
+                Ray r{{ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]}, {rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]}};
+                Bvh8::Stats st;
+                Bvh8::Result c = B.Closest(r, st);
+                int tri = c.tri;
+                TriIsect is = c.isect;
+                if (c.amb) {
+                    Octree::Hit b = T.Traverse(r, use_cull != 0);
+                    tri = b.tri;
+                    is = b.isect;
+                }
+                prim[i] = tri;
+                if (tri >= 0) { bt[4 * i] = is.b0; bt[4 * i + 1] = is.b1; bt[4 * i + 2] = is.b2; bt[4 * i + 3] = is.t; }
+                else bt[4 * i] = bt[4 * i + 1] = bt[4 * i + 2] = bt[4 * i + 3] = 0.f;
+                int a = c.amb ? 1 : 0;
+                if (tmax) {
+                    Bvh8::Result o = BA.AnyHit(r, tmax[i], st);
+                    occluded[i] = o.amb ? (T.Occluded(r, tmax[i]) ? 1 : 0) : o.occluded;
+                    a |= o.amb ? 2 : 0;
+                }
+                amb[i] = a;
+            }
+        });
+    for (auto& t : pool) t.join();
+    return 0;
+}
+
 // RGBToSpectrumTable::operator() over n colours (rgb[3 n] -> out[3 n]) with the given table
 int orc_rgb_table_lookup(const float* znodes, const float* coeffs, int res, int n, const float* rgb, float* out) {
     for (int i = 0; i < n; ++i) {

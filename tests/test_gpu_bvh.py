@@ -1,0 +1,131 @@
+"""GPU parity of the fast multi-level traversal itself, beyond films.
+
+The canonical rule is pinned against the reference BFS on >= 10 M CPU rays (tests/test_canonical_traversal.py) over
+the BVH the product builds on the host.  Here the device side is checked against that:
+  * the BVH the context uploads (rt_bvh_export) is the host build (rt_debug_bvh_build), bit for bit;
+  * >= 2 M rays per mesh (CFG3, the CFG4 mesh) through the device walk (rt_debug_trace / rt_debug_occluded) equal
+    the oracle's restated walk (Bvh8, the reference BFS for ambiguous rays) in triangle id, (b0, b1, b2, t) bits and
+    occlusion: camera-like, random-in-the-box, axis-aligned, bounce and shadow families, any-hit tMax at the hit
+    distance x {0.5, 0.999, 1, 1.001, 2} (the window's edges) and the shadow rays' 0.999 x light distance;
+  * RTMI_FORCE_AMB declares a quarter of all rays ambiguous, so every fallback path (the BFS after the trace
+    kernel's BVH loop, the deferred shadow queue of the simple path, k_path_nee<Q, true> of mixed scenes) runs on
+    many rays: the fallback counters are non-zero and the films stay bit-exact.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from computational_ray_tracer_amd import capi, scene
+from computational_ray_tracer_amd.renderer import Renderer, build_bvh_host
+from test_canonical_traversal import _rays, _unit, _world_tris
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _mesh_cfg(which):
+    if which == "cfg3":
+        return scene.cfg3_blob(res=(64, 36), spp_side=2)
+    cfg = scene.cfg4_mixed(res=(64, 36), spp=(2, 2))
+    cfg.model = copy.deepcopy(cfg.model)
+    cfg.model.shapes = []   # the mesh walk alone (rt_debug_trace would add the analytic shapes after it)
+    cfg.model.lights = [l for l in cfg.model.lights if l.get("type", capi.RT_LIGHT_QUAD) == capi.RT_LIGHT_QUAD]
+    return cfg
+
+
+@pytest.mark.parametrize("which", ["cfg3", "cfg4", "cfg0"])
+def test_uploaded_bvh_equals_host_build(oracle_lib, which):
+    cfg = scene.cfg0_reference(res=(32, 32), n_index=1) if which == "cfg0" else _mesh_cfg(which)
+    g = Renderer(cfg)
+    for st in ((0, 1) if which == "cfg0" else (0,)):
+        a, b = g.bvh(st), build_bvh_host(cfg.model, st)
+        assert len(a["nodes"]) > 100 and len(a["tiles"]) > 1000
+        for k in ("nodes", "tiles", "consts"):
+            assert np.array_equal(bits(a[k]), bits(b[k])), (st, k)
+
+
+def _secondary(rng, ro, rd, prim, bt, tris, light):
+    h = (prim >= 0) & (prim < len(tris))
+    ro, rd, prim, t = ro[h].astype(np.float64), rd[h].astype(np.float64), prim[h], bt[h, 3].astype(np.float64)
+    tri = tris[prim]
+    p = ro + rd * t[:, None]
+    ng = _unit(np.cross(tri[:, 0] - tri[:, 2], tri[:, 1] - tri[:, 2]))
+    ng = np.where((np.sum(ng * rd, 1) > 0)[:, None], -ng, ng)
+    off = 1e-4 * (1 + np.abs(p).max(1))
+    po = (p + ng * off[:, None]).astype(np.float32)
+    wi = _unit(ng + _unit(rng.normal(size=ng.shape)) * 0.999).astype(np.float32)
+    lp = np.asarray(light["p"]) + rng.uniform(size=(len(p), 1)) * np.asarray(light["e1"]) + \
+        rng.uniform(size=(len(p), 1)) * np.asarray(light["e2"])
+    wv = lp - po
+    dist = np.linalg.norm(wv, axis=1)
+    return po, wi, (wv / dist[:, None]).astype(np.float32), (dist * 0.999).astype(np.float32)
+
+
+@pytest.mark.parametrize("which", ["cfg3", "cfg4"])
+def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, which):
+    cfg = _mesh_cfg(which)
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    bvh = g.bvh(0)
+    tris = _world_tris(cfg.model)
+    light = cfg.model.lights[0]
+    rng = np.random.default_rng({"cfg3": 301, "cfg4": 401}[which])
+    total, chunk, done, amb = 2_000_000, 400_000, 0, 0
+    g.reset_stats()
+    while done < total:
+        ro, rd = _rays(rng, chunk // 2, light, tris)
+        pg, bg = g.trace(ro, rd, False)
+        t = np.where(pg >= 0, bg[:, 3], 400.0)
+        tmax = (t * rng.choice([0.5, 0.999, 1.0, 1.001, 2.0], size=len(t))).astype(np.float32)
+        og = g.occluded(ro, rd, tmax)
+        po, bo, oo, ao = o.bvh_query(bvh, ro, rd, tmax)
+        assert np.array_equal(pg, po), np.flatnonzero(pg != po)[:5]
+        assert np.array_equal(bits(bg), bits(bo))
+        assert np.array_equal(og, oo)
+        amb += int((ao != 0).sum())
+        done += len(ro)
+        # bounce rays (closest hit + any hit to the light distance) and shadow rays from the device's hits
+        s_o, s_wi, s_ws, s_max = _secondary(rng, ro, rd, pg, bg, tris, light)
+        m = min(len(s_o), (chunk - len(ro)) // 2)
+        for d in (s_wi[:m], s_ws[:m]):
+            pg2, bg2 = g.trace(s_o[:m], d, False)
+            og2 = g.occluded(s_o[:m], d, s_max[:m])
+            po2, bo2, oo2, ao2 = o.bvh_query(bvh, s_o[:m], d, s_max[:m])
+            assert np.array_equal(pg2, po2)
+            assert np.array_equal(bits(bg2), bits(bo2))
+            assert np.array_equal(og2, oo2)
+            amb += int((ao2 != 0).sum())
+            done += m
+    st = g.stats()
+    assert done >= total
+    assert st["rays"] >= total and st["shadow_rays"] >= total
+    assert amb < 1e-2 * done
+    # executed work per ray: the 8-wide nodes keep it far below the reference BFS's (CFG3: 67.7 boxes, 63.7 tris)
+    assert st["nodes_tested"] / st["rays"] < 60 and st["tris_tested"] / st["rays"] < 16, st
+
+
+@pytest.mark.parametrize("kind", ["cfg3_path", "cfg3_shadowq", "cfg4_mis", "cfg4_path"])
+def test_forced_fallback_paths_film_bitexact(oracle_lib, monkeypatch, kind):
+    """A quarter of all BVH queries forced ambiguous (RTMI_FORCE_AMB=2): the exact fallbacks carry them and the
+    film is bit-exact against the oracle, with the fallback counters far above their natural rate."""
+    monkeypatch.setenv("RTMI_FORCE_AMB", "2")
+    if kind.startswith("cfg3"):
+        if kind == "cfg3_shadowq":
+            monkeypatch.setenv("RTMI_SHADOW_QUEUE", "1")
+        cfg = scene.cfg3_blob(res=(48, 27), spp_side=2, max_depth=4)
+    else:
+        cfg = scene.cfg4_mixed(res=(48, 27), spp=(2, 2), frequency=16)
+        cfg.integrator = scene.Integrator(capi.RT_INTEGRATOR_PATH_MIS if kind == "cfg4_mis" else capi.RT_INTEGRATOR_PATH,
+                                          max_depth=4)
+    g = Renderer(cfg)
+    g.reset_stats()
+    fg = g.render_pass(0, 4)
+    fo = oracle_lib.OracleScene(cfg).render(0, 4)
+    bad = np.any(bits(fg) != bits(fo), axis=1)
+    assert bad.sum() == 0, f"{bad.sum()} pixels differ"
+    st = g.stats()
+    assert st["fallback_rays"] > 0.1 * st["rays"], st
+    assert st["shadow_fallback_rays"] > 0.1 * st["shadow_rays"], st
