@@ -441,8 +441,9 @@ struct Work {
     float4 *sO = nullptr, *sD = nullptr;
     int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
-    void* sTemp = nullptr;
-    size_t sTempBytes = 0, sCap = 0;
+    unsigned* sQKey = nullptr;  // the ray queue's sort keys at queue positions (written by the shade kernels)
+    void* sTemp = nullptr;      // the sorts' histograms and meta (sort_temp_bytes)
+    size_t sCap = 0;
     // shadow queue (multi-level octrees): {o, tMax}, {d, slot}, pending contribution (2 x float4)
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
     size_t shCap = 0;
@@ -610,14 +611,14 @@ int ensure_shadow_workspace(rt_ctx* c, Work& w, size_t n) {
 }
 
 void free_sort_workspace(Work& w) {
-    void* ptrs[] = {w.sO, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sTemp};  // (sD = sO + 1)
+    void* ptrs[] = {w.sO, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sQKey, w.sTemp};  // (sD = sO + 1)
     for (void* p : ptrs)
         if (p) hipFree(p);
     w.sO = w.sD = nullptr;
     w.sS = w.sVals = w.sValsAlt = nullptr;
-    w.sKeys = w.sKeysAlt = nullptr;
+    w.sKeys = w.sKeysAlt = w.sQKey = nullptr;
     w.sTemp = nullptr;
-    w.sTempBytes = w.sCap = 0;
+    w.sCap = 0;
 }
 
 int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
@@ -626,9 +627,8 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
     // the side queue's rays as interleaved (o, d) pairs like the queues' (sD = sO + 1)
     HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1; HIPCHK(c, dalloc(&w.sS, n));
     HIPCHK(c, dalloc(&w.sVals, n)); HIPCHK(c, dalloc(&w.sValsAlt, n));
-    HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n));
-    w.sTempBytes = sort_rays_temp_bytes((int)n);
-    HIPCHK(c, hipMalloc(&w.sTemp, std::max<size_t>(w.sTempBytes, 16)));
+    HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n)); HIPCHK(c, dalloc(&w.sQKey, n));
+    HIPCHK(c, hipMalloc(&w.sTemp, sort_temp_bytes()));
     w.sCap = n;
     return RT_OK;
 }
@@ -1150,18 +1150,11 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 // padded keys instead, without the host read: -0.6 %); the other lane keeps the GPU busy meanwhile.
                 const QueueView qv = depth == 0 ? QueueView{nullptr, Sq[l], nSq[l], nsh}
                                                 : QueueView{qc_cur + kQLen, Sq[l], 0, nsh};
-                if (sort_rays && depth > 0) {
-                    SortRaysIO so{cO, cD, cS, w.sO, w.sD, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt,
-                                  w.sTemp, w.sTempBytes, c->sort_lo, c->sort_scale, c->sort_dir_bits, c->sort_org_bits,
-                                  c->sort_org_major >= 0 ? c->sort_org_major : (c->dsc.full ? 0 : 1),
-                                  qc_cur + kQLen, Sq[l]};
-                    int lens[kShards * kQStride];
-                    HIPCHK(c, hipMemcpyAsync(lens, qc_cur + kQLen, sizeof(lens), hipMemcpyDeviceToHost, s));
-                    HIPCHK(c, hipStreamSynchronize(s));
-                    int nq = 0;
-                    for (int j = 0; j < kShards; ++j) nq += lens[j * kQStride];
+                if (sort_rays && depth > 0) {  // the device reads the queue length itself: no host round trip
+                    SortRaysIO so{w.sQKey, cO, w.sO, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
+                                  c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l]};
                     e0 = ev_start(c, s);
-                    HIPCHK(c, launch_sort_rays(s, nq, so));
+                    HIPCHK(c, launch_sort_rays(s, so));
                     ev_mark(c, s, ST_SORT, e0);
                     cO = w.sO; cD = w.sD; cS = w.sS;
                 }
@@ -1184,6 +1177,14 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     for (int d = 0; d < depth; ++d) pio.dim = dim_get2d(smp, dim_get2d(smp, pio.dim));
                 }
                 pio.ticket = dyn ? qc_cur + kQShadeTicket : nullptr;
+                if (sort_rays && depth < c->integ.max_depth) {  // keys of the rays this shade appends (next sort)
+                    pio.nkey.key = w.sQKey;
+                    pio.nkey.lo = c->sort_lo;
+                    pio.nkey.scale = c->sort_scale;
+                    pio.nkey.dir_bits = c->sort_dir_bits;
+                    pio.nkey.org_bits = c->sort_org_bits;
+                    pio.nkey.org_major = c->sort_org_major >= 0 ? c->sort_org_major : (c->dsc.full ? 0 : 1);
+                }
                 ShadowQueueIO sqio{};
                 if (shq) {  // this queue's region holds the shadow-queue length and ticket (zeroed with it)
                     sqio.shO = w.shO; sqio.shD = w.shD; sqio.shLA = w.shLA; sqio.shLB = w.shLB;
@@ -1201,16 +1202,11 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio, nio));
                 ev_mark(c, s, ST_SHADE, e0);
-                if (sort_nee) {  // NEE vertices in Morton order of their shading points
-                    int lens[kShards * kQStride];
-                    HIPCHK(c, hipMemcpyAsync(lens, qc_cur + kQShadowLen, sizeof(lens), hipMemcpyDeviceToHost, s));
-                    HIPCHK(c, hipStreamSynchronize(s));
-                    int nq = 0;
-                    for (int j = 0; j < kShards; ++j) nq += lens[j * kQStride];
+                if (sort_nee) {  // NEE vertices in Morton order of their shading points (no host round trip)
                     SortNeeIO so{w.neeSlot, qc_cur + kQShadowLen, Sq[l], nee_key, w.sKeys, w.sKeysAlt, w.sVals,
-                                 w.sValsAlt, w.sTemp, w.sTempBytes, c->sort_nee_bits};
+                                 w.sValsAlt, w.sTemp, c->sort_nee_bits};
                     e0 = ev_start(c, s);
-                    HIPCHK(c, launch_sort_nee(s, nq, so));
+                    HIPCHK(c, launch_sort_nee(s, so));
                     ev_mark(c, s, ST_SORT, e0);
                 }
                 if (nee) {  // this bounce's shadow rays, before the next bounce reads L

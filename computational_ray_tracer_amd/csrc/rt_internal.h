@@ -258,6 +258,12 @@ struct ShadeRefIO {
     int rsh;  // ray k at rayD[k << rsh]
 };
 
+// Coherence-sort key parameters of the bounce rays a shade kernel appends (ray_sort_key below).
+struct RayKeyIO {
+    unsigned* key = nullptr;  // per next-queue position; nullptr: no sort
+    float4 lo, scale;         // origin quantisation: (p - lo) * scale in [0, 512)
+    int dir_bits = 0, org_bits = 0, org_major = 0;
+};
 struct PathIO {
     // queue rays are interleaved (o, d) pairs, 32 B per ray: ray k at rayO[2k] / rayD[2k] (rayD = rayO + 1), nO / nD too
     const float4* rayO; const float4* rayD; const int* slot; QueueView q;       // current queue
@@ -270,6 +276,7 @@ struct PathIO {
     int dim;    // >= 0: the sampler dimension every path of this depth starts from (simple path: each bounce takes
                 // two Get2D); -1: per slot in R_MISC
     int* ticket;  // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
+    RayKeyIO nkey;  // multi-level scenes: the coherence-sort key of every appended ray (rt_sort.hip)
 };
 
 // Shadow queue (multi-level octrees): the shade kernel appends NEE shadow rays {o, tMax}, {d, slot} and their
@@ -324,6 +331,19 @@ __device__ __forceinline__ unsigned morton_key(float x, float y, float z, float4
            spread3_9(q((z - lo.z) * scale.z) >> (9 - bits));
 }
 
+// Coherence-sort key of a bounce ray (rt_sort.hip; DESIGN.md §6 key table): direction octant, the direction's cell
+// on a 2^dir_bits x 2^dir_bits octahedral grid, and the origin's Morton code with org_bits per axis — origin-major
+// (org_major) or direction-major.  Written by the shade kernels beside every appended ray.
+__device__ __forceinline__ unsigned ray_sort_key(float4 p, float4 v, const RayKeyIO& k) {
+    const unsigned oct = (v.x < 0.f ? 4u : 0u) | (v.y < 0.f ? 2u : 0u) | (v.z < 0.f ? 1u : 0u);
+    const float sum = fabsf(v.x) + fabsf(v.y) + fabsf(v.z);
+    const float G = (float)(1 << k.dir_bits);
+    const unsigned ux = (unsigned)fminf(fabsf(v.x) / sum * G, G - 1), uy = (unsigned)fminf(fabsf(v.y) / sum * G, G - 1);
+    const unsigned mo = morton_key(p.x, p.y, p.z, k.lo, k.scale, k.org_bits);
+    const unsigned dk = oct << (2 * k.dir_bits) | ux << k.dir_bits | uy;
+    return k.org_major ? (mo << (3 + 2 * k.dir_bits)) | dk : (dk << (3 * k.org_bits)) | mo;
+}
+
 struct PathFilmIO {
     const int* work_pixels; int n_pixels; int n_index;
     RecView rec; const float4* pdfA; const float4* pdfB;
@@ -345,29 +365,28 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
                                 unsigned long long* ctr);
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
                            int* out, unsigned long long* ctr);
+// Coherence sorts (rt_sort.hip): stable device radix sorts with no host read.  temp = sort_temp_bytes() bytes.
 struct SortRaysIO {
-    const float4* o; const float4* d; const int* slot;   // the queue (interleaved (o, d) pairs: d = o + 1, ray k at 2k)
-    float4* so; float4* sd; int* ss;                      // the sorted side queue (interleaved the same way)
+    const unsigned* qkey;                                 // ray keys at the queue positions (ray_sort_key, written
+                                                          // by the shade kernel that appended the rays)
+    const float4* o;                                      // the queue (interleaved (o, d) pairs: ray k at o[2k])
+    float4* so; int* ss;                                  // the sorted side queue (interleaved the same way)
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
-    void* temp; size_t temp_bytes;
-    float4 lo, scale;                                     // origin quantisation: (p - lo) * scale in [0, 512)
+    void* temp;
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin
-    int org_major;                                        // 1: origin Morton code in the high bits instead
     int* len;     // the queue's shard lengths (kQLen region): read, then rewritten for the sorted queue
     int S;        // shard stride (the sorted queue keeps it; its shards split the sorted order evenly)
 };
-size_t sort_rays_temp_bytes(int nmax);
-// n = total length of the queue's shards (read back by the host)
-hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io);
+size_t sort_temp_bytes();
+hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io);
 struct SortNeeIO {
     int* slot; int* len; int S;                          // the NEE queue (NeeIO slot / len), sorted in place
     const unsigned* key;                                 // per queue position, written by k_path_shade_full (NeeIO key)
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
-    void* temp; size_t temp_bytes;
+    void* temp;
     int org_bits;                                        // key: 3 x org_bits Morton code of the shading point
 };
-// n = total length of the NEE queue's shards (read back by the host)
-hipError_t launch_sort_nee(hipStream_t st, int n, const SortNeeIO& io);
+hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io);
 hipError_t launch_oct_classify(hipStream_t st, int nnodes, const float* cbox, const int* seg, const int* ent,
                                const float* tri9, unsigned char* mask, int* stats);
 hipError_t launch_oct_scatter(hipStream_t st, int njobs, int nchild, const int* job, const int* ent,

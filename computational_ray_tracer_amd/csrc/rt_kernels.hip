@@ -1528,6 +1528,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         if (wantNext) {
             nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
             io.nO[2 * pn] = nO; io.nD[2 * pn] = nD; io.nSlot[pn] = slot;
+            if (io.nkey.key) io.nkey.key[pn] = ray_sort_key(nO, nD, io.nkey);
         }
     }
     count_add(ctr, C_SNODES, snn);
@@ -1835,6 +1836,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
         if (wantNext) {
             nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
             io.nO[2 * pn] = nO; io.nD[2 * pn] = nD; io.nSlot[pn] = slot;
+            if (io.nkey.key) io.nkey.key[pn] = ray_sort_key(nO, nD, io.nkey);
         }
     }
 }

@@ -1,164 +1,267 @@
-// Coherence sort of a path-mode ray queue (multi-level octrees): rays are reordered by (direction octant, direction
-// cell on an octahedral grid, Morton code of the origin within the scene bounds) with a stable device radix sort,
-// then gathered into a side queue that the bounce's trace and shade kernels read.  Traversal results are per ray, so
-// the order changes nothing but which rays share a wave: neighbouring rays walk the same nodes and leaves.  The sort
-// must be stable: within a key, rays keep their slot order, so the shade kernel's per-slot state reads stay close
-// (an atomic counting sort with the same keys, unstable, measured CFG3 463 -> 375 Msamples/s).
-#include <hipcub/hipcub.hpp>
+// Coherence sorts of the multi-level path queues: the bounce rays of a depth by their ray key
+// (direction octant, direction cell on an octahedral grid, Morton code of the origin: ray_sort_key, written by the
+// shade kernel beside each appended ray) and the deferred NEE vertices by the Morton code of their shading point
+// (written by k_path_shade_full).  Traversal results are per ray, so the order changes nothing but which rays share a
+// wave: neighbouring rays walk the same nodes and leaves.
+//
+// A hand-written stable LSD radix sort that runs entirely on the device (no host read of the queue length):
+//   k_rs_prep     the queue's shard lengths -> n and the shard prefix (meta), read by every later kernel;
+//   per pass of <= 8 key bits:
+//   k_rs_hist     block b counts the digits of its chunk of the (concatenated) queue in LDS;
+//   k_rs_offsets  one block, thread = digit: the digit totals, their exclusive scan, and every block's exclusive
+//                 start per digit (in place over the histograms);
+//   k_rs_scatter  block b walks its chunk in tiles of 256 items in order; a wave ranks its items among the same
+//                 digit with kRsBits ballots (stable: lane order), the tile's waves are prefixed per digit through
+//                 LDS, and a running count per digit (one digit per thread) carries the order across tiles.  The
+//                 first pass reads the keys at the queue positions; the last one gathers the rays (or NEE slots)
+//                 straight into the sorted side queue, split evenly over the shards.
+// Stability matters: within a key, rays keep their slot order, so the shade kernel's per-slot state reads stay
+// close (an unstable atomic counting sort with the same keys measured CFG3 463 -> 375 Msamples/s in round 2).
+#include <algorithm>
 
 #include "rt_internal.h"
 
 namespace rtmi {
 namespace {
 
+constexpr int kRsMaxBits = 8, kRsBins = 1 << kRsMaxBits;
+constexpr int kRsGrid = 512;           // blocks of the histogram / scatter kernels (2 per CU)
+constexpr int kRsTile = kBlockThreads;  // items per tile: one per thread
+static_assert(kRsTile == kRsBins, "one digit per thread in k_rs_scatter / k_rs_offsets");
 
-__device__ __forceinline__ unsigned spread3(unsigned v) {  // 9 bits -> every third bit of 27
-    v &= 0x1ffu;
-    v = (v | (v << 16)) & 0x030000ffu;
-    v = (v | (v << 8)) & 0x0300f00fu;
-    v = (v | (v << 4)) & 0x030c30c3u;
-    v = (v | (v << 2)) & 0x09249249u;
-    return v;
-}
-
-// (both queues hold interleaved (o, d) pairs: ray k at o[2k], d[2k] with d = o + 1, one 32-B line per ray)
-// key = direction octant, then the octahedral position of the direction on a 2^B x 2^B grid, then a Morton code of
-// the origin with O bits per axis (DESIGN.md §6 key table).  Entry k of the sort is the k-th live ray of the sharded
-// queue (shards in order); its value is the ray's queue position.
-__global__ void __launch_bounds__(kBlockThreads) k_sort_keys(int n, const int* __restrict__ len, int S,
-                                                              const float4* __restrict__ o,
-                                                              const float4* __restrict__ d, float4 lo, float4 scale,
-                                                              int kDirB, int kOrgB, int org_major,
-                                                              unsigned* __restrict__ keys, int* __restrict__ vals) {
-    int pre[kShards + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int j = 0; j < kShards; ++j) pre[j + 1] = pre[j] + len[j * kQStride];
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        int j = 0;
-#pragma unroll
-        for (int u = 1; u < kShards; ++u) j += k >= pre[u] ? 1 : 0;
-        int base = pre[0];
-#pragma unroll
-        for (int u = 1; u < kShards; ++u) base = j == u ? pre[u] : base;
-        const int pos = j * S + (k - base);
-        float4 p = o[2 * pos], v = d[2 * pos];
-        auto q = [](float x) {
-            x = x < 0.f ? 0.f : (x > 511.f ? 511.f : x);
-            return (unsigned)x;
-        };
-        unsigned oct = (v.x < 0.f ? 4u : 0u) | (v.y < 0.f ? 2u : 0u) | (v.z < 0.f ? 1u : 0u);
-        float sum = fabsf(v.x) + fabsf(v.y) + fabsf(v.z);
-        const float G = (float)(1 << kDirB);
-        unsigned ux = (unsigned)fminf(fabsf(v.x) / sum * G, G - 1), uy = (unsigned)fminf(fabsf(v.y) / sum * G, G - 1);
-        unsigned mo = spread3(q((p.x - lo.x) * scale.x) >> (9 - kOrgB)) << 2 |
-                      spread3(q((p.y - lo.y) * scale.y) >> (9 - kOrgB)) << 1 |
-                      spread3(q((p.z - lo.z) * scale.z) >> (9 - kOrgB));
-        const unsigned dk = oct << (2 * kDirB) | ux << kDirB | uy;
-        keys[k] = org_major ? (mo << (3 + 2 * kDirB)) | dk : (dk << (3 * kOrgB)) | mo;
-        vals[k] = pos;
+// meta: [0] n, [1 .. kShards + 1] the exclusive prefix of the shard lengths
+__global__ void k_rs_prep(const int* __restrict__ len, int* __restrict__ meta) {
+    if (threadIdx.x == 0) {
+        int p = 0;
+        for (int j = 0; j < kShards; ++j) {
+            meta[1 + j] = p;
+            p += len[j * kQStride];
+        }
+        meta[1 + kShards] = p;
+        meta[0] = p;
     }
 }
 
-// sorted entry k -> shard k / S2 of the side queue (S2 = shard_stride(n, kShards) <= S; sorted queues have kShards: the sorted order split evenly over
-// the shards), and the side queue's shard lengths replace the queue's (every reader of this bounce uses the side
-// queue)
-__global__ void __launch_bounds__(kBlockThreads) k_sort_gather(int n, const int* __restrict__ perm, int S, int S2,
-                                                                const float4* __restrict__ o,
-                                                                const float4* __restrict__ d,
-                                                                float4* __restrict__ so,
-                                                                float4* __restrict__ sd, int* __restrict__ ss,
-                                                                int* __restrict__ len) {
-    if (blockIdx.x == 0 && threadIdx.x < kShards) {
-        const int c = n - (int)threadIdx.x * S2;
-        len[threadIdx.x * kQStride] = c < 0 ? 0 : (c > S2 ? S2 : c);
-    }
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const int j = perm[k];
-        const int pos = (k / S2) * S + k % S2;
-        const float4 oj = o[2 * j];
-        so[2 * pos] = oj;
-        sd[2 * pos] = d[2 * j];
-        ss[pos] = __float_as_int(oj.w);  // bounce rays carry their slot in o.w: two scattered reads per ray, not three
+__device__ __forceinline__ int rs_chunk(int n) {  // items per block: a multiple of the tile
+    const int c = (n + kRsGrid - 1) / kRsGrid;
+    return (c + kRsTile - 1) / kRsTile * kRsTile;
+}
+// queue position of concatenated item k (shards in order)
+__device__ __forceinline__ int rs_pos(const int* meta, int S, int k) {
+    int j = 0;
+#pragma unroll
+    for (int u = 1; u < kShards; ++u) j += k >= meta[1 + u] ? 1 : 0;
+    int base = meta[1];
+#pragma unroll
+    for (int u = 1; u < kShards; ++u) base = j == u ? meta[1 + u] : base;
+    return j * S + (k - base);
+}
+
+enum { SRC_ARRAY = 0, SRC_RAYQ = 1, SRC_NEEQ = 2 };       // where a pass reads (key, value)
+enum { DST_ARRAY = 0, DST_RAYQ = 1, DST_NEEQ = 2 };       // where it writes them
+
+struct RsPass {
+    const int* meta;
+    int S;                       // the queue's shard stride
+    // sources: SRC_ARRAY keys_in / vals_in[k]; SRC_RAYQ qkey[pos], value pos; SRC_NEEQ qkey[pos], value slot[pos]
+    const unsigned* keys_in; const int* vals_in;
+    const unsigned* qkey; const int* qslot;
+    int shift, nbits;
+    int* hist;                   // kRsGrid x kRsBins: counts, then (k_rs_offsets) exclusive starts
+    // destinations: DST_ARRAY keys_out / vals_out[k']; DST_RAYQ the side queue (rays gathered from o / d by value,
+    // interleaved pairs) + slots; DST_NEEQ the NEE queue's slots in place; both rewrite the shard lengths `len`
+    unsigned* keys_out; int* vals_out;
+    const float4* o; float4* so; int* ss;
+    int* nslot;
+    int* len;
+};
+
+template <int SRC>
+__device__ __forceinline__ void rs_load(const RsPass& p, int k, unsigned& key, int& val) {
+    if constexpr (SRC == SRC_ARRAY) {
+        key = p.keys_in[k];
+        val = p.vals_in[k];
+    } else {
+        const int pos = rs_pos(p.meta, p.S, k);
+        key = p.qkey[pos];
+        val = SRC == SRC_RAYQ ? pos : p.qslot[pos];
     }
 }
 
-// NEE queue coherence sort (mixed scenes, RTMI_SORT_NEE): the deferred NEE vertices of one bounce reordered by the
-// Morton code of their shading point (org_bits per axis; k_path_shade_full writes it beside the queue entry), so the
-// shadow rays of a wave start close together and walk the same BVH nodes toward each light.  k_path_nee still traces and adds a vertex's lights in light order, and the
-// vertices are independent of each other (one slot each), so the film is unchanged.  Entry k is the k-th queued
-// vertex (shards in order); its value is the vertex's slot.
-__global__ void __launch_bounds__(kBlockThreads) k_nee_keys(int n, const int* __restrict__ len, int S,
-                                                             const int* __restrict__ slot,
-                                                             const unsigned* __restrict__ key,
-                                                             unsigned* __restrict__ keys, int* __restrict__ vals) {
-    int pre[kShards + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int j = 0; j < kShards; ++j) pre[j + 1] = pre[j] + len[j * kQStride];
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        int j = 0;
-#pragma unroll
-        for (int u = 1; u < kShards; ++u) j += k >= pre[u] ? 1 : 0;
-        int base = pre[0];
-#pragma unroll
-        for (int u = 1; u < kShards; ++u) base = j == u ? pre[u] : base;
-        const int pos = j * S + (k - base);
-        keys[k] = key[pos];
-        vals[k] = slot[pos];
+template <int SRC>
+__global__ void __launch_bounds__(kBlockThreads) k_rs_hist(RsPass p) {
+    __shared__ int h[kRsBins];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int n = p.meta[0], c = rs_chunk(n);
+    const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
+    const unsigned mask = (1u << p.nbits) - 1u;
+    for (int k = b0 + (int)threadIdx.x; k < b1; k += kBlockThreads) {
+        unsigned key;
+        int val;
+        rs_load<SRC>(p, k, key, val);
+        atomicAdd(&h[(key >> p.shift) & mask], 1);
+    }
+    __syncthreads();
+    p.hist[blockIdx.x * kRsBins + threadIdx.x] = h[threadIdx.x];
+}
+
+// one block, thread d = digit d: start of block b's digit-d items = (items of smaller digits) + (digit-d items of
+// blocks before b)
+__global__ void __launch_bounds__(kBlockThreads) k_rs_offsets(int* __restrict__ hist) {
+    __shared__ int tot[kRsBins];
+    const int d = threadIdx.x;
+    int t = 0;
+#pragma unroll 16
+    for (int b = 0; b < kRsGrid; ++b) t += hist[b * kRsBins + d];
+    tot[d] = t;
+    __syncthreads();
+    // exclusive scan of the digit totals (Hillis-Steele over 256 entries)
+    for (int off = 1; off < kRsBins; off <<= 1) {
+        const int v = d >= off ? tot[d - off] : 0;
+        __syncthreads();
+        tot[d] += v;
+        __syncthreads();
+    }
+    int run = tot[d] - t;
+#pragma unroll 16
+    for (int b = 0; b < kRsGrid; ++b) {
+        const int v = hist[b * kRsBins + d];
+        hist[b * kRsBins + d] = run;
+        run += v;
     }
 }
 
-// sorted entry k -> shard k / S2 of the NEE queue (in place: the slots were copied into the sort's values), and the
-// shard lengths rewritten for that split
-__global__ void __launch_bounds__(kBlockThreads) k_nee_scatter(int n, const int* __restrict__ sorted, int S, int S2,
-                                                                int* __restrict__ slot, int* __restrict__ len) {
-    if (blockIdx.x == 0 && threadIdx.x < kShards) {
-        const int c = n - (int)threadIdx.x * S2;
-        len[threadIdx.x * kQStride] = c < 0 ? 0 : (c > S2 ? S2 : c);
+__device__ __forceinline__ int rs_lane() {
+    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+template <int SRC, int DST>
+__global__ void __launch_bounds__(kBlockThreads) k_rs_scatter(RsPass p) {
+    constexpr int NW = kBlockThreads / 64;
+    __shared__ int wcnt[NW][kRsBins];
+    __shared__ int wpre[NW][kRsBins];
+    const int n = p.meta[0], c = rs_chunk(n);
+    const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
+    const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
+    const unsigned mask = (1u << p.nbits) - 1u;
+    int run = p.hist[blockIdx.x * kRsBins + tid];  // this thread's digit (tid): next output index
+    const int S2 = shard_stride(n, kShards);      // the sorted queue: item k' at shard k' / S2
+    if (DST != DST_ARRAY && blockIdx.x == 0 && tid < kShards) {
+        const int cc = n - tid * S2;
+        p.len[tid * kQStride] = cc < 0 ? 0 : (cc > S2 ? S2 : cc);
     }
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
-        slot[(k / S2) * S + k % S2] = sorted[k];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int t0 = b0; t0 < b1; t0 += kRsTile) {  // (block-uniform trip count)
+        const int k = t0 + tid;
+        const bool valid = k < b1;
+        unsigned key = 0;
+        int val = 0;
+        if (valid) rs_load<SRC>(p, k, key, val);
+        const unsigned dg = (key >> p.shift) & mask;
+        // lanes of this wave with the same digit: AND over the digit's bits of (ballot of the bit, or its complement)
+        uint64_t m = __ballot(valid);
+        for (int bit = 0; bit < p.nbits; ++bit) {
+            const uint64_t bb = __ballot((dg >> bit) & 1u);
+            m &= ((dg >> bit) & 1u) ? bb : ~bb;
+        }
+        const int rank = __popcll(m & lt);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) wcnt[i][tid] = 0;
+        __syncthreads();
+        if (valid && rank == 0) wcnt[w][dg] = __popcll(m);  // the digit's lowest lane reports the wave's count
+        __syncthreads();
+        {  // digit tid: prefix over the tile's waves, then carry the running count
+            int r = run;
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                wpre[i][tid] = r;
+                r += wcnt[i][tid];
+            }
+            run = r;
+        }
+        __syncthreads();
+        if (valid) {
+            const int dst = wpre[w][dg] + rank;
+            if constexpr (DST == DST_ARRAY) {
+                p.keys_out[dst] = key;
+                p.vals_out[dst] = val;
+            } else {
+                const int pos = (dst / S2) * p.S + dst % S2;
+                if constexpr (DST == DST_RAYQ) {
+                    const float4 oj = p.o[2 * val], dj = p.o[2 * val + 1];
+                    p.so[2 * pos] = oj;
+                    p.so[2 * pos + 1] = dj;
+                    p.ss[pos] = __float_as_int(oj.w);  // bounce rays carry their slot in o.w
+                } else {
+                    p.nslot[pos] = val;
+                }
+            }
+        }
+        // (wcnt / wpre are rewritten only after the next tile's first barrier)
+    }
+}
+
+template <int SRC, int DST>
+void rs_launch(hipStream_t st, const RsPass& p) {
+    hipLaunchKernelGGL(k_rs_hist<SRC>, dim3(kRsGrid), dim3(kBlockThreads), 0, st, p);
+    hipLaunchKernelGGL(k_rs_offsets, dim3(1), dim3(kBlockThreads), 0, st, p.hist);
+    hipLaunchKernelGGL((k_rs_scatter<SRC, DST>), dim3(kRsGrid), dim3(kBlockThreads), 0, st, p);
+}
+
+// the passes of a `bits`-bit key, <= kRsMaxBits each (split evenly), ping-ponging between the two arrays
+template <int SRC, int DST>
+hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* kb, int* va, int* vb) {
+    // (the NEE queue is sorted in place: its first pass must finish reading the slots before any is rewritten)
+    const int passes = std::max((bits + kRsMaxBits - 1) / kRsMaxBits, DST == DST_NEEQ ? 2 : 1);
+    const int per = (bits + passes - 1) / passes;
+    hipLaunchKernelGGL(k_rs_prep, dim3(1), dim3(64), 0, st, p.len, const_cast<int*>(p.meta));
+    for (int i = 0; i < passes; ++i) {
+        p.shift = i * per;
+        p.nbits = bits - p.shift < per ? bits - p.shift : per;
+        const bool first = i == 0, last = i == passes - 1;
+        p.keys_out = (i & 1) ? kb : ka;
+        p.vals_out = (i & 1) ? vb : va;
+        if (first && last) rs_launch<SRC, DST>(st, p);
+        else if (first) rs_launch<SRC, DST_ARRAY>(st, p);
+        else if (last) rs_launch<SRC_ARRAY, DST>(st, p);
+        else rs_launch<SRC_ARRAY, DST_ARRAY>(st, p);
+        p.keys_in = p.keys_out;
+        p.vals_in = p.vals_out;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace
 
-size_t sort_rays_temp_bytes(int nmax) {
-    size_t bytes = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned*)nullptr, (unsigned*)nullptr,
-                                       (const int*)nullptr, (int*)nullptr, nmax, 0, 32);
-    return bytes;
+size_t sort_temp_bytes() { return sizeof(int) * ((size_t)kRsGrid * kRsBins + 64); }
+
+hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io) {
+    RsPass p{};
+    int* hist = static_cast<int*>(io.temp);
+    p.hist = hist;
+    p.meta = hist + (size_t)kRsGrid * kRsBins;
+    p.S = io.S;
+    p.qkey = io.qkey;
+    p.o = io.o;
+    p.so = io.so;
+    p.ss = io.ss;
+    p.len = io.len;
+    const int bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
+    return rs_sort<SRC_RAYQ, DST_RAYQ>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
-hipError_t launch_sort_rays(hipStream_t st, int n, const SortRaysIO& io) {
-    if (n <= 0) return hipSuccess;
-    int g = (n + kBlockThreads - 1) / kBlockThreads;
-    g = g < 8192 ? g : 8192;
-    const int key_bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
-    hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.len, io.S, io.o, io.d, io.lo, io.scale,
-                       io.dir_bits, io.org_bits, io.org_major, io.keys, io.vals);
-    size_t bytes = io.temp_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
-                                                      key_bits, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_sort_gather, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.S, shard_stride(n, kShards),
-                       io.o, io.d, io.so, io.sd, io.ss, io.len);
-    return hipGetLastError();
-}
-
-hipError_t launch_sort_nee(hipStream_t st, int n, const SortNeeIO& io) {
-    if (n <= 0) return hipSuccess;
-    int g = (n + kBlockThreads - 1) / kBlockThreads;
-    g = g < 8192 ? g : 8192;
-    hipLaunchKernelGGL(k_nee_keys, dim3(g), dim3(kBlockThreads), 0, st, n, io.len, io.S, io.slot, io.key, io.keys,
-                       io.vals);
-    size_t bytes = io.temp_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(io.temp, bytes, io.keys, io.keys_alt, io.vals, io.vals_alt, n, 0,
-                                                      3 * io.org_bits, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_nee_scatter, dim3(g), dim3(kBlockThreads), 0, st, n, io.vals_alt, io.S,
-                       shard_stride(n, kShards), io.slot, io.len);
-    return hipGetLastError();
+hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io) {
+    RsPass p{};
+    int* hist = static_cast<int*>(io.temp);
+    p.hist = hist;
+    p.meta = hist + (size_t)kRsGrid * kRsBins;
+    p.S = io.S;
+    p.qkey = io.key;
+    p.qslot = io.slot;
+    p.nslot = io.slot;  // in place: the first pass copied the slots into the values
+    p.len = io.len;
+    return rs_sort<SRC_NEEQ, DST_NEEQ>(st, 3 * io.org_bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 }  // namespace rtmi
