@@ -24,8 +24,8 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-from computational_ray_tracer_amd import scene  # noqa: E402
-from computational_ray_tracer_amd.distributed import FrameLoop  # noqa: E402
+from computational_ray_tracer_amd import capi, scene  # noqa: E402
+from computational_ray_tracer_amd.distributed import FrameLoop, init_distributed, timed_steps  # noqa: E402
 from computational_ray_tracer_amd.renderer import Renderer  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -54,10 +54,10 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
 
     Algorithmic bytes follow SURVEY.md §8(d): the per-ray HBM streams are `achieved` (k_trace_closest: 40 B per
     ray cast; k_path_shade: 312 B per shaded bounce + 32 B per shadow ray); the §8(d) scene terms (32 B per box
-    test + 40 B per triangle test actually executed) are reported beside them as `achieved_incl_scene` — they are
-    cache hits (the Cornell scene is 1.8 KB, the CFG3 BVH 1.7 MB + 4.7 MB of triangles), so folding them into an
-    HBM rate could exceed the HBM peak.  `traffic` is the PMC-measured DRAM bytes per launch and `valu` the
-    SQ_INSTS_VALU per launch over the same single-lane launch time, both from profiles/counters_<config>.json."""
+    test + 40 B per triangle test actually executed) are reported beside them as bytes only — they are cache hits
+    (the Cornell scene is 1.8 KB, the CFG3 BVH 1 MB + 4.7 MB of triangles), never an HBM rate.  `traffic` is the
+    PMC-measured DRAM bytes per launch and `valu` the SQ_INSTS_VALU per launch over the same single-lane launch time,
+    both from profiles/counters_<config>.json when it was measured on the loaded library build."""
     ks = {
         "k_trace_closest": (st["ms_trace"], st["launches_trace"], 40 * st["rays"],
                             32 * st["nodes_tested"] + 40 * st["tris_tested"]),
@@ -90,8 +90,9 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
                      "traffic": kc.get("dram_bytes_per_launch"),
                      "kernel": name, "launches": launches, "avg_launch_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": int(stream_b / launches),
-                     "scene_bytes_per_launch": int(scene_b / launches),
-                     "achieved_incl_scene": round((stream_b + scene_b) / launches / avg_s / 1e9, 1),
+                     # §8(d) scene terms over the EXECUTED box / triangle tests: served by LDS / L1 / L2 (the
+                     # scenes are <= 6 MB), so they are reported as bytes, never as an HBM rate
+                     "scene_bytes_per_launch_cache_served": int(scene_b / launches),
                      "total_ms": round(ms, 3)}
         if kc.get("valu_insts_per_launch"):
             g = kc["valu_insts_per_launch"] / avg_s / 1e9
@@ -202,15 +203,11 @@ def cpu_baseline(cfg, seconds):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    torch.cuda.set_device(local if world > 1 else 0)
+    # RCCL over xGMI; a finite collective timeout + async error handling: a dead rank fails the run, not hangs it
+    world, rank = init_distributed("nccl", device_id=torch.device("cuda", local) if world > 1 else None)
     W, H = (int(x) for x in a.res.split("x"))
     if a.config == "cornell":
         cfg = scene.cfg_cornell(res=(W, H), spp_side=16, max_depth=5)
@@ -240,37 +237,27 @@ def main():
     def step():
         return loop.step(lambda i0, i1, f: r.render_pass_device(i0, i1, f.data_ptr(), stream.cuda_stream))
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    r.reset_stats()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    idx_done = 0
-    for _ in range(a.steps):
-        idx_done += step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    tm = timed_steps(step, a.steps, a.warmup, torch.cuda.synchronize, lambda: r.stats()["samples"], r.reset_stats)
+    dt, total_samples = tm["dt"], tm["total"]
     st = r.stats()
-    if world > 1:
-        t = torch.tensor([dt], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        tot = torch.tensor([st["samples"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tot)
-        total_samples = float(tot.item())
-    else:
-        total_samples = float(st["samples"])
     value = total_samples / dt / 1e6
     # roofline of the dominant kernel (most HIP-event time), from a single-lane pass (see single_lane_pass)
-    counters = None
+    # PMC bytes / VALU instructions (profiles/counters_<config>.json, tools/counters.py) are only valid for the
+    # workload AND the library build they measured: they are used only when their build id is the loaded library's
+    counters, cstat = None, None
     cf = COUNTERS_DIR / f"counters_{a.config}.json"
-    if cf.exists():  # PMC bytes / VALU instructions are only valid for the workload they measured
-        counters = json.loads(cf.read_text()).get("kernels")
+    loaded = capi.library_sha16()
+    if cf.exists():
+        cj = json.loads(cf.read_text())
+        cstat = {"file": str(cf.relative_to(ROOT)), "tag": cj.get("tag"), "lib_sha16": cj.get("lib_sha16"),
+                 "loaded_lib_sha16": loaded}
+        if cj.get("lib_sha16") == loaded:
+            counters = cj.get("kernels")
+            cstat["status"] = "current build"
+        else:
+            cstat["status"] = "stale (another build): traffic / valu omitted"
+    else:
+        cstat = {"status": "none: traffic / valu omitted", "loaded_lib_sha16": loaded}
     roofline = {}
     if rank == 0:
         st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
@@ -282,6 +269,7 @@ def main():
         roofline["ms_per_step_single_lane"] = round(dt1 / a.steps * 1e3, 3)
         roofline["limiter"] = "VALU issue and memory latency (box + watertight triangle tests); see DESIGN.md §4"
         roofline["other_kernels"] = {k: v for k, v in rl.items() if k != dom}
+        roofline["counters"] = cstat
     # Two batches run concurrently on two streams in the timed region (DESIGN.md §4 lanes); the node-level figure
     # divides every kernel's §8(d) stream bytes (generate 96 B/sample, trace 40 B/ray, shade 312 B/bounce + 32 B per
     # shadow ray, film 128 B/sample) by the wall time of the timed region.
@@ -292,7 +280,8 @@ def main():
                         "basis": "all kernels' algorithmic stream bytes / wall time of the timed region"}
     out = {
         "metric": "Msamples/s (whole node) at 1920x1080; achieved HBM GB/s vs roofline",
-        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "ranks": tm["ranks"],
+        "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (procedural Cornell box scene, no datasets)",
         "config": {"workload": workload,

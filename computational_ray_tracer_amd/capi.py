@@ -140,12 +140,24 @@ class RTError(RuntimeError):
         self.status = status
 
 
+def library_path():
+    """The librtmi355x.so that load_library() loads (RTMI_LIB overrides the in-tree build)."""
+    return Path(os.environ.get("RTMI_LIB", LIB_PATH))
+
+
+def library_sha16(path=None):
+    """Build id of a library file: the first 16 hex digits of its SHA-256 (profiles/counters_*.json carry the id of
+    the build they were measured on; bench.py uses their PMC figures only for the same build)."""
+    import hashlib
+    return hashlib.sha256(Path(path or library_path()).read_bytes()).hexdigest()[:16]
+
+
 def load_library(path=None):
     """Load librtmi355x.so (built in-tree).  Raises if it is missing — no fallback exists."""
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else Path(os.environ.get("RTMI_LIB", LIB_PATH))  # RTMI_LIB: A/B kernel variants
+    p = Path(path) if path else library_path()  # RTMI_LIB: A/B kernel variants
     if not p.exists():
         raise RuntimeError(f"{p} is missing: build it with `python __graft_entry__.py build` "
                            "(the MI355X HIP extension is the only implementation of the hot path)")

@@ -435,11 +435,11 @@ struct Work {
     float4 *rayO = nullptr, *rayD = nullptr, *lamA = nullptr, *lamB = nullptr, *pdfA = nullptr, *pdfB = nullptr;
     float4* hitB = nullptr;
     float4* rec = nullptr;     // path mode: one 128-B record per slot (rt_internal.h R_*)
-    int *slot = nullptr, *hitPrim = nullptr;
+    int* hitPrim = nullptr;
     int* d_qcount = nullptr;   // queue q's counters at [q * kQRegion + kQLen / kQTraceTicket / ...] (rt_internal.h)
     // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers
     float4 *sO = nullptr, *sD = nullptr;
-    int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;
+    int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;  // sS: the sort permutation (TraceIO perm)
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
     unsigned* sQKey = nullptr;  // the ray queue's sort keys at queue positions (written by the shade kernels)
     void* sTemp = nullptr;      // the sorts' histograms and meta (sort_temp_bytes)
@@ -503,14 +503,14 @@ struct rt_ctx {
     int bvh_max_leaf = kBvhMaxLeaf;  // triangles per BVH leaf at most (RTMI_BVH_LEAF)
     int bvh_count[2][2] = {};  // per tile set: BVH nodes, BVH tiles (rt_bvh_export)
     int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
-    int sort_dir_bits = 3, sort_org_bits = 4;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; 3/7 3/2 2/5 within 2 %)
+    int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
     // queue has a sort of its own (CFG4 372 vs 367)
     int sort_org_major = -1;
     // Morton sort of the NEE queue (mixed multi-level scenes; RTMI_SORT_NEE="on[/bits]"): CFG4 337 -> 364 at 9 bits
     // per axis (6 / 7 bits: 353 / 356; CFG5 334 -> 355 at 7)
-    int sort_nee = 1, sort_nee_bits = 9;
+    int sort_nee = 1, sort_nee_bits = 8;  // (r03, device radix sort: 8 bits = 3 passes, CFG4 +1.5 % over 9 bits = 4 passes)
     hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
     size_t batch_samples = 0;  // samples in flight per batch (0: 16 Mi; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
@@ -637,11 +637,11 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
 void free_workspace(Work& w) {
     free_sort_workspace(w);
     free_shadow_workspace(w);
-    void* ptrs[] = {w.rayO, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.rec, w.slot, w.hitPrim};  // (rayD = rayO + 1)
+    void* ptrs[] = {w.rayO, w.lamA, w.lamB, w.pdfA, w.pdfB, w.hitB, w.rec, w.hitPrim};  // (rayD = rayO + 1)
     for (void* p : ptrs)
         if (p) hipFree(p);
     w.rayO = w.rayD = w.lamA = w.lamB = w.pdfA = w.pdfB = w.hitB = w.rec = nullptr;
-    w.slot = w.hitPrim = nullptr;
+    w.hitPrim = nullptr;
     w.cap = 0;
 }
 void free_ring(Work& w) {
@@ -690,7 +690,7 @@ int ensure_workspace(rt_ctx* c, Work& w, size_t n, bool path) {
     size_t nq = path ? 2 * n : n;
     // rays as interleaved (o, d) pairs, 32 B per ray (rayD = rayO + 1, kernels index [k << rsh] with rsh = 1): a
     // scattered read of one ray (the coherence sort's gather) touches one line instead of two
-    HIPCHK(c, dalloc(&w.rayO, 2 * nq)); w.rayD = w.rayO + 1; HIPCHK(c, dalloc(&w.slot, nq));
+    HIPCHK(c, dalloc(&w.rayO, 2 * nq)); w.rayD = w.rayO + 1;
     HIPCHK(c, dalloc(&w.pdfA, n)); HIPCHK(c, dalloc(&w.pdfB, n));
     HIPCHK(c, dalloc(&w.hitB, n)); HIPCHK(c, dalloc(&w.hitPrim, n));
     if (path) {
@@ -1042,7 +1042,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             int nIdx = std::min(B, ie - b0);
             int nS = nIdx * c->n_work;
             SampleIds ids = sample_ids(c, b0);
-            GenOut go{w.rayO, w.rayD, w.slot, w.lamA, w.lamB, w.pdfA, w.pdfB, RecView{nullptr, 0, 0}, 0, 1};
+            GenOut go{w.rayO, w.rayD, w.lamA, w.lamB, w.pdfA, w.pdfB, RecView{nullptr, 0, 0}, 0, 1};
             hipEvent_t e0 = ev_start(c, st);
             HIPCHK(c, launch_generate(st, c->grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, st, ST_GEN, e0);
@@ -1120,7 +1120,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             nSq[l] = nS;
             Sq[l] = shard_stride(nS, nsh);  // every queue of this batch: shard j at [j S, j S + len_j)
             SampleIds ids = sample_ids(c, b0);
-            GenOut go{w.rayO, w.rayD, w.slot, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0, 1};
+            GenOut go{w.rayO, w.rayD, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0, 1};
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, s, ST_GEN, e0);
@@ -1139,7 +1139,6 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 int nxt = cur[l] ^ 1;
                 const float4* cO = w.rayO + 2 * (size_t)cur[l] * qs;
                 const float4* cD = cO + 1;
-                const int* cS = w.slot + (size_t)cur[l] * qs;
                 int* qc_cur = w.d_qcount + kQRegion * cur[l];
                 int* qc_nxt = w.d_qcount + kQRegion * nxt;
                 // the next queue's length and the chunk tickets its trace and shade launches will use
@@ -1150,25 +1149,27 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 // padded keys instead, without the host read: -0.6 %); the other lane keeps the GPU busy meanwhile.
                 const QueueView qv = depth == 0 ? QueueView{nullptr, Sq[l], nSq[l], nsh}
                                                 : QueueView{qc_cur + kQLen, Sq[l], 0, nsh};
+                const DevScene dsl = lane_scene(c, w);
+                TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
                 if (sort_rays && depth > 0) {  // the device reads the queue length itself: no host round trip
-                    SortRaysIO so{w.sQKey, cO, w.sO, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
+                    SortRaysIO so{w.sQKey, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
                                   c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l]};
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, so));
                     ev_mark(c, s, ST_SORT, e0);
-                    cO = w.sO; cD = w.sD; cS = w.sS;
+                    tio.perm = w.sS;  // the trace kernel gathers the sorted rays into the side queue
+                    tio.so = w.sO;
+                    cO = w.sO; cD = w.sD;
                 }
-                const DevScene dsl = lane_scene(c, w);
-                TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
                 ev_mark(c, s, ST_TRACE, e0);
                 PathIO pio{};
                 pio.lean = lean ? 1 : 0;
-                pio.rayO = cO; pio.rayD = cD; pio.slot = cS; pio.q = qv;
+                pio.rayO = cO; pio.rayD = cD; pio.q = qv;
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
                 pio.nO = w.rayO + 2 * (size_t)nxt * qs; pio.nD = pio.nO + 1;
-                pio.nSlot = w.slot + (size_t)nxt * qs; pio.nCount = qc_nxt + kQLen;
+                pio.nCount = qc_nxt + kQLen;
                 pio.rec = rv; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 pio.dim = -1;
@@ -2332,7 +2333,7 @@ static int impl_rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, con
         hipMemcpy(dp, pixel_ids, 4 * (size_t)n, hipMemcpyHostToDevice);
         hipMemcpy(di, indices, 4 * (size_t)n, hipMemcpyHostToDevice);
         SampleIds ids{nullptr, 1, 0, dp, di};
-        GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].slot, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA,
+        GenOut go{c->ws[0].rayO, c->ws[0].rayD, c->ws[0].lamA, c->ws[0].lamB, c->ws[0].pdfA,
                   c->ws[0].pdfB, RecView{nullptr, 0, 0}, 0, 1};
         DevFilm fd = dev_film(c);
         TraceIO tio{c->ws[0].rayO, c->ws[0].rayD, QueueView{nullptr, shard_stride(n, 1), n, 1}, c->cull ? 1 : 0, c->ws[0].hitB,

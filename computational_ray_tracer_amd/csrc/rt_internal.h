@@ -199,7 +199,7 @@ struct RecView {
 };
 
 struct GenOut {
-    float4* rayO; float4* rayD; int* slot;
+    float4* rayO; float4* rayD;   // the origin's w = the ray's path slot
     float4* lamA; float4* lamB; float4* pdfA; float4* pdfB;  // reference mode (lamA/lamB) + pdfs
     RecView rec;                                             // path mode: the slot state (λ, sampler, β, L, ...)
     int lean;  // simple path kernel: no β = 1 / L = 0 / pdf / dimension stores (depth 0, the film kernel and the
@@ -247,6 +247,10 @@ struct TraceIO {
     int* hitPrim;
     int* ticket = nullptr;    // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
     int rsh = 0;              // ray k at rayO[k << rsh] (1: the workspace's interleaved (o, d) pairs; 0: caller arrays)
+    // sorted bounce (multi-level scenes, tickets only): position p traces the queue's ray perm[p] (rt_sort.hip) and
+    // stores it to so[2p], so[2p + 1] — the sorted side queue the shade kernel reads; nullptr: no sort
+    const int* perm = nullptr;
+    float4* so = nullptr;
 };
 
 struct ShadeRefIO {
@@ -266,9 +270,9 @@ struct RayKeyIO {
 };
 struct PathIO {
     // queue rays are interleaved (o, d) pairs, 32 B per ray: ray k at rayO[2k] / rayD[2k] (rayD = rayO + 1), nO / nD too
-    const float4* rayO; const float4* rayD; const int* slot; QueueView q;       // current queue
+    const float4* rayO; const float4* rayD; QueueView q;  // current queue (origin w = the ray's path slot)
     const float4* hitB; const int* hitPrim;                                     // at queue position
-    float4* nO; float4* nD; int* nSlot; int* nCount;  // next queue: same shard stride, lengths at nCount + j kQStride
+    float4* nO; float4* nD; int* nCount;  // next queue: same shard stride, lengths at nCount + j kQStride
     RecView rec;                                                          // slot state (R_LAM ...)
     float4* pdfA; float4* pdfB;                                           // TerminateSecondary writes them
     int depth, max_depth;
@@ -369,8 +373,8 @@ hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, 
 struct SortRaysIO {
     const unsigned* qkey;                                 // ray keys at the queue positions (ray_sort_key, written
                                                           // by the shade kernel that appended the rays)
-    const float4* o;                                      // the queue (interleaved (o, d) pairs: ray k at o[2k])
-    float4* so; int* ss;                                  // the sorted side queue (interleaved the same way)
+    int* perm;                                            // out: sorted position -> queue position (the trace
+                                                          // kernel gathers the rays: TraceIO perm)
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp;
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin

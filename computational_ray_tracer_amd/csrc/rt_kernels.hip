@@ -429,9 +429,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         mat4_mul(cam.c2w, o.x, o.y, o.z, 1.f, wo);
         mat4_mul(cam.c2w, d.x, d.y, d.z, 0.f, wd);
         float inv = 1.0f / sqrtf((wd[0] * wd[0] + wd[1] * wd[1]) + (wd[2] * wd[2] + wd[3] * wd[3]));  // glm dot vec4
-        out.rayO[s << out.rsh] = make_float4(wo[0], wo[1], wo[2], 0.f);
+        // the origin's w carries the path slot (= s for camera rays) through every queue and sort
+        out.rayO[s << out.rsh] = make_float4(wo[0], wo[1], wo[2], __int_as_float(s));
         out.rayD[s << out.rsh] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
-        out.slot[s] = s;
         if (!out.lean) store8(out.pdfA, out.pdfB, s, pdf);
         if (out.rec.p) {  // path mode: the slot's state
             rstore8(out.rec, s, R_LAM, lam);
@@ -577,6 +577,12 @@ __device__ __forceinline__ uint32_t cluster_mask(const float4* cl, int ncl, bool
     }
     return hm;
 }
+// triangles of the clusters in mask hm (the last cluster may hold fewer than kClusterTris of the leaf's n)
+__device__ __forceinline__ int cluster_tris(uint32_t hm, int ncl, int n) {
+    int t = __popc(hm) * kClusterTris;
+    if ((hm >> (ncl - 1)) & 1u) t -= ncl * kClusterTris - n;
+    return t;
+}
 // ===================================================================================== K2 traverse
 // Octtree_Model.h:66-127 — FIFO BFS.  The 8 children of an internal node are contiguous, so the queue
 // holds one entry per child *group*; popping a group visits its 8 nodes in order, which reproduces the
@@ -617,6 +623,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 // error-bound tail run per candidate, not once per triangle for whichever lane reached it
                 uint64_t cand = 0;
                 int k = 0;
+                int ntest = r.y;  // candidate tests this lane executes (the culled paths test only hit clusters)
                 const uint64_t fp = sc.fan_pairs[set];  // bit k: leaf tiles k, k+1 share vertices (a,b,c),(a,c,d)
                 // conservative cluster boxes first: a cluster no lane of the wave reaches is skipped whole
                 // (closest hit: the box over [0, inf); any hit: over [0, tMax], exact for a fixed tMax).  Shadow rays
@@ -646,6 +653,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         cw.cand[ln] = 0;
                         int np = 0;
                         const uint32_t hm = cluster_mask(cl, ncl, far, o, inv, cl_t);
+                        ntest = cluster_tris(hm, ncl, r.y);
                         for (int c = 0; c < ncl; ++c) {
                             const bool hb = (hm >> c) & 1u;
                             uint64_t m = __ballot(hb);
@@ -678,6 +686,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         k = r.y;
                     } else {
                     const uint32_t hm = cluster_mask(cl, ncl, far, o, inv, cl_t);
+                    ntest = cluster_tris(hm, ncl, r.y);
                     for (int c = 0; c < ncl; ++c) {
                         const bool hb = (hm >> c) & 1u;
                         if (__ballot(hb) == 0) continue;
@@ -722,7 +731,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     int e = 3 * (r.x + k);
                     if (tri_candidate<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2))) cand |= 1ull << k;
                 }
-                nt += r.y;
+                nt += ntest;  // executed tests (the reference tests all r.y of them)
                 while (cand) {
                     int j = __builtin_ctzll(cand);
                     cand &= cand - 1;
@@ -1218,13 +1227,18 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
             }
         }
     } else {
+        // Multi-level scenes, sorted bounces: position p's ray is the queue's ray perm[p] (rt_sort.hip), gathered
+        // here into the sorted side queue `so` (coalesced stores) on its way to the traversal
         WaveTickets tk(io.ticket, io.q);
         int j, base;
         while (tk.next(j, base)) {
             const int idx = base + lane_id();
             if (idx < tk.len) {
                 const int p = j * io.q.S + idx;
-                trace_one(p, io.rayO[p << io.rsh], io.rayD[p << io.rsh]);
+                const int src = io.perm ? io.perm[p] : p;
+                const float4 o4 = io.rayO[src << io.rsh], d4 = io.rayD[src << io.rsh];
+                if (io.so) { io.so[2 * p] = o4; io.so[2 * p + 1] = d4; }
+                trace_one(p, o4, d4);
             }
         }
     }
@@ -1384,7 +1398,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         float Ld[8];
         int slot = -1;
         if (live) {
-            slot = io.slot[k];
+            slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
             const int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
@@ -1526,8 +1540,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevSc
         }
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
-            nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
-            io.nO[2 * pn] = nO; io.nD[2 * pn] = nD; io.nSlot[pn] = slot;
+            nO.w = __int_as_float(slot);  // the ray's origin carries its slot
+            io.nO[2 * pn] = nO; io.nD[2 * pn] = nD;
             if (io.nkey.key) io.nkey.key[pn] = ray_sort_key(nO, nD, io.nkey);
         }
     }
@@ -1630,7 +1644,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int slot = -1;
         if (live) {
-            slot = io.slot[k];
+            slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
             int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
@@ -1834,8 +1848,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
         }
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
-            nO.w = __int_as_float(slot);  // (the slot again, for the coherence sort's gather: rt_sort.hip)
-            io.nO[2 * pn] = nO; io.nD[2 * pn] = nD; io.nSlot[pn] = slot;
+            nO.w = __int_as_float(slot);  // the ray's origin carries its slot
+            io.nO[2 * pn] = nO; io.nD[2 * pn] = nD;
             if (io.nkey.key) io.nkey.key[pn] = ray_sort_key(nO, nD, io.nkey);
         }
     }

@@ -8,13 +8,14 @@
 //   k_rs_prep     the queue's shard lengths -> n and the shard prefix (meta), read by every later kernel;
 //   per pass of <= 8 key bits:
 //   k_rs_hist     block b counts the digits of its chunk of the (concatenated) queue in LDS;
-//   k_rs_offsets  one block, thread = digit: the digit totals, their exclusive scan, and every block's exclusive
-//                 start per digit (in place over the histograms);
-//   k_rs_scatter  block b walks its chunk in tiles of 256 items in order; a wave ranks its items among the same
+//   k_rs_offsets  block = digit: the exclusive scan of the digit's counts over the blocks and the digit's total;
+//   k_rs_scatter  block b scans the digit totals into digit starts, then walks its chunk in tiles of 256 items in
+//                 order; a wave ranks its items among the same
 //                 digit with kRsBits ballots (stable: lane order), the tile's waves are prefixed per digit through
 //                 LDS, and a running count per digit (one digit per thread) carries the order across tiles.  The
-//                 first pass reads the keys at the queue positions; the last one gathers the rays (or NEE slots)
-//                 straight into the sorted side queue, split evenly over the shards.
+//                 first pass reads the keys at the queue positions; the last one writes the queue positions (rays:
+//                 the trace kernel gathers them, TraceIO perm) or the NEE slots (in place) in the sorted queue's
+//                 sharded layout, the sorted order split evenly over the shards.
 // Stability matters: within a key, rays keep their slot order, so the shade kernel's per-slot state reads stay
 // close (an unstable atomic counting sort with the same keys measured CFG3 463 -> 375 Msamples/s in round 2).
 #include <algorithm>
@@ -25,7 +26,7 @@ namespace rtmi {
 namespace {
 
 constexpr int kRsMaxBits = 8, kRsBins = 1 << kRsMaxBits;
-constexpr int kRsGrid = 512;           // blocks of the histogram / scatter kernels (2 per CU)
+constexpr int kRsGrid = 1024;          // blocks of the histogram / scatter kernels (4 per CU)
 constexpr int kRsTile = kBlockThreads;  // items per tile: one per thread
 static_assert(kRsTile == kRsBins, "one digit per thread in k_rs_scatter / k_rs_offsets");
 
@@ -58,7 +59,7 @@ __device__ __forceinline__ int rs_pos(const int* meta, int S, int k) {
 }
 
 enum { SRC_ARRAY = 0, SRC_RAYQ = 1, SRC_NEEQ = 2 };       // where a pass reads (key, value)
-enum { DST_ARRAY = 0, DST_RAYQ = 1, DST_NEEQ = 2 };       // where it writes them
+enum { DST_ARRAY = 0, DST_PERM = 1, DST_NEEQ = 2 };       // where it writes them
 
 struct RsPass {
     const int* meta;
@@ -67,11 +68,13 @@ struct RsPass {
     const unsigned* keys_in; const int* vals_in;
     const unsigned* qkey; const int* qslot;
     int shift, nbits;
-    int* hist;                   // kRsGrid x kRsBins: counts, then (k_rs_offsets) exclusive starts
-    // destinations: DST_ARRAY keys_out / vals_out[k']; DST_RAYQ the side queue (rays gathered from o / d by value,
-    // interleaved pairs) + slots; DST_NEEQ the NEE queue's slots in place; both rewrite the shard lengths `len`
+    int* hist;                   // kRsBins x kRsGrid (digit-major): counts, then (k_rs_offsets) each block's
+                                 // exclusive start within its digit
+    int* tot;                    // kRsBins digit totals (k_rs_offsets)
+    // destinations: DST_ARRAY keys_out / vals_out[k']; DST_PERM the values (queue positions) in the sorted queue's
+    // sharded layout (perm: the trace kernel gathers the rays); DST_NEEQ the NEE queue's slots in place; both rewrite
+    // the shard lengths `len`
     unsigned* keys_out; int* vals_out;
-    const float4* o; float4* so; int* ss;
     int* nslot;
     int* len;
 };
@@ -88,48 +91,59 @@ __device__ __forceinline__ void rs_load(const RsPass& p, int k, unsigned& key, i
     }
 }
 
+// barrier for LDS hand-offs only: waits for the block's LDS operations, not for its global loads in flight
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <int SRC>
 __global__ void __launch_bounds__(kBlockThreads) k_rs_hist(RsPass p) {
+    constexpr int U = 4;  // items in flight per thread
     __shared__ int h[kRsBins];
     h[threadIdx.x] = 0;
     __syncthreads();
     const int n = p.meta[0], c = rs_chunk(n);
     const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
     const unsigned mask = (1u << p.nbits) - 1u;
-    for (int k = b0 + (int)threadIdx.x; k < b1; k += kBlockThreads) {
-        unsigned key;
-        int val;
-        rs_load<SRC>(p, k, key, val);
-        atomicAdd(&h[(key >> p.shift) & mask], 1);
+    for (int k0 = b0 + (int)threadIdx.x; k0 < b1; k0 += U * kBlockThreads) {
+        unsigned key[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * kBlockThreads;
+            int val;
+            key[u] = 0;
+            if (k < b1) rs_load<SRC>(p, k, key[u], val);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (k0 + u * kBlockThreads < b1) atomicAdd(&h[(key[u] >> p.shift) & mask], 1);
     }
     __syncthreads();
-    p.hist[blockIdx.x * kRsBins + threadIdx.x] = h[threadIdx.x];
+    p.hist[threadIdx.x * kRsGrid + blockIdx.x] = h[threadIdx.x];  // digit-major: k_rs_offsets scans a digit's row
 }
 
-// one block, thread d = digit d: start of block b's digit-d items = (items of smaller digits) + (digit-d items of
-// blocks before b)
-__global__ void __launch_bounds__(kBlockThreads) k_rs_offsets(int* __restrict__ hist) {
-    __shared__ int tot[kRsBins];
-    const int d = threadIdx.x;
-    int t = 0;
-#pragma unroll 16
-    for (int b = 0; b < kRsGrid; ++b) t += hist[b * kRsBins + d];
-    tot[d] = t;
+// block d = digit d, thread b = block b of the histogram kernel: the exclusive scan of row d over the blocks (in
+// place), and the digit's total in tot[d] (the scatter kernel turns the totals into digit starts)
+__global__ void __launch_bounds__(kRsGrid) k_rs_offsets(int* __restrict__ hist, int* __restrict__ tot) {
+    __shared__ int wsum[kRsGrid / 64];
+    int* row = hist + (size_t)blockIdx.x * kRsGrid;
+    const int b = threadIdx.x, lane = b & 63, w = b >> 6;
+    const int v = row[b];
+    int x = v;  // inclusive wave scan
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        x += lane >= off ? y : 0;
+    }
+    if (lane == 63) wsum[w] = x;
     __syncthreads();
-    // exclusive scan of the digit totals (Hillis-Steele over 256 entries)
-    for (int off = 1; off < kRsBins; off <<= 1) {
-        const int v = d >= off ? tot[d - off] : 0;
-        __syncthreads();
-        tot[d] += v;
-        __syncthreads();
-    }
-    int run = tot[d] - t;
-#pragma unroll 16
-    for (int b = 0; b < kRsGrid; ++b) {
-        const int v = hist[b * kRsBins + d];
-        hist[b * kRsBins + d] = run;
-        run += v;
-    }
+    int base = 0;
+#pragma unroll
+    for (int i = 0; i < kRsGrid / 64; ++i) base += i < w ? wsum[i] : 0;
+    row[b] = base + x - v;
+    if (b == kRsGrid - 1) tot[blockIdx.x] = base + x;
 }
 
 __device__ __forceinline__ int rs_lane() {
@@ -145,19 +159,37 @@ __global__ void __launch_bounds__(kBlockThreads) k_rs_scatter(RsPass p) {
     const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
     const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
     const unsigned mask = (1u << p.nbits) - 1u;
-    int run = p.hist[blockIdx.x * kRsBins + tid];  // this thread's digit (tid): next output index
+    {  // the digits' starts: exclusive scan of the digit totals (Hillis-Steele over the 256 digits, in wpre[0])
+        int* sc = wpre[0];
+        sc[tid] = p.tot[tid];
+        __syncthreads();
+        for (int off = 1; off < kRsBins; off <<= 1) {
+            const int y = tid >= off ? sc[tid - off] : 0;
+            __syncthreads();
+            sc[tid] += y;
+            __syncthreads();
+        }
+    }
+    // this thread's digit (tid): next output index
+    int run = wpre[0][tid] - p.tot[tid] + p.hist[tid * kRsGrid + blockIdx.x];
+    __syncthreads();
     const int S2 = shard_stride(n, kShards);      // the sorted queue: item k' at shard k' / S2
     if (DST != DST_ARRAY && blockIdx.x == 0 && tid < kShards) {
         const int cc = n - tid * S2;
         p.len[tid * kQStride] = cc < 0 ? 0 : (cc > S2 ? S2 : cc);
     }
     const uint64_t lt = (1ull << lane) - 1ull;
+    // software-pipelined over the tiles: tile t + 1's (key, value) are loaded before tile t's ranking, whose
+    // barriers wait for LDS only (lds_barrier)
+    unsigned key_n = 0;
+    int val_n = 0;
+    if (b0 + tid < b1) rs_load<SRC>(p, b0 + tid, key_n, val_n);
     for (int t0 = b0; t0 < b1; t0 += kRsTile) {  // (block-uniform trip count)
         const int k = t0 + tid;
         const bool valid = k < b1;
-        unsigned key = 0;
-        int val = 0;
-        if (valid) rs_load<SRC>(p, k, key, val);
+        const unsigned key = key_n;
+        const int val = val_n;
+        if (k + kRsTile < b1) rs_load<SRC>(p, k + kRsTile, key_n, val_n);
         const unsigned dg = (key >> p.shift) & mask;
         // lanes of this wave with the same digit: AND over the digit's bits of (ballot of the bit, or its complement)
         uint64_t m = __ballot(valid);
@@ -168,9 +200,9 @@ __global__ void __launch_bounds__(kBlockThreads) k_rs_scatter(RsPass p) {
         const int rank = __popcll(m & lt);
 #pragma unroll
         for (int i = 0; i < NW; ++i) wcnt[i][tid] = 0;
-        __syncthreads();
+        lds_barrier();
         if (valid && rank == 0) wcnt[w][dg] = __popcll(m);  // the digit's lowest lane reports the wave's count
-        __syncthreads();
+        lds_barrier();
         {  // digit tid: prefix over the tile's waves, then carry the running count
             int r = run;
 #pragma unroll
@@ -180,22 +212,14 @@ __global__ void __launch_bounds__(kBlockThreads) k_rs_scatter(RsPass p) {
             }
             run = r;
         }
-        __syncthreads();
+        lds_barrier();
         if (valid) {
             const int dst = wpre[w][dg] + rank;
             if constexpr (DST == DST_ARRAY) {
                 p.keys_out[dst] = key;
                 p.vals_out[dst] = val;
             } else {
-                const int pos = (dst / S2) * p.S + dst % S2;
-                if constexpr (DST == DST_RAYQ) {
-                    const float4 oj = p.o[2 * val], dj = p.o[2 * val + 1];
-                    p.so[2 * pos] = oj;
-                    p.so[2 * pos + 1] = dj;
-                    p.ss[pos] = __float_as_int(oj.w);  // bounce rays carry their slot in o.w
-                } else {
-                    p.nslot[pos] = val;
-                }
+                p.nslot[(dst / S2) * p.S + dst % S2] = val;
             }
         }
         // (wcnt / wpre are rewritten only after the next tile's first barrier)
@@ -205,7 +229,7 @@ __global__ void __launch_bounds__(kBlockThreads) k_rs_scatter(RsPass p) {
 template <int SRC, int DST>
 void rs_launch(hipStream_t st, const RsPass& p) {
     hipLaunchKernelGGL(k_rs_hist<SRC>, dim3(kRsGrid), dim3(kBlockThreads), 0, st, p);
-    hipLaunchKernelGGL(k_rs_offsets, dim3(1), dim3(kBlockThreads), 0, st, p.hist);
+    hipLaunchKernelGGL(k_rs_offsets, dim3(kRsBins), dim3(kRsGrid), 0, st, p.hist, p.tot);
     hipLaunchKernelGGL((k_rs_scatter<SRC, DST>), dim3(kRsGrid), dim3(kBlockThreads), 0, st, p);
 }
 
@@ -234,28 +258,28 @@ hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* k
 
 }  // namespace
 
-size_t sort_temp_bytes() { return sizeof(int) * ((size_t)kRsGrid * kRsBins + 64); }
+size_t sort_temp_bytes() { return sizeof(int) * ((size_t)kRsGrid * kRsBins + kRsBins + 64); }
 
 hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io) {
     RsPass p{};
     int* hist = static_cast<int*>(io.temp);
     p.hist = hist;
-    p.meta = hist + (size_t)kRsGrid * kRsBins;
+    p.tot = hist + (size_t)kRsGrid * kRsBins;
+    p.meta = p.tot + kRsBins;
     p.S = io.S;
     p.qkey = io.qkey;
-    p.o = io.o;
-    p.so = io.so;
-    p.ss = io.ss;
+    p.nslot = io.perm;
     p.len = io.len;
     const int bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
-    return rs_sort<SRC_RAYQ, DST_RAYQ>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
+    return rs_sort<SRC_RAYQ, DST_PERM>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io) {
     RsPass p{};
     int* hist = static_cast<int*>(io.temp);
     p.hist = hist;
-    p.meta = hist + (size_t)kRsGrid * kRsBins;
+    p.tot = hist + (size_t)kRsGrid * kRsBins;
+    p.meta = p.tot + kRsBins;
     p.S = io.S;
     p.qkey = io.key;
     p.qslot = io.slot;

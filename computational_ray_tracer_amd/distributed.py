@@ -6,6 +6,10 @@ accumulates its pixels' samples in the reference's per-pixel index order.  The o
 reduce of the full-frame {r,g,b,w} films to rank 0 (RCCL over xGMI on MI355X; gloo on CPU in tests).
 Each pixel has exactly one non-zero contributor, so the reduced film is bit-identical to a 1-GPU render.
 """
+import os
+import time
+from datetime import timedelta
+
 import numpy as np
 
 
@@ -68,3 +72,58 @@ def reduce_film(film, dst=0):
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM)
     return film
+
+
+def init_distributed(backend="nccl", timeout_s=None, device_id=None):
+    """One process per GPU (torchrun's RANK / WORLD_SIZE / MASTER_* environment).  Every collective gets a finite
+    timeout (RTMI_DIST_TIMEOUT seconds, default 300) and, on RCCL, asynchronous error handling that tears the process
+    down, so a rank that dies or hangs makes the others fail with a non-zero exit instead of waiting forever.
+    Returns (world, rank)."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("RTMI_DIST_TIMEOUT", "300"))
+        if backend == "nccl":
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        kw = {"timeout": timedelta(seconds=timeout_s)}
+        if device_id is not None:
+            kw["device_id"] = device_id
+        dist.init_process_group(backend, **kw)
+    return world, rank
+
+
+def timed_steps(step, steps, warmup, sync, samples, reset=None):
+    """bench.py's timed region, shared with the multi-process CPU tests: `warmup` untimed steps, then exactly `steps`
+    steps bracketed by barrier + `sync()` on both sides; the wall time is the MAX over ranks and the per-rank sample
+    counts (`samples()` after the timed steps, `reset()` before them) are gathered to every rank.
+    Returns dict(dt=max seconds, total=samples over all ranks, ranks=[{rank, samples, s}, ...])."""
+    import torch
+    import torch.distributed as dist
+    multi = dist.is_initialized() and dist.get_world_size() > 1
+    for _ in range(warmup):
+        step()
+    sync()
+    if reset:
+        reset()
+    if multi:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if multi:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    mine = float(samples())
+    if not multi:
+        return {"dt": dt, "total": mine, "ranks": [{"rank": 0, "samples": int(mine), "s": round(dt, 6)}]}
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    v = torch.tensor([mine, dt], dtype=torch.float64, device=dev)
+    allv = [torch.zeros_like(v) for _ in range(dist.get_world_size())]
+    dist.all_gather(allv, v)
+    ranks = [{"rank": r, "samples": int(x[0].item()), "s": round(float(x[1].item()), 6)} for r, x in enumerate(allv)]
+    return {"dt": max(r["s"] for r in ranks), "total": float(sum(r["samples"] for r in ranks)), "ranks": ranks}

@@ -18,11 +18,11 @@ import json
 from pathlib import Path
 
 KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_nee", "k_path_nee_fb", "k_path_shadow", "k_generate",
-           "k_path_film", "k_ref_shade_film", "k_sort_keys", "k_sort_gather")
+           "k_path_film", "k_ref_shade_film", "k_rs_hist", "k_rs_scatter", "k_rs_offsets")
 
 
 def kname(raw):
-    full = raw.split("(")[0].replace("void ", "")
+    full = raw.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     base = full.split("<")[0].split("::")[-1]
     if base == "k_path_nee" and full.replace(" ", "").endswith(",true>"):
         return "k_path_nee_fb"  # the exact-traversal fallback instantiation (undecided vertices), not the NEE pass
@@ -45,6 +45,8 @@ def main():
     p.add_argument("--tag", required=True)
     p.add_argument("--dir", required=True)
     p.add_argument("--out")
+    p.add_argument("--lib", default="computational_ray_tracer_amd/lib/librtmi355x.so",
+                   help="the library build the runs used (its id is stamped into the output)")
     a = p.parse_args()
     d = Path(a.dir)
     fetch = per_dispatch(d / "fetch", "FETCH_SIZE")
@@ -55,7 +57,9 @@ def main():
     for f in glob.glob(str(d / "kt" / "**" / "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             avg_ns[kname(r["Name"])] = float(r["AverageNs"])
+    import hashlib
     out = {"tag": a.tag, "config": a.config, "lanes": 1,
+           "lib_sha16": hashlib.sha256(Path(a.lib).read_bytes()).hexdigest()[:16],
            "units": "per launch (mean over the run's dispatches); bytes; wave-level instructions",
            "correction": "FETCH_SIZE x2 (gfx950 half-count of 16 B/lane reads), KiB -> bytes x1024",
            "kernels": {}}
