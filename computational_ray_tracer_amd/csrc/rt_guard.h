@@ -15,7 +15,8 @@
 namespace rtmi {
 
 // Test hook: RTMI_FAULT_INJECT=bad_alloc | system_error | runtime | other makes every guarded entry point throw that
-// exception inside its firewall (tests/test_abi_firewall.py).  Read per call: entry points are not hot.
+// exception inside its firewall (tests/test_abi_firewall.py).  Read per call: entry points are not hot.  The release
+// entry points (rt_destroy, rt_mesh_free) are exempt: an injected fault there would only leak what they free.
 inline void fault_injection_point() {
     const char* f = std::getenv("RTMI_FAULT_INJECT");
     if (!f || !*f) return;
@@ -26,12 +27,12 @@ inline void fault_injection_point() {
 }
 
 template <class Body, class OnError>
-int guarded(Body&& body, OnError&& on_error) noexcept {
+int guarded(Body&& body, OnError&& on_error, bool inject = true) noexcept {
     const char* what = nullptr;
     std::string msg;
     int code = RT_E_STATE;
     try {
-        fault_injection_point();
+        if (inject) fault_injection_point();
         return body();
     } catch (const std::bad_alloc&) {
         code = RT_E_OOM;

@@ -2040,11 +2040,12 @@ static int film_set_one(rt_ctx* c, const rt_film_desc* d) {
         return fail(c, RT_E_ARG, "unknown sensor or sensor illuminant");
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);  // queued passes may still read the old tables
+    int y_int = 0;  // committed with the film descriptor below, only once the sensor is set up
     {  // RayTracerTestApp.h:289-291 divides in float; the kernels may divide integers where that is identical
         const int w = d->res_x, n = d->res_x * d->res_y;
         int ok = 1;
         for (int p = 0; p < n && ok; ++p) ok = (int)std::floor((float)p / (float)w) == p / w;
-        c->film_y_int = ok;
+        y_int = ok;
     }
     int rc = setup_sensor(c, *d);
     if (rc) return rc;
@@ -2058,6 +2059,7 @@ static int film_set_one(rt_ctx* c, const rt_film_desc* d) {
         c->cdf_n = n;
     }
     c->film = *d;
+    c->film_y_int = y_int;
     c->have_film = true;
     c->work_dirty = true;
     return RT_OK;
@@ -2549,7 +2551,7 @@ int rt_set_shard(rt_ctx* c, int tile_size, int n_shards, int shard_id) {
     return guarded([&] { return impl_rt_set_shard(c, tile_size, n_shards, shard_id); }, [&](const std::string& m) { set_error(c, m); });
 }
 void rt_destroy(rt_ctx* c) {
-    guarded([&] { impl_rt_destroy(c); return 0; }, [](const std::string&) {});
+    guarded([&] { impl_rt_destroy(c); return 0; }, [](const std::string&) {}, /*inject=*/false);
 }
 
 }  // extern "C"

@@ -218,7 +218,7 @@ int rt_image_write(const char* path, int w, int h, const uint8_t* rgb, int flip_
     return guarded([&] { return impl_rt_image_write(path, w, h, rgb, flip_y); }, [](const std::string&) {});
 }
 void rt_mesh_free(rt_mesh* m) {
-    guarded([&] { impl_rt_mesh_free(m); return 0; }, [](const std::string&) {});
+    guarded([&] { impl_rt_mesh_free(m); return 0; }, [](const std::string&) {}, /*inject=*/false);
 }
 
 }  // extern "C"

@@ -39,7 +39,7 @@ def test_host_entry_points_return_status(lib, monkeypatch, tmp_path, kind, code)
     opt = capi.rt_options()
     assert lib.rt_create(C.byref(opt), C.byref(ctx)) == code
     assert not ctx
-    lib.rt_destroy(None)       # void entry points swallow the fault
+    lib.rt_destroy(None)       # the release entry points are exempt from the injection (NULL: no-op)
     lib.rt_mesh_free(None)
     monkeypatch.delenv("RTMI_FAULT_INJECT")
     assert lib.rt_rgb_to_sigmoid(rgb, coeffs) == capi.RT_OK

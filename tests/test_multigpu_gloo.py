@@ -74,3 +74,86 @@ def test_gloo_two_ranks_equal_single_rank(oracle_lib):
     part = np.zeros_like(acc)
     part[pix0] = o.render(0, 2)[pix0]
     assert np.array_equal(acc.view(np.uint32), part.view(np.uint32))
+
+
+def _timed_worker(rank, world, port, q):
+    """bench.py's timed region (distributed.timed_steps) on a frame loop spanning more than one frame: 6 steps of 2
+    indices (one per rank) over frames of 4, after 1 warmup step -> frames complete at steps 2, 4 and 6."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from computational_ray_tracer_amd.distributed import init_distributed, timed_steps
+    w, r = init_distributed("gloo", timeout_s=120)
+    assert (w, r) == (world, rank)
+    from oracle.oracle import OracleScene
+    cfg = scene.cfg_cornell(res=(40, 24), spp_side=2)
+    o = OracleScene(cfg)
+    pix = shard_pixels(cfg.film.res, 16, world, rank)
+    acc = torch.zeros((40 * 24, 4), dtype=torch.float32)
+    loop = FrameLoop(4, 2, acc, dst=0)
+    done = {"samples": 0}
+
+    def render(i0, i1, f):
+        f.add_(torch.from_numpy(o.render(i0, i1, nthreads=2, pixel_ids=pix)))
+        done["samples"] += (i1 - i0) * len(pix)
+
+    tm = timed_steps(lambda: loop.step(render), 6, 1, lambda: None, lambda: done["samples"],
+                     lambda: done.update(samples=0))
+    if rank == 0:
+        q.put((tm, loop.frames_done, loop.frame.numpy().copy(), len(pix)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_timed_steps_over_several_frames(oracle_lib):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_timed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    tm, frames, frame, npix0 = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert frames == 3  # warmup (1 step) + 6 timed steps of 2 indices over 4-index frames: frames end at 2, 4, 6
+    assert [r["rank"] for r in tm["ranks"]] == [0, 1]
+    assert tm["ranks"][0]["samples"] == 6 * 2 * npix0
+    assert tm["total"] == 6 * 2 * 40 * 24 and tm["dt"] == max(r["s"] for r in tm["ranks"])
+    # the last completed frame (indices 0..3, rendered as two 2-index steps) equals the single-rank render
+    cfg = scene.cfg_cornell(res=(40, 24), spp_side=2)
+    o = oracle_lib.OracleScene(cfg)
+    two = o.render(0, 2) + o.render(2, 4)
+    assert np.array_equal(frame.view(np.uint32), two.view(np.uint32))
+
+
+def _hung_peer_worker(rank, world, port, q):
+    """Rank 1 hangs (never reaches the timed region's barrier); rank 0's collectives must time out and raise."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from computational_ray_tracer_amd.distributed import init_distributed, timed_steps
+    init_distributed("gloo", timeout_s=5)
+    if rank == 1:
+        time.sleep(600)
+        return
+    t0 = time.time()
+    try:
+        timed_steps(lambda: None, 2, 0, lambda: None, lambda: 0)
+        q.put(("no error", time.time() - t0))
+    except Exception as e:  # noqa: BLE001 — the test checks that it is raised, whatever torch calls it
+        q.put((type(e).__name__, time.time() - t0))
+
+
+def test_gloo_hung_peer_fails_instead_of_hanging():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_hung_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        what, waited = q.get(timeout=120)
+    finally:
+        for p in ps:
+            p.kill()
+            p.join(timeout=30)
+    assert what != "no error"
+    assert waited < 60, waited
