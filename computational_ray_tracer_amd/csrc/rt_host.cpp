@@ -503,6 +503,8 @@ struct rt_ctx {
     int bvh_max_leaf = kBvhMaxLeaf;  // triangles per BVH leaf at most (RTMI_BVH_LEAF)
     int bvh_count[2][2] = {};  // per tile set: BVH nodes, BVH tiles (rt_bvh_export)
     int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
+    int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
+    int anyhit_sort = 1;       // RTMI_ANYHIT_SORT=0: any-hit BVH walks take children in slot order (A/B)
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
@@ -1088,8 +1090,13 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const bool nee = c->dsc.full && c->dsc.n_lights > 0;
     if (nee)
         for (int l = 0; l < lanes; ++l)
-            if ((rc = ensure_nee_workspace(c, c->ws[l], nmax * (size_t)nee_stride(c->dsc.n_lights), 3 * (size_t)ncap)))
-                return rc;  // (the NEE queue, the fallback list, the NEE sort keys: rt_internal.h NeeIO)
+            if ((rc = ensure_nee_workspace(c, c->ws[l], nmax * (size_t)nee_stride(c->dsc.n_lights),
+                                           (3 + kMatClasses) * (size_t)ncap)))
+                return rc;  // (the NEE queue, the fallback list, the NEE sort keys: rt_internal.h NeeIO; the
+                            // material bins' index lists: TraceIO bin_idx)
+    // mixed multi-level scenes: the trace kernel bins the hits by material class and each class is shaded by a kernel
+    // holding only its materials' code (k_path_shade_full<Q, 1 / 2>)
+    const bool bins = nee && c->dsc.qcap != 1 && c->mat_bins;
     // Concurrent lanes share the CUs.  Each launch still asks for every resident block (grid_div 1): the dispatcher
     // hands blocks to whichever lane's kernel has them pending, so a VALU-bound trace and an HBM-bound shade of the
     // other lane end up co-resident (Cornell A/B: 1 lane 1217, 2 lanes with half grids 1422, with full grids 1500)
@@ -1151,6 +1158,8 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                                                 : QueueView{qc_cur + kQLen, Sq[l], 0, nsh};
                 const DevScene dsl = lane_scene(c, w);
                 TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
+                BinIO bio{qv, w.hitPrim, {w.neeSlot + 3 * ncap, w.neeSlot + 4 * ncap}, qc_cur + kQBinLen};
+                static_assert(kMatClasses == 2, "bin index lists");
                 if (sort_rays && depth > 0) {  // the device reads the queue length itself: no host round trip
                     SortRaysIO so{w.sQKey, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
                                   c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l]};
@@ -1201,7 +1210,20 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                                 qc_cur + kQNeeFallback, sort_nee ? nee_key : nullptr, c->sort_lo, c->sort_scale,
                                 c->sort_nee_bits};
                 e0 = ev_start(c, s);
-                HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio, nio));
+                if (bins) {  // the hits binned by material, then one kernel per bin over its index list
+                    HIPCHK(c, launch_bin_materials(s, grid, dsl, bio));
+                    for (int cl = 0; cl < kMatClasses; ++cl) {
+                        PathIO bp = pio;
+                        bp.q = QueueView{qc_cur + kQBinLen + cl * kShards * kQStride, Sq[l], 0, nsh};
+                        bp.ticket = qc_cur + kQBinTicket + cl * kShards * kQStride;
+                        bp.bin_idx = bio.idx[cl];
+                        HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, bp, c->d_ctr,
+                                                    sqio, nio, 1 + cl));
+                    }
+                } else {
+                    HIPCHK(c, launch_path_shade(s, grid, c->dsc.qcap, dsl, c->d_spec, smp, fd, ids, pio, c->d_ctr, sqio,
+                                                nio));
+                }
                 ev_mark(c, s, ST_SHADE, e0);
                 if (sort_nee) {  // NEE vertices in Morton order of their shading points (no host round trip)
                     SortNeeIO so{w.neeSlot, qc_cur + kQShadowLen, Sq[l], nee_key, w.sKeys, w.sKeysAlt, w.sVals,
@@ -1508,6 +1530,8 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_BVH_CI")) c->bvh_node_cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_BVH_LEAF")) c->bvh_max_leaf = std::max(1, std::min(15, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
+    if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
+    if (const char* e = std::getenv("RTMI_ANYHIT_SORT")) c->anyhit_sort = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) {
         int db = 3, ob = 4, om = -1;
         const int got = std::sscanf(e, "%d/%d/%d", &db, &ob, &om);
@@ -1854,7 +1878,8 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     std::vector<DevMaterial> mats;
     for (int i = 0; i < s->n_materials; ++i) {
         const rt_material& m = s->materials[i];
-        mats.push_back(DevMaterial{m.sigmoid[0], m.sigmoid[1], m.sigmoid[2], m.emission_scale, m.type, m.eta, -1, 0});
+        const int cls = m.emission_scale > 0 || m.type == RT_MAT_DIFFUSE ? 0 : 1;  // material bin (kMatClasses)
+        mats.push_back(DevMaterial{m.sigmoid[0], m.sigmoid[1], m.sigmoid[2], m.emission_scale, m.type, m.eta, -1, cls});
     }
     if (mats.empty()) mats.push_back(DevMaterial{0.f, 0.f, 0.f, 0.f, RT_MAT_DIFFUSE, 0.f, -1, 0});
     std::vector<DevShape> shapes(s->n_shapes);
@@ -1981,6 +2006,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     }
     d.wabs = wabs;
     d.oguard = oguard;
+    d.anyhit_sort = c->anyhit_sort;
     d.amb_force = c->force_amb >= 0;
     d.amb_mask = c->force_amb > 0 ? (1u << c->force_amb) - 1u : 0u;
     c->info.bvh_nodes = bvh_nodes0;

@@ -93,7 +93,7 @@ struct DevMaterial {                // rt_material + the area light it feeds (MI
     int type;
     float eta;
     int light;
-    int pad;
+    int cls;                        // material bin: 0 Lambert or emitter, 1 mirror or dielectric (kMatClasses)
 };
 
 struct DevShape {                   // rt_shape (Shapes.h:209-907)
@@ -139,6 +139,7 @@ struct DevScene {
     float wabs;                     // canonical-rule window W(t) = t 2^-16 + wabs
     float oguard;                   // rays whose origin has a coordinate beyond +-oguard are ambiguous (the box
                                     // padding covers the slab test's rounding only for origins inside 8 M)
+    int anyhit_sort;                // any-hit walks visit children nearest-first (RTMI_ANYHIT_SORT=0: slot order)
     unsigned amb_mask;              // test knob (RTMI_FORCE_AMB=k): with amb_force set, rays whose direction-bit hash
     int amb_force;                  // has its low k bits zero are declared ambiguous (exercises every fallback path)
 };
@@ -220,7 +221,11 @@ static const int kShards = 8;
 static const int kQStride = 64;
 enum { kQLen = 0, kQTraceTicket = 1 * kShards * kQStride, kQShadeTicket = 2 * kShards * kQStride,
        kQShadowLen = 3 * kShards * kQStride, kQShadowTicket = 4 * kShards * kQStride,
-       kQNeeFallback = 5 * kShards * kQStride, kQRegion = 6 * kShards * kQStride };
+       kQNeeFallback = 5 * kShards * kQStride,
+       // material bins of a mixed multi-level scene's bounce (TraceIO bin_*): class c's shard lengths at
+       // kQBinLen + c kShards kQStride, the chunk tickets of its shade kernel at kQBinTicket + c kShards kQStride
+       kQBinLen = 6 * kShards * kQStride, kQBinTicket = 8 * kShards * kQStride, kQRegion = 10 * kShards * kQStride };
+static const int kMatClasses = 2;  // material bins: 0 Lambert or emitter (NEE), 1 mirror or dielectric
 // Shard stride of a queue of ns shards for n items (a multiple of 64, so wave chunks stay line-aligned); capacity
 // ns * S.  Single-leaf scenes (static chunks, one block append per 256 rays) keep one shard: sharding their queues
 // cost the Cornell box 3 %; multi-level scenes (per-wave tickets and appends) use kShards (CFG3 +5.5 %).
@@ -253,6 +258,17 @@ struct TraceIO {
     float4* so = nullptr;
 };
 
+// Material binning of a mixed multi-level scene's bounce (k_bin_materials, after the trace): every hit's queue
+// position is appended to the index list of its material class (idx[c], sharded like the queue, shard lengths at
+// len + c kShards kQStride); misses end their paths there.
+struct BinIO {
+    QueueView q;             // the traced queue
+    const int* hitPrim;
+    int* idx[kMatClasses];
+    int* len;
+};
+hipError_t launch_bin_materials(hipStream_t st, int grid, const DevScene& sc, const BinIO& io);
+
 struct ShadeRefIO {
     const int* work_pixels; int n_pixels; int n_index;
     const float4* rayD; const float4* lamA; const float4* lamB; const float4* pdfA; const float4* pdfB;
@@ -281,6 +297,7 @@ struct PathIO {
                 // two Get2D); -1: per slot in R_MISC
     int* ticket;  // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
     RayKeyIO nkey;  // multi-level scenes: the coherence-sort key of every appended ray (rt_sort.hip)
+    const int* bin_idx = nullptr;  // material-binned shade: item i of q is queue position bin_idx[i] (BinIO)
 };
 
 // Shadow queue (multi-level octrees): the shade kernel appends NEE shadow rays {o, tMax}, {d, slot} and their
@@ -401,10 +418,11 @@ hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* 
                           const ShadeRefIO& sio, const RecordIO& io);
 hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, const DevScene& sc, const PathIO& io,
                               const ShadowQueueIO& shq, unsigned long long* ctr);
+// matclass (mixed scenes): 0 every material in one kernel; 1 / 2 the Lambert-or-emitter / specular bin (io.bin_idx)
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
                              unsigned long long* ctr, const ShadowQueueIO& shq = ShadowQueueIO{},
-                             const NeeIO& nee = NeeIO{});
+                             const NeeIO& nee = NeeIO{}, int matclass = 0);
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr);
 hipError_t launch_path_nee_fallback(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,

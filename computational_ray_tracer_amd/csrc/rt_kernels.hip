@@ -623,7 +623,6 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 // error-bound tail run per candidate, not once per triangle for whichever lane reached it
                 uint64_t cand = 0;
                 int k = 0;
-                int ntest = r.y;  // candidate tests this lane executes (the culled paths test only hit clusters)
                 const uint64_t fp = sc.fan_pairs[set];  // bit k: leaf tiles k, k+1 share vertices (a,b,c),(a,c,d)
                 // conservative cluster boxes first: a cluster no lane of the wave reaches is skipped whole
                 // (closest hit: the box over [0, inf); any hit: over [0, tMax], exact for a fixed tMax).  Shadow rays
@@ -653,7 +652,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         cw.cand[ln] = 0;
                         int np = 0;
                         const uint32_t hm = cluster_mask(cl, ncl, far, o, inv, cl_t);
-                        ntest = cluster_tris(hm, ncl, r.y);
+                        nt += cluster_tris(hm, ncl, r.y);  // executed tests: the hit clusters' (the reference: all)
                         for (int c = 0; c < ncl; ++c) {
                             const bool hb = (hm >> c) & 1u;
                             uint64_t m = __ballot(hb);
@@ -686,7 +685,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                         k = r.y;
                     } else {
                     const uint32_t hm = cluster_mask(cl, ncl, far, o, inv, cl_t);
-                    ntest = cluster_tris(hm, ncl, r.y);
+                    nt += cluster_tris(hm, ncl, r.y);  // executed tests: the hit clusters' (the reference: all)
                     for (int c = 0; c < ncl; ++c) {
                         const bool hb = (hm >> c) & 1u;
                         if (__ballot(hb) == 0) continue;
@@ -710,6 +709,7 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     k = r.y;
                     }
                 }
+                nt += r.y - k;  // unculled: every triangle's candidate test runs
                 for (; k + U <= r.y; k += U) {
                     int e = 3 * (r.x + k);
                     float4 T[3 * U];
@@ -731,7 +731,6 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     int e = 3 * (r.x + k);
                     if (tri_candidate<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2))) cand |= 1ull << k;
                 }
-                nt += ntest;  // executed tests (the reference tests all r.y of them)
                 while (cand) {
                     int j = __builtin_ctzll(cand);
                     cand &= cand - 1;
@@ -948,7 +947,7 @@ static constexpr unsigned kNoChild = 0xffffffffu;
 struct Bvh8Ray {
     V3 inv, oi;
 };
-__device__ __forceinline__ void node_keys(const BvhNode8& n, const Bvh8Ray& r, float tcut, unsigned k[8]) {
+__device__ __forceinline__ void node_keys(const BvhNode8& n, const Bvh8Ray& r, float tcut, unsigned k[8], bool sort) {
     const unsigned w0 = __float_as_uint(n.N0.w);
     const float sx = ldexpf(r.inv.x, (int)(w0 & 255u) - 127), sy = ldexpf(r.inv.y, (int)((w0 >> 8) & 255u) - 127),
                 sz = ldexpf(r.inv.z, (int)((w0 >> 16) & 255u) - 127);
@@ -974,6 +973,7 @@ __device__ __forceinline__ void node_keys(const BvhNode8& n, const Bvh8Ray& r, f
         const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tcut)) * 1.00000048f;
         k[s] = (((valid >> s) & 1u) && tn <= tf) ? ((__float_as_uint(tn) & 0x7ffffff8u) | (unsigned)s) : kNoChild;
     }
+    if (!sort) return;  // (any-hit walks: any order gives the same answer)
     // Batcher's odd-even merge sort, 19 compare-exchanges
     kswap(k[0], k[1]); kswap(k[2], k[3]); kswap(k[4], k[5]); kswap(k[6], k[7]);
     kswap(k[0], k[2]); kswap(k[1], k[3]); kswap(k[4], k[6]); kswap(k[5], k[7]);
@@ -1001,7 +1001,7 @@ __device__ __forceinline__ int child_word(const BvhNode8& n, unsigned key) {
 // overflow (the ray is then ambiguous).
 template <class LeafFn>
 __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, const Bvh8Ray& r, float& cut, ctr_t& nn,
-                                          LeafFn&& leaf) {
+                                          bool sort, LeafFn&& leaf) {
     uint2* stk = g_bstk + threadIdx.x;
     int sp = 0;
     bool overflow = false;
@@ -1021,7 +1021,7 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
             const BvhNode8 bn = load_node8(nodes, node);
             nn += __popc(bn.N1.w);
             unsigned k[8];
-            node_keys(bn, r, cut, k);
+            node_keys(bn, r, cut, k, sort);
             node = -1;
 #pragma unroll
             for (int i = 7; i >= 1; --i)
@@ -1058,7 +1058,7 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
     const TriRay R = make_triray<KZ>(o, d);
     float cut = tMaxInit, t2 = __builtin_inff();
     int best = -1, second = -1;
-    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, [&](int lf, int lc) {
+    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, true, [&](int lf, int lc) {
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             const float4 A = tp[0], B = tp[1], Cc = tp[2];
@@ -1100,7 +1100,7 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
     const float sure = tMax - canon_window(tMax, sc.wabs);
     bool window = false, occluded = false;
     float cut = tMax;
-    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, [&](int lf, int lc) {
+    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, sc.anyhit_sort != 0, [&](int lf, int lc) {
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             ++nt;
@@ -1249,6 +1249,68 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
     count_add(ctr, C_FALLBACK, nfb);
 }
 
+// Material bins of a mixed multi-level scene's bounce (BinIO): every hit's queue position is appended to the index
+// list of its material class, shard by shard, in queue order within a chunk; misses end their paths here.  A pass
+// over the hit ids of its own (in the trace kernel the appends cost registers the traversal needs).  A block takes
+// chunks of kBinItems x 256 consecutive positions of one shard: it counts each class (wave ballots, LDS), makes ONE
+// atomic per class and chunk (per-wave appends on the 16 shard counters saturated them: 313 us per launch), then
+// writes the positions at their ranks.
+static constexpr int kBinItems = 8;
+__global__ void __launch_bounds__(kBlock) k_bin_materials(DevScene sc, BinIO io) {
+    constexpr int NW = kBlock / 64, CH = kBinItems * kBlock;
+    __shared__ int wc[kMatClasses][kBinItems][NW];  // per (class, item round, wave): count, then exclusive start
+    __shared__ int base[kMatClasses];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int mx = 0;
+#pragma unroll
+    for (int j = 0; j < kShards; ++j) {
+        const int l = j < io.q.ns ? q_len(io.q, j) : 0;
+        mx = l > mx ? l : mx;
+    }
+    const int per_shard = (mx + CH - 1) / CH, nent = io.q.ns * per_shard;
+    for (int e = blockIdx.x; e < nent; e += gridDim.x) {  // entry e = chunk e / ns of shard e % ns
+        const int j = e % io.q.ns, c0 = (e / io.q.ns) * CH, len = q_len(io.q, j);
+        if (c0 >= len) continue;  // (block-uniform)
+        int cls[kBinItems];
+#pragma unroll
+        for (int r = 0; r < kBinItems; ++r) {
+            const int idx = c0 + r * kBlock + (int)threadIdx.x;
+            cls[r] = -1;
+            if (idx < len) {
+                const int prim = io.hitPrim[j * io.q.S + idx];
+                if (prim >= 0)
+                    cls[r] = sc.materials[prim < sc.n_tris ? sc.triMaterial[prim] : sc.shapes[prim - sc.n_tris].material].cls;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kMatClasses; ++c)
+#pragma unroll
+            for (int r = 0; r < kBinItems; ++r) {
+                const uint64_t m = __ballot(cls[r] == c);
+                if (lane == 0) wc[c][r][w] = __popcll(m);
+            }
+        __syncthreads();
+        if (threadIdx.x < kMatClasses) {  // exclusive starts in (round, wave) order, then the chunk's one atomic
+            const int c = threadIdx.x;
+            int t = 0;
+            for (int r = 0; r < kBinItems; ++r)
+                for (int i = 0; i < NW; ++i) { const int v = wc[c][r][i]; wc[c][r][i] = t; t += v; }
+            base[c] = t ? atomicAdd(io.len + (c * kShards + j) * kQStride, t) : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < kMatClasses; ++c)
+#pragma unroll
+            for (int r = 0; r < kBinItems; ++r) {
+                const uint64_t m = __ballot(cls[r] == c);
+                if (cls[r] == c)
+                    io.idx[c][j * io.q.S + base[c] + wc[c][r][w] + __popcll(m & lt)] = j * io.q.S + c0 + r * kBlock + (int)threadIdx.x;
+            }
+        __syncthreads();  // (wc / base are rewritten by the block's next chunk)
+    }
+}
+
 // ======================================================================= K3 reference shading + film
 // RayTracerTestApp.h:218-284 (Li, active branch):  0.3·F1(λ) + clamp(n·(0,0,-1), 0, 1)·(D65(λ)·albedo(λ)),
 // n = object-space interpolated normal flipped against the ray (Shapes.h:1066-1075).
@@ -1372,7 +1434,7 @@ __device__ __forceinline__ bool cosine_bounce(float u0, float u1, V3 nrm, V3& wi
 }
 
 template <int QCAP>
-__global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? 4 : RT_MULTI_WAVES))) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp,
                                                                          DevFilm film, SampleIds ids, PathIO io,
                                                                          unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
@@ -1623,7 +1685,9 @@ __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const f
     count_add(ctr, C_SFALLBACK, nfb);
 }
 
-template <int QCAP>
+// MC (material class): 0 every material; 1 the Lambert-or-emitter bin, 2 the mirror-or-dielectric bin (items of
+// io.bin_idx: hits only, the trace kernel dropped the misses) — each bin kernel holds only its materials' code.
+template <int QCAP, int MC>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(DevScene sc, const DevSpectra* sp,
                                                                               DevSampler smp, DevFilm film,
                                                                               SampleIds ids, PathIO io,
@@ -1638,7 +1702,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
     int qj, qidx;
     bool live;
     while (items.next(qj, qidx, live)) {
-        const int k = qj * io.q.S + qidx;  // queue position
+        int k = qj * io.q.S + qidx;  // queue position (binned: of the item's hit)
+        if (MC != 0 && live) k = io.bin_idx[k];
         bool wantNext = false, wantNee = false;
         unsigned neeKey = 0;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
@@ -1686,7 +1751,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                 }
                 const DevMaterial mt = sc.materials[mid];
                 float prevPdf = rec_prev_pdf(io.rec, slot);
-                if (mt.emit > 0) {  // one-sided pure emitter, ends the path
+                if (MC != 2 && mt.emit > 0) {  // one-sided pure emitter, ends the path
                     if (front) {
                         float L[8];
                         rload8(io.rec, slot, R_L, L);
@@ -1712,7 +1777,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                     float R[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.c0, mt.c1, mt.c2, lam[i]);
-                    if (mt.type == 1) {  // perfect mirror: no sampler draws
+                    if (MC != 1 && mt.type == 1) {  // perfect mirror: no sampler draws
 #pragma unroll
                         for (int i = 0; i < 8; ++i) beta[i] *= R[i];
                         rstore8(io.rec, slot, R_BETA, beta);
@@ -1724,7 +1789,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                     } else {
                         Smp sm;
                         restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed);
-                        if (mt.type == 2) {  // smooth dielectric
+                        if (MC != 1 && mt.type == 2) {  // smooth dielectric
                             if (mt.eta == 0) {  // dispersive BK7: TerminateSecondary (spectrum.h:302-310)
                                 float pdf[8];
                                 load8(io.pdfA, io.pdfB, slot, pdf);
@@ -1758,7 +1823,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                             nO = make_float4(po.x, po.y, po.z, 0.f);
                             nD = make_float4(wi.x, wi.y, wi.z, 0.f);
                             rec_set_prev_pdf(io.rec, slot, 0.f);
-                        } else {  // Lambert: NEE per light (deferred to k_path_nee), then a cosine-hemisphere bounce
+                        } else if constexpr (MC != 2) {  // Lambert: NEE per light (k_path_nee), then a cosine bounce
                             V3 po = vadd(p, vmul(nrm, off));
                             float4* nr = nee.rec + (size_t)slot * nee_f4;
                             float* nwgt = reinterpret_cast<float*>(nr + N_RAY + sc.n_lights);
@@ -1841,10 +1906,12 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                 }
             }
         }
-        const int pe = queue_append<WAVE>(nee.len + qj * kQStride, wantNee, lds) + qj * io.q.S;
-        if (wantNee) {
-            nee.slot[pe] = slot;
-            if (nee.key) nee.key[pe] = neeKey;
+        if constexpr (MC != 2) {
+            const int pe = queue_append<WAVE>(nee.len + qj * kQStride, wantNee, lds) + qj * io.q.S;
+            if (wantNee) {
+                nee.slot[pe] = slot;
+                if (nee.key) nee.key[pe] = neeKey;
+            }
         }
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
@@ -2132,7 +2199,7 @@ hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, cons
 
 hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
-                             unsigned long long* ctr, const ShadowQueueIO& shq, const NeeIO& nee) {
+                             unsigned long long* ctr, const ShadowQueueIO& shq, const NeeIO& nee, int matclass) {
     int gb = grid > 0 ? grid : 1;
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
@@ -2140,9 +2207,15 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
     if (!sc.full && qcap != 1 && !shq.shO) return hipErrorInvalidValue;       // so is the shadow queue
 #define RT_SHADE_CASE(Q)                                                                                         \
     case Q:                                                                                                      \
-        if (sc.full)                                                                                             \
-            hipLaunchKernelGGL(k_path_shade_full<Q>, dim3(resident_grid(k_path_shade_full<Q>, gb, grid)), b, 0, st, \
-                               sc, sp, smp, film, ids, io, nee);                                                 \
+        if (sc.full && Q != 1 && matclass == 1)                                                                 \
+            hipLaunchKernelGGL((k_path_shade_full<Q, 1>), dim3(resident_grid(k_path_shade_full<Q, 1>, gb, grid)), b, 0, \
+                               st, sc, sp, smp, film, ids, io, nee);                                             \
+        else if (sc.full && Q != 1 && matclass == 2)                                                            \
+            hipLaunchKernelGGL((k_path_shade_full<Q, 2>), dim3(resident_grid(k_path_shade_full<Q, 2>, gb, grid)), b, 0, \
+                               st, sc, sp, smp, film, ids, io, nee);                                             \
+        else if (sc.full)                                                                                        \
+            hipLaunchKernelGGL((k_path_shade_full<Q, 0>), dim3(resident_grid(k_path_shade_full<Q, 0>, gb, grid)), b, 0, \
+                               st, sc, sp, smp, film, ids, io, nee);                                             \
         else                                                                                                     \
             hipLaunchKernelGGL(k_path_shade<Q>, dim3(resident_grid(k_path_shade<Q>, gb, grid)), b, 0, st, sc, sp,  \
                                smp, film, ids, io, ctr, shq);                                                    \
@@ -2221,5 +2294,11 @@ hipError_t launch_film_scatter(hipStream_t st, int n, const int* work, const flo
     hipLaunchKernelGGL(k_film_scatter, dim3(grid_for(n, 2048)), dim3(kBlock), 0, st, n, work, in, film);
     return hipGetLastError();
 }
+
+hipError_t launch_bin_materials(hipStream_t st, int grid, const DevScene& sc, const BinIO& io) {
+    hipLaunchKernelGGL(k_bin_materials, dim3(resident_grid(k_bin_materials, grid, grid)), dim3(kBlock), 0, st, sc, io);
+    return hipGetLastError();
+}
+
 
 }  // namespace rtmi
