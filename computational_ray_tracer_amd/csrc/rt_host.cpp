@@ -501,10 +501,11 @@ struct rt_ctx {
     int sort_rays = 1;         // RTMI_SORT=0: no coherence sort (A/B)
     float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
     int bvh_max_leaf = kBvhMaxLeaf;  // triangles per BVH leaf at most (RTMI_BVH_LEAF)
-    int bvh_count[2][2] = {};  // per tile set: BVH nodes, BVH tiles (rt_bvh_export)
+    int bvh_count[3][2] = {};  // per BVH (set 0, set 1, any-hit): nodes, tiles (rt_bvh_export)
+    float bvh_any_cost = 2.f;  // the any-hit BVH's SAH node cost and leaf size (RTMI_BVH_ANY="cost/leaf"; r03 A/B:
+    int bvh_any_leaf = 4;      // 2/4 halves the shadow rays' triangle tests against 3/8: CFG4 +5 %)
     int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
     int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
-    int anyhit_sort = 1;       // RTMI_ANYHIT_SORT=0: any-hit BVH walks take children in slot order (A/B)
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
@@ -1529,9 +1530,16 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_SORT")) c->sort_rays = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BVH_CI")) c->bvh_node_cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_BVH_LEAF")) c->bvh_max_leaf = std::max(1, std::min(15, std::atoi(e)));
+    if (const char* e = std::getenv("RTMI_BVH_ANY")) {
+        float ac = 2.f;
+        int al = 4;
+        if (std::sscanf(e, "%f/%d", &ac, &al) == 2) {
+            c->bvh_any_cost = ac;
+            c->bvh_any_leaf = std::max(1, std::min(15, al));
+        }
+    }
     if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
-    if (const char* e = std::getenv("RTMI_ANYHIT_SORT")) c->anyhit_sort = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) {
         int db = 3, ob = 4, om = -1;
         const int got = std::sscanf(e, "%d/%d/%d", &db, &ob, &om);
@@ -1853,11 +1861,14 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     }
     // multi-level octrees: the fast traversal's BVH per tile set (non-degenerate triangles; set 1 without the
     // back-facing ones) and the canonical-rule window (rt_bvh.cpp)
-    BvhData bvh[2];
+    // [kBvhAny]: the any-hit BVH of the shadow rays (set 0), built with its own SAH cost and leaf size
+    BvhData bvh[3];
     float wabs = 0.f, oguard = 0.f;
-    if (qcap != 1)
+    if (qcap != 1) {
         for (int st = 0; st < (c->cull ? 2 : 1); ++st)
             scene_bvh(sw, st, c->bvh_node_cost, c->bvh_max_leaf, bvh[st], wabs, oguard);
+        scene_bvh(sw, 0, c->bvh_any_cost, c->bvh_any_leaf, bvh[kBvhAny], wabs, oguard);
+    }
     c->info.n_nodes = nn;
     c->info.n_leaf_refs = (int)c->h_refs.size();
     c->info.max_queue_groups = bound;
@@ -1985,10 +1996,10 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     void *pc0 = nullptr, *pc1 = nullptr;
     if ((rc = up(clus[0].data(), clus[0].size() * 16, &pc0)) || (rc = up(clus[1].data(), clus[1].size() * 16, &pc1)))
         return rc;
-    void* pbv[2] = {nullptr, nullptr};
-    void* pbt[2] = {nullptr, nullptr};
+    void* pbv[3] = {nullptr, nullptr, nullptr};
+    void* pbt[3] = {nullptr, nullptr, nullptr};
     const int bvh_nodes0 = (int)(bvh[0].nodes.size() / kBvhNodeF4);
-    for (int st = 0; st < 2; ++st) {
+    for (int st = 0; st < 3; ++st) {
         c->bvh_count[st][0] = (int)(bvh[st].nodes.size() / kBvhNodeF4);
         c->bvh_count[st][1] = (int)(bvh[st].tiles.size() / 3);
         if (bvh[st].nodes.empty()) continue;
@@ -2000,13 +2011,12 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
             return rc;
     }
     DevScene& d = c->dsc;
-    for (int st = 0; st < 2; ++st) {
+    for (int st = 0; st < 3; ++st) {
         d.bvh[st] = (const float4*)(pbv[st] ? pbv[st] : pbv[0]);
         d.btiles[st] = (const float4*)(pbt[st] ? pbt[st] : pbt[0]);
     }
     d.wabs = wabs;
     d.oguard = oguard;
-    d.anyhit_sort = c->anyhit_sort;
     d.amb_force = c->force_amb >= 0;
     d.amb_mask = c->force_amb > 0 ? (1u << c->force_amb) - 1u : 0u;
     c->info.bvh_nodes = bvh_nodes0;
@@ -2238,7 +2248,7 @@ static int impl_rt_octree_export(rt_ctx* c, float* bounds, int32_t* child, int32
 
 // The fast traversal's BVH as uploaded (tile set `set`): counts always, arrays when the pointers are non-null.
 static int impl_rt_bvh_export(rt_ctx* c, int set, int* n_nodes, int* n_tiles, float* consts, float* nodes, float* tiles) {
-    if (!c || set < 0 || set > 1) return RT_E_ARG;
+    if (!c || set < 0 || set > 2) return RT_E_ARG;
     if (!c->have_scene) return fail(c, RT_E_STATE, "no scene");
     if (set == 1 && !c->cull) set = 0;  // the kernels use set 0's arrays when there is no culled set
     if (n_nodes) *n_nodes = c->bvh_count[set][0];
@@ -2256,7 +2266,7 @@ static int impl_rt_bvh_export(rt_ctx* c, int set, int* n_nodes, int* n_tiles, fl
 // build parameters (RTMI_BVH_CI / RTMI_BVH_LEAF as rt_create reads them).  For CPU tests of the traversal.
 static int impl_rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes, int* n_tiles, float* consts,
                                    float* nodes, float* tiles) {
-    if (!s || set < 0 || set > 1 || s->n_triangles <= 0 || s->n_vertices <= 0 || !s->positions || !s->indices)
+    if (!s || set < 0 || set > 2 || s->n_triangles <= 0 || s->n_vertices <= 0 || !s->positions || !s->indices)
         return RT_E_ARG;
     if (s->cull_backfaces && !s->normals) return RT_E_ARG;
     for (int t = 0; t < 3 * s->n_triangles; ++t)
@@ -2265,11 +2275,20 @@ static int impl_rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes
     int leaf = kBvhMaxLeaf;
     if (const char* e = std::getenv("RTMI_BVH_CI")) cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_BVH_LEAF")) leaf = std::max(1, std::min(15, std::atoi(e)));
+    if (set == kBvhAny) {  // rt_create's defaults / RTMI_BVH_ANY for the any-hit BVH
+        cost = 2.f;
+        leaf = 4;
+        if (const char* e = std::getenv("RTMI_BVH_ANY")) {
+            float ac = 2.f;
+            int al = 4;
+            if (std::sscanf(e, "%f/%d", &ac, &al) == 2) { cost = ac; leaf = std::max(1, std::min(15, al)); }
+        }
+    }
     SceneWorld sw;
     scene_world(s, sw);
     BvhData b;
     float wabs = 0.f, oguard = 0.f;
-    scene_bvh(sw, s->cull_backfaces ? set : 0, cost, leaf, b, wabs, oguard);
+    scene_bvh(sw, set == 1 && s->cull_backfaces ? 1 : 0, cost, leaf, b, wabs, oguard);
     if (n_nodes) *n_nodes = (int)(b.nodes.size() / kBvhNodeF4);
     if (n_tiles) *n_tiles = (int)(b.tiles.size() / 3);
     if (consts) { consts[0] = wabs; consts[1] = oguard; }

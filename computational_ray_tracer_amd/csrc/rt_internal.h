@@ -134,12 +134,11 @@ struct DevScene {
     // multi-level octrees (qcap != 1): the fast traversal's 8-wide compressed BVH per tile set (rt_bvh.cpp:
     // kBvhNodeF4 float4 per node) and its leaf-ordered triangle tiles; rays it finds ambiguous fall back to the
     // octree BFS
-    const float4* bvh[2];
-    const float4* btiles[2];
+    const float4* bvh[3];           // [0], [1]: closest-hit BVH of tile set 0 / 1; [kBvhAny]: the any-hit BVH (set 0,
+    const float4* btiles[3];        // smaller leaves: shadow rays test fewer triangles)
     float wabs;                     // canonical-rule window W(t) = t 2^-16 + wabs
     float oguard;                   // rays whose origin has a coordinate beyond +-oguard are ambiguous (the box
                                     // padding covers the slab test's rounding only for origins inside 8 M)
-    int anyhit_sort;                // any-hit walks visit children nearest-first (RTMI_ANYHIT_SORT=0: slot order)
     unsigned amb_mask;              // test knob (RTMI_FORCE_AMB=k): with amb_force set, rays whose direction-bit hash
     int amb_force;                  // has its low k bits zero are declared ambiguous (exercises every fallback path)
 };
@@ -160,6 +159,7 @@ __host__ __device__ inline size_t ctr_word(int slot, int sub) { return ((size_t)
 static const int kBvhNodeF4 = 8, kBvhNodeRead = 5;  // float4 per node / float4 the kernels read (N0..N4)
 static const int kBvhTopLevels = 2, kBvhTopNodes = 9;
 static const int kBvhMaxLeaf = 8;                     // triangles per leaf (SAH may stop earlier)
+static const int kBvhAny = 2;                         // DevScene bvh / btiles index of the any-hit BVH
 struct BvhData {
     std::vector<float4> nodes, tiles;
     int depth = 0, max_leaf = 0;

@@ -54,15 +54,18 @@ __device__ __forceinline__ void stage_leaf1(const DevScene& sc, int set) {
 // each; rt_bvh.cpp emit_root), which every ray opens, staged in LDS at kernel start by every kernel that traverses
 // the BVH
 __shared__ float4 g_top[kBvhNodeRead * kBvhTopNodes];
-template <int QCAP>
+// ANY: the kernel's BVH walks are any-hit queries, which walk the any-hit BVH (sc.bvh[kBvhAny]); otherwise the
+// closest-hit BVH of tile set `set`
+template <int QCAP, bool ANY = true>
 __device__ __forceinline__ void stage_scene(const DevScene& sc, int set) {
     if constexpr (QCAP == 1) {
         stage_leaf1(sc, set);
     } else {
         // (the host pads every node array to at least kBvhTopNodes nodes)
-        if (sc.bvh[set])
+        const float4* b = sc.bvh[ANY ? kBvhAny : set];
+        if (b)
             for (int i = threadIdx.x; i < kBvhNodeRead * kBvhTopNodes; i += blockDim.x)
-                g_top[i] = sc.bvh[set][(i / kBvhNodeRead) * kBvhNodeF4 + i % kBvhNodeRead];
+                g_top[i] = b[(i / kBvhNodeRead) * kBvhNodeF4 + i % kBvhNodeRead];
         __syncthreads();
     }
 }
@@ -999,10 +1002,16 @@ __device__ __forceinline__ int child_word(const BvhNode8& n, unsigned key) {
 // (child word, key) (an entry whose entry distance lies beyond the current cut is dropped when popped); leaves are
 // handed to `leaf(lf, lc)`, which may lower the cut and returns true to end the walk.  Returns false on a stack
 // overflow (the ray is then ambiguous).
-template <class LeafFn>
+// ANY (any-hit, fixed cut): the entries are the child words alone — every pushed child was entered within the fixed
+// tMax, so there is nothing to cull on pop — and the same LDS column holds twice as many of them (2 kBvhStack).
+template <bool ANY, class LeafFn>
 __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, const Bvh8Ray& r, float& cut, ctr_t& nn,
                                           bool sort, LeafFn&& leaf) {
+    constexpr int CAP = ANY ? 2 * kBvhStack : kBvhStack;
     uint2* stk = g_bstk + threadIdx.x;
+    // (ANY) entry e at word (e / 2) 2 kBlock + e % 2 of this thread's OWN uint2 column: the exact-BFS fallback of a
+    // concurrent wave reuses its own column (traverse's LDS FIFO), so no thread may step outside its column
+    unsigned* stw = reinterpret_cast<unsigned*>(g_bstk + threadIdx.x);
     int sp = 0;
     bool overflow = false;
     int node = 0, lf = 0, lc = 0;
@@ -1011,9 +1020,15 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
         while (lc == 0) {
             if (node < 0) {
                 if (sp == 0) break;
-                const uint2 e = stk[--sp * kBlock];
-                if (__uint_as_float(e.y & 0x7ffffff8u) > cut) continue;  // entered beyond the current cut
-                const int w = (int)e.x;
+                int w;
+                if constexpr (ANY) {
+                    --sp;
+                    w = (int)stw[(sp >> 1) * (2 * kBlock) + (sp & 1)];
+                } else {
+                    const uint2 e = stk[--sp * kBlock];
+                    if (__uint_as_float(e.y & 0x7ffffff8u) > cut) continue;  // entered beyond the current cut
+                    w = (int)e.x;
+                }
                 if (w >= 0) node = w;
                 else decode_leaf(w, lf, lc);
                 continue;
@@ -1026,8 +1041,9 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
 #pragma unroll
             for (int i = 7; i >= 1; --i)
                 if (k[i] != kNoChild) {
-                    if (sp < kBvhStack) stk[sp++ * kBlock] = make_uint2((unsigned)child_word(bn, k[i]), k[i]);
-                    else overflow = true;
+                    if (sp >= CAP) overflow = true;
+                    else if constexpr (ANY) { stw[(sp >> 1) * (2 * kBlock) + (sp & 1)] = (unsigned)child_word(bn, k[i]); ++sp; }
+                    else stk[sp++ * kBlock] = make_uint2((unsigned)child_word(bn, k[i]), k[i]);
                 }
             if (k[0] != kNoChild) {
                 const int w = child_word(bn, k[0]);
@@ -1058,7 +1074,7 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
     const TriRay R = make_triray<KZ>(o, d);
     float cut = tMaxInit, t2 = __builtin_inff();
     int best = -1, second = -1;
-    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, true, [&](int lf, int lc) {
+    const bool ok = bvh8_walk<false>(sc.bvh[set], r, cut, nn, true, [&](int lf, int lc) {
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             const float4 A = tp[0], B = tp[1], Cc = tp[2];
@@ -1092,7 +1108,7 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
         amb = true;
         return -1;
     }
-    const float4* __restrict__ tiles = sc.btiles[set];
+    const float4* __restrict__ tiles = sc.btiles[kBvhAny];  // (shadow rays: every triangle, set 0)
     Bvh8Ray r;
     r.inv = bvh_inv(d);
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
@@ -1100,7 +1116,7 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
     const float sure = tMax - canon_window(tMax, sc.wabs);
     bool window = false, occluded = false;
     float cut = tMax;
-    const bool ok = bvh8_walk(sc.bvh[set], r, cut, nn, sc.anyhit_sort != 0, [&](int lf, int lc) {
+    const bool ok = bvh8_walk<true>(sc.bvh[kBvhAny], r, cut, nn, true, [&](int lf, int lc) {
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             ++nt;
@@ -1170,7 +1186,7 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
-    stage_scene<QCAP>(sc, io.set);
+    stage_scene<QCAP, false>(sc, io.set);
     ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
     // one ray at queue position p: octree (BVH / BFS), then the analytic shapes with the running tMax (DESIGN.md §5;
     // hitB = object-space point for a shape)

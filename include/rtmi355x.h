@@ -307,8 +307,8 @@ int rt_octree_get_info(rt_ctx* ctx, rt_octree_info* out);
  * node_leaf_first[n], node_leaf_count[n], leaf_refs[n_leaf_refs] (triangle ids incl. culled ones). */
 int rt_octree_export(rt_ctx* ctx, float* node_bounds, int32_t* node_child, int32_t* node_leaf_first,
                      int32_t* node_leaf_count, int32_t* leaf_refs);
-/* The fast multi-level traversal's 8-wide compressed BVH as uploaded for tile set `set` (0 all triangles, 1 without
- * back faces), DESIGN.md §6b: *n_nodes nodes of 32 floats (128 B, layout in rt_bvh.cpp), *n_tiles triangle tiles of
+/* The fast multi-level traversal's 8-wide compressed BVH as uploaded: set 0 / 1 the closest-hit BVH of tile set 0 (all
+ * triangles) / 1 (without back faces), set 2 the any-hit BVH of the shadow rays (all triangles), DESIGN.md §6b: *n_nodes nodes of 32 floats (128 B, layout in rt_bvh.cpp), *n_tiles triangle tiles of
  * 12 floats, consts[2] = (wabs, oguard) of the canonical rule.  Counts always; arrays when non-NULL.  Not a
  * reference structure (the reference traverses only its octree): exported so tests can replay the GPU's walk. */
 int rt_bvh_export(rt_ctx* ctx, int set, int* n_nodes, int* n_tiles, float* consts, float* nodes, float* tiles);

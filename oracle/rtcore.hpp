@@ -1129,8 +1129,10 @@ struct Bvh8 {
         return (int)(0x80000000u | first << 4 | (cnt - 1u));
     }
     // the walk; leaf(first, count) returns true to stop; false on a stack overflow
+    // any: the any-hit walk (no cull on pop, twice the stack entries: 4-byte words in the same LDS)
     template <class Leaf>
-    bool Walk(const Ray& ray, float& cut, Stats& st, Leaf&& leaf) const {
+    bool Walk(const Ray& ray, float& cut, Stats& st, bool any, Leaf&& leaf) const {
+        const int cap = any ? 2 * stack_cap : stack_cap;
         const vec3 inv = {ClampInv(ray.d.x), ClampInv(ray.d.y), ClampInv(ray.d.z)};
         const vec3 oi = {ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z};
         std::vector<std::pair<int, unsigned>> stk;
@@ -1143,7 +1145,7 @@ struct Bvh8 {
                     if (stk.empty()) break;
                     auto e = stk.back();
                     stk.pop_back();
-                    if (F(e.second & 0x7ffffff8u) > cut) continue;
+                    if (!any && F(e.second & 0x7ffffff8u) > cut) continue;
                     if (e.first >= 0) node = e.first;
                     else { lf = (e.first >> 4) & 0x7ffffff; lc = (e.first & 15) + 1; }
                     continue;
@@ -1156,7 +1158,7 @@ struct Bvh8 {
                 node = -1;
                 for (int i = 7; i >= 1; --i)
                     if (k[i] != kNo) {
-                        if ((int)stk.size() < stack_cap) stk.emplace_back(Word(cur, k[i]), k[i]);
+                        if ((int)stk.size() < cap) stk.emplace_back(Word(cur, k[i]), k[i]);
                         else overflow = true;
                     }
                 st.max_sp = std::max(st.max_sp, (int)stk.size());
@@ -1185,7 +1187,7 @@ struct Bvh8 {
         if (!Guarded(ray)) { res.amb = true; return res; }
         float cut = std::numeric_limits<float>::max(), t2 = std::numeric_limits<float>::infinity();
         int best = -1, second = -1;
-        const bool ok = Walk(ray, cut, st, [&](int lf, int lc) {
+        const bool ok = Walk(ray, cut, st, false, [&](int lf, int lc) {
             for (int k = 0; k < lc; ++k) {
                 vec3 p0, p1, p2;
                 int id;
@@ -1219,7 +1221,7 @@ struct Bvh8 {
         const float sure = tMax - Octree::Window(tMax, wabs);
         bool window = false, occ = false;
         float cut = tMax;
-        const bool ok = Walk(ray, cut, st, [&](int lf, int lc) {
+        const bool ok = Walk(ray, cut, st, true, [&](int lf, int lc) {
             for (int k = 0; k < lc; ++k) {
                 vec3 p0, p1, p2;
                 int id;

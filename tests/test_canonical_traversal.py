@@ -74,7 +74,7 @@ def _secondary(rng, ro, rd, prim, bt, tris, light):
 
 
 def _check(o, bvh, ro, rd, tmax, use_cull, totals):
-    st = o.bvh_check(bvh[1 if use_cull else 0], ro, rd, tmax, use_cull=use_cull, bvh_any=bvh[0])
+    st = o.bvh_check(bvh[1 if use_cull else 0], ro, rd, tmax, use_cull=use_cull, bvh_any=bvh[2])
     assert st["closest_mismatch"] == 0 and st["anyhit_mismatch"] == 0, st
     for k, v in st.items():
         if k == "max_stack":
@@ -92,7 +92,9 @@ def test_canonical_rule_equals_reference_bfs(oracle_lib, which, share):
     else:
         cfg, use_cull = scene.cfg0_reference(res=(64, 64), n_index=1), True
     o = oracle_lib.OracleScene(cfg)
-    bvh = [build_bvh_host(cfg.model, 0), build_bvh_host(cfg.model, 1) if use_cull else None]
+    # the closest-hit BVH of each tile set and the any-hit BVH (smaller leaves) the shadow rays walk
+    bvh = [build_bvh_host(cfg.model, 0), build_bvh_host(cfg.model, 1) if use_cull else None,
+           build_bvh_host(cfg.model, 2)]
     tris = _world_tris(cfg.model)
     light = cfg.model.lights[0] if cfg.model.lights else dict(p=(213.0, 548.7, 227.0), e1=(0, 0, 105.0),
                                                               e2=(130.0, 0, 0))

@@ -2,7 +2,8 @@
 
 The canonical rule is pinned against the reference BFS on >= 10 M CPU rays (tests/test_canonical_traversal.py) over
 the BVH the product builds on the host.  Here the device side is checked against that:
-  * the BVH the context uploads (rt_bvh_export) is the host build (rt_debug_bvh_build), bit for bit;
+  * the BVHs the context uploads (rt_bvh_export: closest-hit per tile set, and the any-hit BVH of the shadow rays)
+    are the host builds (rt_debug_bvh_build), bit for bit;
   * >= 2 M rays per mesh (CFG3, the CFG4 mesh) through the device walk (rt_debug_trace / rt_debug_occluded) equal
     the oracle's restated walk (Bvh8, the reference BFS for ambiguous rays) in triangle id, (b0, b1, b2, t) bits and
     occlusion: camera-like, random-in-the-box, axis-aligned, bounce and shadow families, any-hit tMax at the hit
@@ -41,7 +42,7 @@ def _mesh_cfg(which):
 def test_uploaded_bvh_equals_host_build(oracle_lib, which):
     cfg = scene.cfg0_reference(res=(32, 32), n_index=1) if which == "cfg0" else _mesh_cfg(which)
     g = Renderer(cfg)
-    for st in ((0, 1) if which == "cfg0" else (0,)):
+    for st in ((0, 1, 2) if which == "cfg0" else (0, 2)):  # 2: the any-hit BVH
         a, b = g.bvh(st), build_bvh_host(cfg.model, st)
         assert len(a["nodes"]) > 100 and len(a["tiles"]) > 1000
         for k in ("nodes", "tiles", "consts"):
@@ -69,7 +70,7 @@ def _secondary(rng, ro, rd, prim, bt, tris, light):
 def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, which):
     cfg = _mesh_cfg(which)
     g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
-    bvh = g.bvh(0)
+    bvh, bvh_any = g.bvh(0), g.bvh(2)
     tris = _world_tris(cfg.model)
     light = cfg.model.lights[0]
     rng = np.random.default_rng({"cfg3": 301, "cfg4": 401}[which])
@@ -81,7 +82,7 @@ def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, which):
         t = np.where(pg >= 0, bg[:, 3], 400.0)
         tmax = (t * rng.choice([0.5, 0.999, 1.0, 1.001, 2.0], size=len(t))).astype(np.float32)
         og = g.occluded(ro, rd, tmax)
-        po, bo, oo, ao = o.bvh_query(bvh, ro, rd, tmax)
+        po, bo, oo, ao = o.bvh_query(bvh, ro, rd, tmax, bvh_any=bvh_any)
         assert np.array_equal(pg, po), np.flatnonzero(pg != po)[:5]
         assert np.array_equal(bits(bg), bits(bo))
         assert np.array_equal(og, oo)
@@ -93,7 +94,7 @@ def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, which):
         for d in (s_wi[:m], s_ws[:m]):
             pg2, bg2 = g.trace(s_o[:m], d, False)
             og2 = g.occluded(s_o[:m], d, s_max[:m])
-            po2, bo2, oo2, ao2 = o.bvh_query(bvh, s_o[:m], d, s_max[:m])
+            po2, bo2, oo2, ao2 = o.bvh_query(bvh, s_o[:m], d, s_max[:m], bvh_any=bvh_any)
             assert np.array_equal(pg2, po2)
             assert np.array_equal(bits(bg2), bits(bo2))
             assert np.array_equal(og2, oo2)
