@@ -31,6 +31,10 @@ static constexpr int kBvhStack = 16;   // BVH traversal stack entries per lane (
 // hands to the reference BFS, after the wave's BVH loop has finished — that BFS's LDS-resident group FIFO.
 __shared__ uint2 g_bstk[kBvhStack * kBlock];
 static_assert(sizeof(uint2) * kBvhStack >= 2 * kLdsQ, "the BFS FIFO lives in the BVH stack's LDS");
+// The any-hit walks' stacks: child words only (nothing to cull with a fixed tMax), 24 per lane: 24 KB per block, so
+// the any-hit kernels (shade, NEE) are not held to 4 blocks per CU by LDS.  The BFS FIFO stays in g_bstk.
+static constexpr int kAnyStack = 24;
+__shared__ unsigned g_astk[kAnyStack * kBlock];
 
 // Single-leaf scenes, closest-hit waves without a shared dominant axis (bounce rays): pass 1 runs on a compacted list
 // of (ray, cluster) pairs whose box test passes (wave ballot + prefix into LDS) instead of every cluster for every lane.
@@ -1002,16 +1006,14 @@ __device__ __forceinline__ int child_word(const BvhNode8& n, unsigned key) {
 // (child word, key) (an entry whose entry distance lies beyond the current cut is dropped when popped); leaves are
 // handed to `leaf(lf, lc)`, which may lower the cut and returns true to end the walk.  Returns false on a stack
 // overflow (the ray is then ambiguous).
-// ANY (any-hit, fixed cut): the entries are the child words alone — every pushed child was entered within the fixed
-// tMax, so there is nothing to cull on pop — and the same LDS column holds twice as many of them (2 kBvhStack).
+// ANY (any-hit, fixed cut): the entries are the child words alone on g_astk — every pushed child was entered within
+// the fixed tMax, so there is nothing to cull on pop.
 template <bool ANY, class LeafFn>
 __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, const Bvh8Ray& r, float& cut, ctr_t& nn,
                                           bool sort, LeafFn&& leaf) {
-    constexpr int CAP = ANY ? 2 * kBvhStack : kBvhStack;
+    constexpr int CAP = ANY ? kAnyStack : kBvhStack;
     uint2* stk = g_bstk + threadIdx.x;
-    // (ANY) entry e at word (e / 2) 2 kBlock + e % 2 of this thread's OWN uint2 column: the exact-BFS fallback of a
-    // concurrent wave reuses its own column (traverse's LDS FIFO), so no thread may step outside its column
-    unsigned* stw = reinterpret_cast<unsigned*>(g_bstk + threadIdx.x);
+    unsigned* stw = g_astk + threadIdx.x;
     int sp = 0;
     bool overflow = false;
     int node = 0, lf = 0, lc = 0;
@@ -1023,7 +1025,7 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
                 int w;
                 if constexpr (ANY) {
                     --sp;
-                    w = (int)stw[(sp >> 1) * (2 * kBlock) + (sp & 1)];
+                    w = (int)stw[sp * kBlock];
                 } else {
                     const uint2 e = stk[--sp * kBlock];
                     if (__uint_as_float(e.y & 0x7ffffff8u) > cut) continue;  // entered beyond the current cut
@@ -1042,7 +1044,7 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
             for (int i = 7; i >= 1; --i)
                 if (k[i] != kNoChild) {
                     if (sp >= CAP) overflow = true;
-                    else if constexpr (ANY) { stw[(sp >> 1) * (2 * kBlock) + (sp & 1)] = (unsigned)child_word(bn, k[i]); ++sp; }
+                    else if constexpr (ANY) stw[sp++ * kBlock] = (unsigned)child_word(bn, k[i]);
                     else stk[sp++ * kBlock] = make_uint2((unsigned)child_word(bn, k[i]), k[i]);
                 }
             if (k[0] != kNoChild) {
@@ -1183,6 +1185,9 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 #define RT_MULTI_WAVES 4  // the one tuning macro left: variant builds for A/B (Makefile `variants`)
 #endif
 #define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_MULTI_WAVES)))
+#ifndef RT_SHADE_WAVES
+#define RT_SHADE_WAVES RT_MULTI_WAVES  // the simple-path shade (its shadow rays' any-hit walks)
+#endif
 
 template <int QCAP>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
@@ -1450,7 +1455,7 @@ __device__ __forceinline__ bool cosine_bounce(float u0, float u1, V3 nrm, V3& wi
 }
 
 template <int QCAP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? 4 : RT_MULTI_WAVES))) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? 4 : RT_SHADE_WAVES))) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp,
                                                                          DevFilm film, SampleIds ids, PathIO io,
                                                                          unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
@@ -1961,7 +1966,10 @@ __device__ __forceinline__ bool scene_occluded_bvh(const DevScene& sc, V3 o, V3 
 // reference BFS for the ambiguous rays), so this kernel never holds the BFS's registers (128 VGPRs + spill -> 108).
 // A vertex's lights are always accumulated together, in light order, by one of the two.
 template <int QCAP, bool FB>
-__global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_nee(DevScene sc, const DevSpectra* sp, PathIO io,
+#ifndef RT_NEE_WAVES
+#define RT_NEE_WAVES 4  // (variant builds: Makefile `variants`)
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? 1 : (FB ? 2 : RT_NEE_WAVES)))) k_path_nee(DevScene sc, const DevSpectra* sp, PathIO io,
                                                                        NeeIO nee, unsigned long long* ctr) {
     stage_scene<QCAP>(sc, 0);
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;

@@ -1080,7 +1080,8 @@ struct Bvh8 {
     const float* tiles = nullptr;   // 12 floats per tile: (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0)
     int n_nodes = 0, n_tiles = 0;
     float wabs = 0, oguard = 0;
-    int stack_cap = 16;             // kBvhStack
+    int stack_cap = 16;             // kBvhStack (closest hit)
+    int any_cap = 24;               // kAnyStack (any hit)
     static constexpr unsigned kNo = 0xffffffffu;
     struct Stats { int64_t nodes = 0, boxes = 0, tris = 0; int max_sp = 0; };
     struct Result { int tri = -1; TriIsect isect{}; bool amb = false; int occluded = 0; };
@@ -1132,7 +1133,7 @@ struct Bvh8 {
     // any: the any-hit walk (no cull on pop, twice the stack entries: 4-byte words in the same LDS)
     template <class Leaf>
     bool Walk(const Ray& ray, float& cut, Stats& st, bool any, Leaf&& leaf) const {
-        const int cap = any ? 2 * stack_cap : stack_cap;
+        const int cap = any ? any_cap : stack_cap;
         const vec3 inv = {ClampInv(ray.d.x), ClampInv(ray.d.y), ClampInv(ray.d.z)};
         const vec3 oi = {ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z};
         std::vector<std::pair<int, unsigned>> stk;

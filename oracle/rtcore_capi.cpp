@@ -511,7 +511,7 @@ int orc_bvh_check(void* h, const float* nodes, int n_nodes, const float* tiles, 
                 st[8] += sc.nodes; st[9] += sc.boxes; st[10] += sc.tris;
                 st[11] = std::max<int64_t>(st[11], std::max(sc.max_sp, sa.max_sp));
                 st[12] += sa.nodes; st[13] += sa.boxes; st[14] += sa.tris;
-                st[15] += (sc.max_sp >= B.stack_cap) + (sa.max_sp >= 2 * BA.stack_cap);
+                st[15] += (sc.max_sp >= B.stack_cap) + (sa.max_sp >= BA.any_cap);
             }
         });
     for (auto& t : pool) t.join();
