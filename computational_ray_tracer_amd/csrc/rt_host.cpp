@@ -2214,6 +2214,13 @@ static int get_stats_one(rt_ctx* c, rt_stats* out) {
     s.samples = (int64_t)h[C_SAMPLES];
     s.fallback_rays = (int64_t)h[C_FALLBACK];
     s.shadow_fallback_rays = (int64_t)h[C_SFALLBACK];
+#if RT_SIMD_STATS
+    unsigned long long sm[8];
+    simd_stats_read(sm);
+    std::fprintf(stderr, "SIMD closest nodes %.3f tris %.3f | any nodes %.3f tris %.3f | steps %llu %llu %llu %llu\n",
+                 sm[1] / (double)(sm[0] + !sm[0]), sm[3] / (double)(sm[2] + !sm[2]), sm[5] / (double)(sm[4] + !sm[4]),
+                 sm[7] / (double)(sm[6] + !sm[6]), sm[0] / 64, sm[2] / 64, sm[4] / 64, sm[6] / 64);
+#endif
     *out = s;
     return RT_OK;
 }

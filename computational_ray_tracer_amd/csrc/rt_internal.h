@@ -146,6 +146,9 @@ struct DevScene {
 // device counter slots (u64).  Every wave of a persistent kernel adds its totals at the end, all at about the same
 // time: one counter word per slot serialised those atomics (a fixed ~0.15 ms tail per trace launch), so each slot
 // is spread over kCtrSubs words, one per 256-B line, picked by wave; the host sums them (ctr_word, ctr_total).
+#if RT_SIMD_STATS
+void simd_stats_read(unsigned long long* out);  // rt_kernels.hip (measurement builds)
+#endif
 enum { C_NODES = 0, C_TRIS, C_HITS, C_RAYS, C_SHADOW, C_SAMPLES, C_SNODES, C_STRIS, C_FALLBACK, C_SFALLBACK,
        C_NCOUNTERS = 16 };
 constexpr int kCtrSubs = 32;   // words per counter slot

@@ -60,6 +60,7 @@ __device__ __forceinline__ void stage_leaf1(const DevScene& sc, int set) {
 __shared__ float4 g_top[kBvhNodeRead * kBvhTopNodes];
 // ANY: the kernel's BVH walks are any-hit queries, which walk the any-hit BVH (sc.bvh[kBvhAny]); otherwise the
 // closest-hit BVH of tile set `set`
+__device__ __forceinline__ void simd_init();  // (RT_SIMD_STATS measurement builds, below)
 template <int QCAP, bool ANY = true>
 __device__ __forceinline__ void stage_scene(const DevScene& sc, int set) {
     if constexpr (QCAP == 1) {
@@ -70,6 +71,7 @@ __device__ __forceinline__ void stage_scene(const DevScene& sc, int set) {
         if (b)
             for (int i = threadIdx.x; i < kBvhNodeRead * kBvhTopNodes; i += blockDim.x)
                 g_top[i] = b[(i / kBvhNodeRead) * kBvhNodeF4 + i % kBvhNodeRead];
+        simd_init();
         __syncthreads();
     }
 }
@@ -118,6 +120,40 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // -------------------------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// SIMD efficiency of the BVH walks (measurement builds only, -DRT_SIMD_STATS=1): per slot pair, the lanes a wave
+// step could have used (64 per step) and the lanes active in it; slots 0/1 closest-hit node tests, 2/3 closest-hit
+// triangle tests, 4/5 any-hit node tests, 6/7 any-hit triangle tests.  Block sums in LDS, flushed by the trace and
+// shade kernels; the host prints them with the stats (rt_host.cpp get_stats_one).
+#ifndef RT_SIMD_STATS
+#define RT_SIMD_STATS 0
+#endif
+#if RT_SIMD_STATS
+__shared__ unsigned long long g_simd[8];
+__device__ unsigned long long g_simd_glob[8];
+__device__ __forceinline__ void simd_tick(int slot) {
+    const uint64_t m = __ballot(1);
+    if (lane_id() == __builtin_ctzll(m)) {
+        atomicAdd(&g_simd[slot], 64ull);
+        atomicAdd(&g_simd[slot + 1], (unsigned long long)__popcll(m));
+    }
+}
+__device__ __forceinline__ void simd_init() {
+    if (threadIdx.x < 8) g_simd[threadIdx.x] = 0;
+}
+__device__ __forceinline__ void simd_flush() {
+    __syncthreads();
+    if (threadIdx.x < 8) atomicAdd(&g_simd_glob[threadIdx.x], g_simd[threadIdx.x]);
+}
+void simd_stats_read(unsigned long long* out) {
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_simd_glob), sizeof(g_simd_glob));
+}
+#define RT_SIMD_TICK(s) simd_tick(s)
+#else
+#define RT_SIMD_TICK(s)
+__device__ __forceinline__ void simd_init() {}
+__device__ __forceinline__ void simd_flush() {}
+#endif
 
 // Append the `pred` lanes of a wave to a queue: one atomicAdd per wave, slots in lane order.
 // Every lane of the wave must call it.
@@ -941,6 +977,12 @@ __device__ __forceinline__ void kswap(unsigned& a, unsigned& b) {
     a = lo; b = hi;
 }
 static constexpr unsigned kNoChild = 0xffffffffu;
+#ifndef RT_SPEC
+#define RT_SPEC 1
+#endif
+#ifndef RT_LEAF_STEP
+#define RT_LEAF_STEP 8
+#endif
 
 // One 8-wide node against the ray: the sorted child keys k[0] <= ... <= k[7].  Key of a child whose slab interval
 // [tn, tf] is non-empty within [0, tcut]: (bits(tn) with the low 3 bits cleared) | slot — tn >= 0, so the keys
@@ -1016,7 +1058,64 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
     unsigned* stw = g_astk + threadIdx.x;
     int sp = 0;
     bool overflow = false;
-    int node = 0, lf = 0, lc = 0;
+    int lf = 0, lc = 0;
+#if RT_SPEC
+    // Speculative while-while (Aila & Laine 2009): a lane that holds a leaf keeps opening nodes while other lanes
+    // of its wave are still looking for theirs, so the node steps the wave executes anyway do useful work (CFG3:
+    // 29 % of the lanes of a node step were busy without it).  node: an internal node to open (>= 0), none (-1), or
+    // a second leaf's word (< -1) waiting until the held leaf (lf, lc) is tested.  A held leaf's triangles are
+    // tested after those nodes, with the cut of that time: more nodes may be opened, the answer is the same (the
+    // canonical rule does not depend on the order; a stack overflow still makes the ray ambiguous).
+    int node = 0;
+    while (true) {
+        while (true) {
+            const bool more = node >= 0 || (node == -1 && sp > 0);
+            if (__ballot(lc == 0 && more) == 0) break;  // every lane holds a leaf or is done
+            if (!more) continue;
+            if (node == -1) {
+                if constexpr (ANY) {
+                    --sp;
+                    node = (int)stw[sp * kBlock];
+                } else {
+                    const uint2 e = stk[--sp * kBlock];
+                    if (__uint_as_float(e.y & 0x7ffffff8u) > cut) continue;  // entered beyond the current cut
+                    node = (int)e.x;
+                }
+            } else {
+                RT_SIMD_TICK(ANY ? 4 : 0);
+                const BvhNode8 bn = load_node8(nodes, node);
+                nn += __popc(bn.N1.w);
+                unsigned k[8];
+                node_keys(bn, r, cut, k, sort);
+                node = -1;
+#pragma unroll
+                for (int i = 7; i >= 1; --i)
+                    if (k[i] != kNoChild) {
+                        if (sp >= CAP) overflow = true;
+                        else if constexpr (ANY) stw[sp++ * kBlock] = (unsigned)child_word(bn, k[i]);
+                        else stk[sp++ * kBlock] = make_uint2((unsigned)child_word(bn, k[i]), k[i]);
+                    }
+                if (k[0] != kNoChild) node = child_word(bn, k[0]);
+            }
+            if (node < -1 && lc == 0) {
+                decode_leaf(node, lf, lc);
+                node = -1;
+            }
+        }
+        if (lc == 0) break;  // nothing held, nothing left: this lane's walk is over
+        // at most RT_LEAF_STEP triangles per leaf phase (the rest stays held)
+        const int m = lc < RT_LEAF_STEP ? lc : RT_LEAF_STEP;
+        const bool done = leaf(lf, m);
+        lf += m;
+        lc -= m;
+        if (done) break;
+        if (lc == 0 && node < -1) {
+            decode_leaf(node, lf, lc);
+            node = -1;
+        }
+    }
+#else
+    int node = 0;
     while (true) {
         // node phase ("while-while"): open internal nodes nearest-first until this lane holds a leaf
         while (lc == 0) {
@@ -1035,6 +1134,7 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
                 else decode_leaf(w, lf, lc);
                 continue;
             }
+            RT_SIMD_TICK(ANY ? 4 : 0);
             const BvhNode8 bn = load_node8(nodes, node);
             nn += __popc(bn.N1.w);
             unsigned k[8];
@@ -1058,6 +1158,7 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
         lc = 0;
         if (done) break;
     }
+#endif
     return !overflow;
 }
 
@@ -1081,6 +1182,7 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
             const float4* tp = tiles + 3 * (lf + k);
             const float4 A = tp[0], B = tp[1], Cc = tp[2];
             ++nt;
+            RT_SIMD_TICK(2);
             float b0, b1, b2, t;
             if (tri_intersect<KZ>(R, cut, A, B, Cc, b0, b1, b2, t) && t < cut) {
                 if (best < 0 || t < rt) {
@@ -1122,6 +1224,7 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             ++nt;
+            RT_SIMD_TICK(6);
             float b0, b1, b2, t;
             if (tri_intersect<KZ>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax) {
                 if (t < sure) { occluded = true; return true; }
@@ -1268,6 +1371,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
     count_add(ctr, C_HITS, nh);
     count_add(ctr, C_RAYS, nr);
     count_add(ctr, C_FALLBACK, nfb);
+    if constexpr (QCAP != 1) simd_flush();
 }
 
 // Material bins of a mixed multi-level scene's bounce (BinIO): every hit's queue position is appended to the index
@@ -1632,6 +1736,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
     count_add(ctr, C_SFALLBACK, sfb);
+    if constexpr (QCAP != 1) simd_flush();
 }
 
 

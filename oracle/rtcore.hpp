@@ -1075,6 +1075,10 @@ struct Octree {
 // push order), over the BVH the product builds (exported through rt_bvh_export / rt_debug_bvh_build: 32 floats per
 // node, 12 per tile).  With it a CPU test checks, on millions of rays, that the canonical rule over THIS BVH returns
 // what Octree::Traverse / Occluded return, and a GPU test checks the device walk against it ray by ray.
+// The device's speculative walk (RT_SPEC, the default) tests a lane's held leaf after the nodes its wave opens
+// meanwhile, i.e. in an order that depends on the other lanes; this restates one ray's walk alone (the RT_SPEC=0
+// order).  Answers agree either way: the canonical rule's result and its ambiguity do not depend on the order in
+// which triangles are tested; only stack overflows (ambiguous, BFS-decided) may fall elsewhere.
 struct Bvh8 {
     const float* nodes = nullptr;   // 32 floats per node (rt_bvh.cpp layout)
     const float* tiles = nullptr;   // 12 floats per tile: (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-kernel resource table (VGPRs, spill bytes, occupancy, LDS) from hipcc -Rpass-analysis=kernel-resource-usage
-remarks on stdin: `make -s resources-raw | python3 tools/kres.py [filter]`."""
+remarks on stdin: `make -s resources | python3 tools/kres.py [filter]`."""
 import re
 import subprocess
 import sys
