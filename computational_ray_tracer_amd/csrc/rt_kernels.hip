@@ -983,6 +983,9 @@ static constexpr unsigned kNoChild = 0xffffffffu;
 #ifndef RT_LEAF_STEP
 #define RT_LEAF_STEP 8
 #endif
+#ifndef RT_POP_OPEN
+#define RT_POP_OPEN 1
+#endif
 
 // One 8-wide node against the ray: the sorted child keys k[0] <= ... <= k[7].  Key of a child whose slab interval
 // [tn, tf] is non-empty within [0, tcut]: (bits(tn) with the low 3 bits cleared) | slot — tn >= 0, so the keys
@@ -1072,6 +1075,25 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
             const bool more = node >= 0 || (node == -1 && sp > 0);
             if (__ballot(lc == 0 && more) == 0) break;  // every lane holds a leaf or is done
             if (!more) continue;
+#if RT_POP_OPEN
+            // pop, then open a popped internal node in the same step (the lanes popping and the lanes holding a
+            // node open theirs together instead of in alternating steps)
+            if (node == -1) {
+                if constexpr (ANY) {
+                    --sp;
+                    node = (int)stw[sp * kBlock];
+                } else {
+                    while (sp > 0) {
+                        const uint2 e = stk[--sp * kBlock];
+                        if (__uint_as_float(e.y & 0x7ffffff8u) <= cut) {  // (entered beyond the current cut: dropped)
+                            node = (int)e.x;
+                            break;
+                        }
+                    }
+                }
+            }
+            if (node >= 0) {
+#else
             if (node == -1) {
                 if constexpr (ANY) {
                     --sp;
@@ -1082,6 +1104,7 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
                     node = (int)e.x;
                 }
             } else {
+#endif
                 RT_SIMD_TICK(ANY ? 4 : 0);
                 const BvhNode8 bn = load_node8(nodes, node);
                 nn += __popc(bn.N1.w);
