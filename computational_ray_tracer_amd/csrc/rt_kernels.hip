@@ -986,6 +986,9 @@ static constexpr unsigned kNoChild = 0xffffffffu;
 #ifndef RT_POP_OPEN
 #define RT_POP_OPEN 1
 #endif
+#ifndef RT_TRI_PREFETCH
+#define RT_TRI_PREFETCH 1
+#endif
 
 // One 8-wide node against the ray: the sorted child keys k[0] <= ... <= k[7].  Key of a child whose slab interval
 // [tn, tf] is non-empty within [0, tcut]: (bits(tn) with the low 3 bits cleared) | slot — tn >= 0, so the keys
@@ -1201,9 +1204,18 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
     float cut = tMaxInit, t2 = __builtin_inff();
     int best = -1, second = -1;
     const bool ok = bvh8_walk<false>(sc.bvh[set], r, cut, nn, true, [&](int lf, int lc) {
+#if RT_TRI_PREFETCH
+        // the next triangle's tile is loaded while this one is tested (a leaf's tiles are contiguous)
+        const float4* tp = tiles + 3 * lf;
+        float4 A = tp[0], B = tp[1], Cc = tp[2];
+        for (int k = 0; k < lc; ++k) {
+            float4 nA = A, nB = B, nC = Cc;
+            if (k + 1 < lc) { nA = tp[3 * k + 3]; nB = tp[3 * k + 4]; nC = tp[3 * k + 5]; }
+#else
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             const float4 A = tp[0], B = tp[1], Cc = tp[2];
+#endif
             ++nt;
             RT_SIMD_TICK(2);
             float b0, b1, b2, t;
@@ -1220,6 +1232,9 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
                     t2 = t;
                 }
             }
+#if RT_TRI_PREFETCH
+            A = nA; B = nB; Cc = nC;
+#endif
         }
         return false;
     });
@@ -1244,6 +1259,22 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
     bool window = false, occluded = false;
     float cut = tMax;
     const bool ok = bvh8_walk<true>(sc.bvh[kBvhAny], r, cut, nn, true, [&](int lf, int lc) {
+#if RT_TRI_PREFETCH
+        const float4* tp = tiles + 3 * lf;
+        float4 A = tp[0], B = tp[1], Cc = tp[2];
+        for (int k = 0; k < lc; ++k) {
+            float4 nA = A, nB = B, nC = Cc;
+            if (k + 1 < lc) { nA = tp[3 * k + 3]; nB = tp[3 * k + 4]; nC = tp[3 * k + 5]; }
+            ++nt;
+            RT_SIMD_TICK(6);
+            float b0, b1, b2, t;
+            if (tri_intersect<KZ>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                if (t < sure) { occluded = true; return true; }
+                window = true;
+            }
+            A = nA; B = nB; Cc = nC;
+        }
+#else
         for (int k = 0; k < lc; ++k) {
             const float4* tp = tiles + 3 * (lf + k);
             ++nt;
@@ -1254,6 +1285,7 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
                 window = true;
             }
         }
+#endif
         return false;
     });
     if (occluded) { amb = false; return 0; }
@@ -2166,6 +2198,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
     count_add(ctr, C_SFALLBACK, sfb);
+    if constexpr (QCAP != 1 && !FB) simd_flush();
 }
 
 // sensor + film for path mode (pixel-owned, index order)
