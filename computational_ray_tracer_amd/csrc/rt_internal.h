@@ -161,7 +161,8 @@ __host__ __device__ inline size_t ctr_word(int slot, int sub) { return ((size_t)
 // multi-level traversal kernels.
 static const int kBvhNodeF4 = 8, kBvhNodeRead = 5;  // float4 per node / float4 the kernels read (N0..N4)
 static const int kBvhTopLevels = 2, kBvhTopNodes = 9;
-static const int kBvhMaxLeaf = 8;                     // triangles per leaf (SAH may stop earlier)
+static const int kBvhMaxLeaf = 4;  // triangles per closest-hit leaf (SAH may stop earlier; r03 A/B with the speculative
+                                   // walk: 4 vs 8 CFG3 +1 %, CFG4 +1.1 %; 5, 6 between)
 static const int kBvhAny = 2;                         // DevScene bvh / btiles index of the any-hit BVH
 struct BvhData {
     std::vector<float4> nodes, tiles;
