@@ -17,15 +17,22 @@ import glob
 import json
 from pathlib import Path
 
-KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_nee", "k_path_nee_fb", "k_path_shadow", "k_generate",
-           "k_path_film", "k_ref_shade_film", "k_rs_hist", "k_rs_scatter", "k_rs_offsets")
+KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_shade_full_c1", "k_path_shade_full_c2",
+           "k_bin_materials", "k_path_nee", "k_path_nee_fb", "k_path_shadow", "k_generate", "k_path_film",
+           "k_ref_shade_film", "k_rs_hist", "k_rs_scatter", "k_rs_offsets", "k_rs_prep")
+# the mixed-scene shade of one bounce with material bins: the binning pass and one kernel per material class, all
+# inside the shade stage's HIP-event bracket (bench.py k_path_shade): summed per launch into "k_path_shade_full"
+SHADE_BINNED = ("k_bin_materials", "k_path_shade_full_c1", "k_path_shade_full_c2")
 
 
 def kname(raw):
     full = raw.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     base = full.split("<")[0].split("::")[-1]
-    if base == "k_path_nee" and full.replace(" ", "").endswith(",true>"):
+    args = full.replace(" ", "").split("<")[1].rstrip(">").split(",") if "<" in full else []
+    if base == "k_path_nee" and args[-1:] == ["true"]:
         return "k_path_nee_fb"  # the exact-traversal fallback instantiation (undecided vertices), not the NEE pass
+    if base == "k_path_shade_full" and len(args) == 2 and args[1] in ("1", "2"):
+        return base + "_c" + args[1]  # one material class's kernel (k_path_shade_full<Q, MC>)
     return base
 
 
@@ -53,10 +60,12 @@ def main():
     write = per_dispatch(d / "write", "WRITE_SIZE")
     sq = {c: per_dispatch(d / "sq", c) for c in ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES",
                                                   "SQ_INSTS_VMEM_RD", "SQ_INSTS_LDS", "SQ_WAVES")}
-    avg_ns = {}
+    tot_ns, calls = collections.Counter(), collections.Counter()  # instantiations of one name pooled
     for f in glob.glob(str(d / "kt" / "**" / "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            avg_ns[kname(r["Name"])] = float(r["AverageNs"])
+            tot_ns[kname(r["Name"])] += float(r["TotalDurationNs"])
+            calls[kname(r["Name"])] += int(r["Calls"])
+    avg_ns = {k: tot_ns[k] / calls[k] for k in calls if calls[k]}
     import hashlib
     out = {"tag": a.tag, "config": a.config, "lanes": 1,
            "lib_sha16": hashlib.sha256(Path(a.lib).read_bytes()).hexdigest()[:16],
@@ -81,6 +90,15 @@ def main():
                 e["dram_gbs"] = round(e["dram_bytes_per_launch"] / avg_ns[k], 1)
         if e:
             out["kernels"][k] = e
+    ks = out["kernels"]
+    if all(k in ks for k in SHADE_BINNED) and "k_path_shade_full" not in ks:
+        e = {"parts": list(SHADE_BINNED)}
+        for f in ("dram_bytes_per_launch", "valu_insts_per_launch", "rocprof_avg_ns"):
+            if all(f in ks[k] for k in SHADE_BINNED):
+                e[f] = sum(ks[k][f] for k in SHADE_BINNED)
+        if "dram_bytes_per_launch" in e and "rocprof_avg_ns" in e:
+            e["dram_gbs"] = round(e["dram_bytes_per_launch"] / e["rocprof_avg_ns"], 1)
+        ks["k_path_shade_full"] = e
     dst = Path(a.out or f"profiles/counters_{a.config}.json")
     dst.write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out, indent=1))
