@@ -49,7 +49,7 @@ def parse():
     return p.parse_args()
 
 
-def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
+def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=False, n_lights=1):
     """Per-kernel HBM and VALU rooflines from HIP-event launch times (the single-lane pass: one launch at a time).
 
     Algorithmic bytes follow SURVEY.md §8(d): the per-ray HBM streams are `achieved` (k_trace_closest: 40 B per
@@ -58,8 +58,12 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
     (the Cornell scene is 1.8 KB, the CFG3 BVH 1 MB + 4.7 MB of triangles), never an HBM rate.  `traffic` is the
     PMC-measured DRAM bytes per launch and `valu` the SQ_INSTS_VALU per launch over the same single-lane launch time,
     both from profiles/counters_<config>.json when it was measured on the loaded library build."""
+    # Multi-level scenes sort their bounce rays (DESIGN.md §6b): the trace kernel reads each bounce ray through the
+    # sort's permutation (4 B index) and writes it to the sorted side queue (32 B) on its way to the traversal —
+    # the sort's data movement, fused into the trace: 36 B per bounce ray on top of the §8(d) 40 B.
+    gather = 36 * max(0, st["rays"] - st["samples"]) if sorted_bounces else 0
     ks = {
-        "k_trace_closest": (st["ms_trace"], st["launches_trace"], 40 * st["rays"],
+        "k_trace_closest": (st["ms_trace"], st["launches_trace"], 40 * st["rays"] + gather,
                             32 * st["nodes_tested"] + 40 * st["tris_tested"]),
         "k_path_shade": (st["ms_shade"], st["launches_shade"], 312 * st["rays"] + 32 * st["shadow_rays"],
                          32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"]),
@@ -76,7 +80,12 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
                     "total_ms": round(st["ms_shadow"], 3)}
     elif st["ms_shadow"] > 0:  # shadow rays in a kernel of their own, one launch per shade launch: the §8(d) 32 B
         # per shadow ray and the shadow scene terms move to it (k_path_nee: mixed scenes; k_path_shadow: shadow queue)
-        ks[shadow_kernel] = (st["ms_shadow"], st["launches_shade"], 32 * st["shadow_rays"],
+        # k_path_nee also reads each vertex's NEE record (rt_internal.h NeeIO: 16 B + 16 B per light + 4 B weight
+        # per light + 32 B, i.e. 128 B with 4 lights) once for its n_lights shadow rays
+        rec = 16 * (1 + n_lights + (n_lights + 3) // 4 + 2)
+        ks[shadow_kernel] = (st["ms_shadow"], st["launches_shade"],
+                             32 * st["shadow_rays"] + (rec * st["shadow_rays"] // max(1, n_lights)
+                                                       if shadow_kernel == "k_path_nee" else 0),
                              32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"])
         ks["k_path_shade"] = (st["ms_shade"], st["launches_shade"], 312 * st["rays"], 0)
     res = {}
@@ -94,6 +103,8 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee"):
                      # scenes are <= 6 MB), so they are reported as bytes, never as an HBM rate
                      "scene_bytes_per_launch_cache_served": int(scene_b / launches),
                      "total_ms": round(ms, 3)}
+        if kc.get("dram_bytes_per_launch") and stream_b:
+            res[name]["traffic_over_algorithmic"] = round(kc["dram_bytes_per_launch"] / (stream_b / launches), 2)
         if kc.get("valu_insts_per_launch"):
             g = kc["valu_insts_per_launch"] / avg_s / 1e9
             res[name]["valu"] = {"achieved": round(g, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
@@ -261,7 +272,9 @@ def main():
     roofline = {}
     if rank == 0:
         st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
-        rl = kernel_rooflines(st1, counters, "k_path_nee" if a.config in ("cfg4", "cfg5") else "k_path_shadow")
+        rl = kernel_rooflines(st1, counters, "k_path_nee" if a.config in ("cfg4", "cfg5") else "k_path_shadow",
+                              sorted_bounces=a.config != "cornell" and os.environ.get("RTMI_SORT", "1") != "0",
+                              n_lights=len(cfg.model.lights))
         dom = max(rl, key=lambda k: rl[k]["total_ms"])
         roofline = dict(rl[dom])
         roofline["basis"] = (f"single-lane pass (RTMI_LANES=1, {a.steps} steps, {dt1 / a.steps * 1e3:.3f} ms/step): "

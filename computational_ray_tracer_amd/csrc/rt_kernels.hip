@@ -1343,6 +1343,9 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 #define RT_MULTI_WAVES 4  // the one tuning macro left: variant builds for A/B (Makefile `variants`)
 #endif
 #define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_MULTI_WAVES)))
+#ifndef RT_SHADE1_WAVES
+#define RT_SHADE1_WAVES 4  // the single-leaf simple-path shade (Cornell)
+#endif
 #ifndef RT_SHADE_WAVES
 #define RT_SHADE_WAVES RT_MULTI_WAVES  // the simple-path shade (its shadow rays' any-hit walks)
 #endif
@@ -1614,7 +1617,7 @@ __device__ __forceinline__ bool cosine_bounce(float u0, float u1, V3 nrm, V3& wi
 }
 
 template <int QCAP>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? 4 : RT_SHADE_WAVES))) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? RT_SHADE1_WAVES : RT_SHADE_WAVES))) k_path_shade(DevScene sc, const DevSpectra* sp, DevSampler smp,
                                                                          DevFilm film, SampleIds ids, PathIO io,
                                                                          unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;

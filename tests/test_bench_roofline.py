@@ -1,0 +1,43 @@
+"""bench.py's per-kernel roofline arithmetic (CPU): algorithmic bytes per launch from the device counters, the
+sort gather fused into the multi-level trace, the NEE record, the PMC traffic ratio and the stale-counter rule."""
+import bench
+
+
+def _stats(**kw):
+    st = dict(ms_trace=10.0, launches_trace=10, ms_shade=20.0, launches_shade=10, ms_shadow=30.0,
+              rays=1_000_000, samples=400_000, shadow_rays=800_000, nodes_tested=0, tris_tested=0,
+              shadow_nodes_tested=0, shadow_tris_tested=0)
+    st.update(kw)
+    return st
+
+
+def test_trace_bytes_with_and_without_the_sort_gather():
+    st = _stats()
+    plain = bench.kernel_rooflines(st, None, "k_path_shadow")
+    srt = bench.kernel_rooflines(st, None, "k_path_shadow", sorted_bounces=True)
+    assert plain["k_trace_closest"]["algorithmic_bytes_per_launch"] == 40 * 1_000_000 // 10
+    # 36 B per bounce ray (rays - camera samples): the permutation index and the sorted side-queue write
+    assert srt["k_trace_closest"]["algorithmic_bytes_per_launch"] == (40 * 1_000_000 + 36 * 600_000) // 10
+    a = srt["k_trace_closest"]
+    assert abs(a["achieved"] - a["algorithmic_bytes_per_launch"] / 1e-3 / 1e9) < 0.1  # 1 ms per launch
+    assert a["frac"] <= 1.0
+
+
+def test_nee_record_bytes_and_traffic_ratio():
+    st = _stats()
+    counters = {"k_path_nee": {"dram_bytes_per_launch": 12_000_000, "valu_insts_per_launch": 1e6}}
+    rl = bench.kernel_rooflines(st, counters, "k_path_nee", sorted_bounces=True, n_lights=4)
+    nee = rl["k_path_nee"]
+    # 32 B per shadow ray + the 128-B record (16 B point, 4 x 16 B rays, 16 B weights, 32 B throughput) per vertex
+    assert nee["algorithmic_bytes_per_launch"] == (32 * 800_000 + 128 * 800_000 // 4) // 10
+    assert nee["traffic"] == 12_000_000
+    assert nee["traffic_over_algorithmic"] == round(12_000_000 / nee["algorithmic_bytes_per_launch"], 2)
+    assert 0 < nee["valu"]["frac"] <= 1.0
+    # the shade kernel keeps its own stream bytes, the shadow rays moved to k_path_nee
+    assert rl["k_path_shade"]["algorithmic_bytes_per_launch"] == 312 * 1_000_000 // 10
+
+
+def test_no_counters_means_no_traffic_fields():
+    rl = bench.kernel_rooflines(_stats(), None, "k_path_shadow")
+    for v in rl.values():
+        assert v.get("traffic") is None and "valu" not in v and "traffic_over_algorithmic" not in v
