@@ -1399,6 +1399,12 @@ int setup_sensor(rt_ctx* c, const rt_film_desc& d) {
         hipMemcpy(base + offsetof(DevSpectra, SG), bars[1].v.data(), 4 * kSpecN, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(base + offsetof(DevSpectra, SB), bars[2].v.data(), 4 * kSpecN, hipMemcpyHostToDevice) != hipSuccess)
         return fail(c, RT_E_HIP, "sensor upload");
+    std::vector<float4> spk(kSpecN);
+    for (int i = 0; i < kSpecN; ++i)
+        spk[i] = make_float4(bars[0].v[i], bars[1].v[i], bars[2].v[i], c->hs.D65d.v[i]);
+    if (hipMemcpy(base + offsetof(DevSpectra, SPK), spk.data(), sizeof(float4) * kSpecN, hipMemcpyHostToDevice) !=
+        hipSuccess)
+        return fail(c, RT_E_HIP, "sensor upload");
     return RT_OK;
 }
 

@@ -27,6 +27,9 @@ struct DevSpectra {                 // Spectra::Init products (spectrum.cpp:2612
     float bk7_lambda[kF1Max], bk7_value[kF1Max];   // glass-BK7 eta, FromInterleaved(.., false) (spectrum.cpp:2674)
     int bk7_n;
     float SR[kSpecN], SG[kSpecN], SB[kSpecN];      // the film's PixelSensor r_bar / g_bar / b_bar (dense)
+    // the same dense values packed per wavelength, {SR, SG, SB, D65}[λ - 360]: the kernels stage it in LDS (7.5 KB)
+    // and gather one ds_read_b128 per hero wavelength instead of a scattered global load per table (rt_kernels.hip)
+    float4 SPK[kSpecN];
 };
 
 struct DevCamera {

@@ -189,6 +189,27 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
     return pred ? base + rank : -1;
 }
 
+// Block-aggregated append of a static chunk's two items (kStaticItems = 2): one atomicAdd and one round of barriers
+// for both; the block's first items take the lower positions, its second items the upper ones.  lds: 2 NW + 1 ints.
+__device__ __forceinline__ void block_append2(int* counter, bool p0, bool p1, int* lds, int& o0, int& o1) {
+    constexpr int NW = kBlock / 64;
+    const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
+    const int wave = threadIdx.x >> 6;
+    const int r0 = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+    const int r1 = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+    if (lane_id() == 0) { lds[wave] = __popcll(m0); lds[NW + wave] = __popcll(m1); }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < 2 * NW; ++w) { int cw = lds[w]; lds[w] = tot; tot += cw; }
+        lds[2 * NW] = tot ? atomicAdd(counter, tot) : 0;
+    }
+    __syncthreads();
+    o0 = p0 ? lds[2 * NW] + lds[wave] + r0 : -1;
+    o1 = p1 ? lds[2 * NW] + lds[NW + wave] + r1 : -1;
+    __syncthreads();
+}
+
 // Work distribution of the persistent queue kernels over a sharded queue (rt_internal.h QueueView).
 __device__ __forceinline__ int q_len(const QueueView& q, int j) {
     if (q.len) return q.len[j * kQStride];
@@ -495,6 +516,50 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
             store8(out.lamA, out.lamB, s, lam);
         }
     }
+}
+
+// Dense spectra in LDS (DevSpectra::SPK, {SR, SG, SB, D65} per nm, 7.5 KB): the hero wavelengths of a wave are spread
+// over 360..830 nm, so a dense_query from global memory is a gather over ~15 cache lines per wave-instruction, and
+// the sensor conversion makes 24 of them per sample; from LDS it is one ds_read_b128 per wavelength.  Same values,
+// same index (spectrum.h:386-398: lround(λ) - 360, 0 outside the table), same arithmetic order: bit-identical.
+#ifndef RT_SPEC_LDS
+#define RT_SPEC_LDS 1
+#endif
+__shared__ float4 g_spk[kSpecN];
+__device__ __forceinline__ void stage_spectra(const DevSpectra* sp) {
+#if RT_SPEC_LDS
+    for (int i = threadIdx.x; i < kSpecN; i += blockDim.x) g_spk[i] = sp->SPK[i];
+    __syncthreads();
+#endif
+}
+__device__ __forceinline__ float4 spk_query(const DevSpectra* sp, float lambda) {
+    long off = (long)roundf(lambda) - 360;  // std::lround: half away from zero
+    if (off < 0 || off >= kSpecN) return make_float4(0.f, 0.f, 0.f, 0.f);
+#if RT_SPEC_LDS
+    return g_spk[off];
+#else
+    return sp->SPK[off];
+#endif
+}
+__device__ __forceinline__ float d65_query(const DevSpectra* sp, float lambda) { return spk_query(sp, lambda).w; }
+// pixelsensor.h:81-87 (to_sensor_rgb, rt_device.h) over the staged table: per channel the same sum in the same order
+__device__ __forceinline__ void to_sensor_rgb_spk(const DevSpectra* sp, const float L_[8], const float lam[8],
+                                                  const float pdf[8], float ir, float rgb[3]) {
+    float L[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) L[i] = (pdf[i] != 0) ? L_[i] / pdf[i] : 0.f;
+    float4 q = spk_query(sp, lam[0]);
+    float sr = q.x * L[0], sg = q.y * L[0], sb = q.z * L[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+        q = spk_query(sp, lam[i]);
+        sr += q.x * L[i];
+        sg += q.y * L[i];
+        sb += q.z * L[i];
+    }
+    rgb[0] = ir * (sr / 8);
+    rgb[1] = ir * (sg / 8);
+    rgb[2] = ir * (sb / 8);
 }
 
 // Loads through the constant address space: with a wave-uniform index they become s_load (scalar cache).
@@ -1343,6 +1408,12 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 #define RT_MULTI_WAVES 4  // the one tuning macro left: variant builds for A/B (Makefile `variants`)
 #endif
 #define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_MULTI_WAVES)))
+#ifndef RT_SHADE_PREFETCH
+#define RT_SHADE_PREFETCH 0  // single-leaf shade: the chunk's second item's slot and hit loaded with the first's
+#endif
+#ifndef RT_PAIR_APPEND
+#define RT_PAIR_APPEND 0  // single-leaf shade: one append per static chunk (two items) instead of per item
+#endif
 #ifndef RT_SHADE1_WAVES
 #define RT_SHADE1_WAVES 4  // the single-leaf simple-path shade (Cornell)
 #endif
@@ -1513,7 +1584,7 @@ __device__ __forceinline__ void li_reference(const DevScene& sc, const DevSpectr
     float cosv = gclamp(vdot(n, v3(0, 0, -1)), 0.0f, 1.0f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        float light = (io.illum_scale * sigmoid_eval(0, 0, io.illum_c2, lam[i])) * dense_query(sp->D65, lam[i]);
+        float light = (io.illum_scale * sigmoid_eval(0, 0, io.illum_c2, lam[i])) * d65_query(sp, lam[i]);
         float amb = piecewise_query(sp->f1_lambda, sp->f1_value, sp->f1_n, lam[i]) * 0.3f;
         float mat = sigmoid_eval(0, 0, io.albedo_c2, lam[i]);
         float r = 0.0f + amb;
@@ -1526,6 +1597,7 @@ __device__ __forceinline__ void li_reference(const DevScene& sc, const DevSpectr
 // indices in increasing order — the same per-pixel summation order as the reference's passes.
 __global__ void __launch_bounds__(kBlock) k_ref_shade_film(DevScene sc, const DevSpectra* sp, DevFilm film,
                                                            ShadeRefIO io, unsigned long long* ctr) {
+    stage_spectra(sp);
     ctr_t ns = 0;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < io.n_pixels; j += gridDim.x * blockDim.x) {
         int pixel = io.work_pixels[j];
@@ -1536,7 +1608,7 @@ __global__ void __launch_bounds__(kBlock) k_ref_shade_film(DevScene sc, const De
             load8(io.lamA, io.lamB, s, lam);
             load8(io.pdfA, io.pdfB, s, pdf);
             li_reference(sc, sp, io, s, lam, L);
-            to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
+            to_sensor_rgb_spk(sp, L, lam, pdf, film.imaging_ratio, rgb);
             const float w = 1.0f;  // FilterSample::weight (Box and Triangle both return 1)
             f.x += w * gclamp(rgb[0], 0.0f, 1.0f);
             f.y += w * gclamp(rgb[1], 0.0f, 1.0f);
@@ -1550,13 +1622,14 @@ __global__ void __launch_bounds__(kBlock) k_ref_shade_film(DevScene sc, const De
 }
 
 __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, ShadeRefIO sio, RecordIO io) {
+    stage_spectra(sp);
     int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= io.n) return;
     float lam[8], pdf[8], L[8], rgb[3];
     load8(io.lamA, io.lamB, s, lam);
     load8(io.pdfA, io.pdfB, s, pdf);
     li_reference(sc, sp, sio, s, lam, L);
-    to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
+    to_sensor_rgb_spk(sp, L, lam, pdf, film.imaging_ratio, rgb);
     float* r = io.out + (size_t)s * io.stride;
     for (int i = 0; i < 8; ++i) { r[i] = lam[i]; r[8 + i] = pdf[i]; }
     float4 o = io.rayO[s << io.rsh], d = io.rayD[s << io.rsh];
@@ -1622,9 +1695,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                                                                          unsigned long long* ctr, ShadowQueueIO shq) {
     const float InvPi = 0.31830988618379067154f;
     bool lds_tris = false;
+    stage_spectra(sp);
     stage_scene<QCAP>(sc, 0);
     if constexpr (QCAP == 1) lds_tris = stage_tris1(sc);
-    __shared__ int lds[kBlock / 64 + 1];
+    __shared__ int lds[2 * (kBlock / 64) + 1];
+#if RT_PAIR_APPEND
+    // single leaf: the first item of a static chunk parks its bounce ray here; the second item appends both
+    __shared__ float4 pend[QCAP == 1 ? 2 * kBlock : 1];
+    bool pend0 = false;
+#endif
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
@@ -1634,6 +1713,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<WAVE>> items(io.ticket, io.q);
     int qj, qidx;
     bool live;
+#if RT_SHADE_PREFETCH
+    int nslot = -1, nprim = -1;  // single leaf: the chunk's second item's (slot, hit), loaded with the first item's
+#endif
     while (items.next(qj, qidx, live)) {
         const int k = qj * io.q.S + qidx;  // queue position
         bool wantShadow = false, wantNext = false, storedL = false;
@@ -1642,9 +1724,27 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         float stmax = 0.f;
         float Ld[8];
         int slot = -1;
+#if RT_SHADE_PREFETCH
+        int prim = -1;
+        if constexpr (QCAP == 1) {
+            if (items.r == 1) {
+                if (live) { slot = __float_as_int(io.rayO[2 * k].w); prim = io.hitPrim[k]; }
+                const int k1 = k + kBlock;
+                if (k1 < items.n) { nslot = __float_as_int(io.rayO[2 * k1].w); nprim = io.hitPrim[k1]; }
+            } else {
+                slot = live ? nslot : -1;
+                prim = live ? nprim : -1;
+            }
+        } else if (live) {
+            slot = __float_as_int(io.rayO[2 * k].w);
+            prim = io.hitPrim[k];
+        }
+        if (live) {
+#else
         if (live) {
             slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
             const int prim = io.hitPrim[k];
+#endif
             if (prim >= 0) {
                 float lam[8], beta[8];
                 rload8(io.rec, slot, R_LAM, lam);
@@ -1671,7 +1771,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         float L[8];
                         rload8_or_zero(io.rec, slot, R_L, L, d0);
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.w * dense_query(sp->D65, lam[i]));
+                        for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.w * d65_query(sp, lam[i]));
                         rstore8(io.rec, slot, R_L, L);
                         storedL = true;
                     }
@@ -1706,7 +1806,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                             float wgt = G * Lq.area;
 #pragma unroll
                             for (int i = 0; i < 8; ++i)
-                                Ld[i] = ((beta[i] * (R[i] * InvPi)) * (le * dense_query(sp->D65, lam[i]))) * wgt;
+                                Ld[i] = ((beta[i] * (R[i] * InvPi)) * (le * d65_query(sp, lam[i]))) * wgt;
                             wantShadow = true;
                             so = po;
                             sd = wi;
@@ -1783,6 +1883,28 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
             const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             rstore8(io.rec, slot, R_L, z);
         }
+#if RT_PAIR_APPEND
+        if constexpr (QCAP == 1) {
+            nO.w = __int_as_float(slot);  // the ray's origin carries its slot
+            if (items.r == 1) {  // first item of the chunk
+                if (wantNext) { pend[2 * threadIdx.x] = nO; pend[2 * threadIdx.x + 1] = nD; }
+                pend0 = wantNext;
+            } else {
+                int p0, p1;
+                block_append2(io.nCount, pend0, wantNext, lds, p0, p1);
+                if (pend0) {
+                    const float4 o0 = pend[2 * threadIdx.x], d0v = pend[2 * threadIdx.x + 1];
+                    io.nO[2 * p0] = o0; io.nD[2 * p0] = d0v;
+                    if (io.nkey.key) io.nkey.key[p0] = ray_sort_key(o0, d0v, io.nkey);
+                }
+                if (wantNext) {
+                    io.nO[2 * p1] = nO; io.nD[2 * p1] = nD;
+                    if (io.nkey.key) io.nkey.key[p1] = ray_sort_key(nO, nD, io.nkey);
+                }
+            }
+            continue;
+        }
+#endif
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // the ray's origin carries its slot
@@ -1878,6 +2000,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                                                               NeeIO nee) {
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[kBlock / 64 + 1];
+    if constexpr (MC != 2) stage_spectra(sp);  // (the mirror / glass bin reads no spectrum table)
     const int nee_f4 = nee_stride(sc.n_lights);
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = QCAP != 1;
@@ -1941,7 +2064,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                         rload8(io.rec, slot, R_L, L);
                         if (prevPdf == 0) {
 #pragma unroll
-                            for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.emit * dense_query(sp->D65, lam[i]));
+                            for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.emit * d65_query(sp, lam[i]));
                         } else if (sc.mis && lidx >= 0) {
                             const DevLight& Lt = sc.lights[lidx];
                             V3 dv = vsub(p, ro);
@@ -1951,7 +2074,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                                 float wb = power_heuristic(prevPdf, dist2 / (cl * Lt.area));
 #pragma unroll
                                 for (int i = 0; i < 8; ++i)
-                                    L[i] += (beta[i] * (mt.emit * dense_query(sp->D65, lam[i]))) * wb;
+                                    L[i] += (beta[i] * (mt.emit * d65_query(sp, lam[i]))) * wb;
                             }
                         }
                         rstore8(io.rec, slot, R_L, L);
@@ -2134,6 +2257,7 @@ template <int QCAP, bool FB>
 #endif
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? 1 : (FB ? 2 : RT_NEE_WAVES)))) k_path_nee(DevScene sc, const DevSpectra* sp, PathIO io,
                                                                        NeeIO nee, unsigned long long* ctr) {
+    stage_spectra(sp);
     stage_scene<QCAP>(sc, 0);
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     const int nl = sc.n_lights, nf4 = nee_stride(nl);
@@ -2177,7 +2301,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                 const float wgt = wg[li];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    float Le = sc_le * dense_query(sp->D65, lam[i]);
+                    float Le = sc_le * d65_query(sp, lam[i]);
                     L[i] += ((x[i] * Le)) * wgt;
                 }
             }
@@ -2207,6 +2331,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
 // sensor + film for path mode (pixel-owned, index order)
 __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevFilm film, PathFilmIO io,
                                                       unsigned long long* ctr) {
+    stage_spectra(sp);
     ctr_t ns = 0;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < io.n_pixels; j += gridDim.x * blockDim.x) {
         int pixel = io.work_pixels[j];
@@ -2222,7 +2347,7 @@ __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevF
                 load8(io.pdfA, io.pdfB, s, pdf);
             }
             rload8(io.rec, s, R_L, L);
-            to_sensor_rgb(sp, L, lam, pdf, film.imaging_ratio, rgb);
+            to_sensor_rgb_spk(sp, L, lam, pdf, film.imaging_ratio, rgb);
             const float w = 1.0f;
             f.x += w * gclamp(rgb[0], 0.0f, 1.0f);
             f.y += w * gclamp(rgb[1], 0.0f, 1.0f);

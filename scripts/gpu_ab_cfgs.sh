@@ -7,6 +7,6 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu_tmp.log; [ $rc -ne 0 ] && exit $rc
 fi
 for c in ${CFGS:-cfg3 cfg4}; do
-  s=1; [ $c = cornell ] && s=4
+  s=${AB_STEPS:-2}; [ $c = cornell ] && s=${AB_STEPS_CORNELL:-6}
   echo "== $c"; BENCH_ARGS="--config $c" BENCH_STEPS=$s bash scripts/gpu_ab.sh || exit 1
 done
