@@ -33,14 +33,16 @@ RT_DEV void sincos_det(float x, float& s, float& c) {
 // (float)atanh((double)x) / (float)cosh((double)x) as the oracle computes them: the fast double evaluation of
 // rt_mathf.h, and the full-precision library call only when that result is within 2^-46 of a float rounding midpoint
 // (about 1 input in 3.4e7; tools/verify_warps.cpp checks every input float of the warps against glibc)
+template <class T = rtm::TabConst>
 RT_DEV float f_atanh(float x) {
-    double r = rtm::atanh_fast(x);
+    double r = rtm::atanh_fast<T>(x);
     float f = (float)r;
     if (rtm::near_midpoint(r, f)) f = (float)atanh((double)x);
     return f;
 }
+template <class T = rtm::TabConst>
 RT_DEV float f_cosh(float x) {
-    double r = rtm::cosh_fast(x);
+    double r = rtm::cosh_fast<T>(x);
     float f = (float)r;
     if (rtm::near_midpoint(r, f)) f = (float)cosh((double)x);
     return f;
@@ -323,13 +325,15 @@ struct Smp {
 };
 
 // ------------------------------------------------------------------------------ sampling warps
+template <class T = rtm::TabConst>
 RT_DEV float visible_pdf(float lambda) {  // Sampling.h:63-67
     if (lambda < 360 || lambda > 830) return 0;
-    float c = f_cosh(0.0072f * (lambda - 538));
+    float c = f_cosh<T>(0.0072f * (lambda - 538));
     return (float)((double)0.0039398042f / ((double)c * (double)c));
 }
+template <class T = rtm::TabConst>
 RT_DEV float sample_visible_wavelength(float u) {  // Sampling.h:69-71
-    return 538 - 138.888889f * f_atanh(0.85691062f - 1.82750197f * u);
+    return 538 - 138.888889f * f_atanh<T>(0.85691062f - 1.82750197f * u);
 }
 RT_DEV float sample_linear(float u, float a, float b) {  // Sampling.h:205-211
     if (u == 0 && a == 0) return 0;

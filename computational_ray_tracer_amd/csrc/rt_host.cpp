@@ -2038,6 +2038,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     d.n_nodes = nn;
     d.n_tris = nt;
     d.n_shapes = s->n_shapes;
+    d.n_materials = (int)mats.size();
     c->scene_full = full;
     d.qcap = qcap;
     d.depth = nn < (1 << 24) ? maxd : 1 << 30;  // DFS stack entries hold 24-bit group ids

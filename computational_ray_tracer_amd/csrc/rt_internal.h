@@ -121,6 +121,7 @@ struct DevScene {
     int n_tris;
     int n_shapes;
     int n_lights;
+    int n_materials;                // entries of materials (>= 1)
     int mis;                        // RT_INTEGRATOR_PATH_MIS
     int full;                       // path shading needs the general kernel (shapes, specular, >1 / non-quad lights, MIS)
     DevLight light0;

@@ -108,6 +108,31 @@ __device__ __forceinline__ bool stage_tris1(const DevScene& sc) {
     __syncthreads();
     return ok;
 }
+// Mixed-scene material table in LDS (<= kLdsMats entries, 32 B each): the shade and binning kernels look up the
+// material of every hit (prim -> triMaterial -> material), so staging the table removes the chain's last global
+// round trip.  Larger tables stay in global memory (mat_at reads through the pointer).
+#ifndef RT_MAT_LDS
+#define RT_MAT_LDS 1
+#endif
+static constexpr int kLdsMats = 64;
+__shared__ DevMaterial g_mat[kLdsMats];
+__device__ __forceinline__ bool stage_materials(const DevScene& sc) {
+#if RT_MAT_LDS
+    const bool ok = sc.n_materials <= kLdsMats;
+    if (ok)
+        for (int i = threadIdx.x; i < sc.n_materials; i += blockDim.x) g_mat[i] = sc.materials[i];
+    __syncthreads();
+    return ok;
+#else
+    return false;
+#endif
+}
+__device__ __forceinline__ DevMaterial mat_at(const DevScene& sc, bool lds, int m) {
+#if RT_MAT_LDS
+    if (lds) return g_mat[m];
+#endif
+    return sc.materials[m];
+}
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -415,12 +440,38 @@ __device__ __forceinline__ void rec_set_prev_pdf(const RecView& r, int slot, flo
     reinterpret_cast<float*>(recf(r, slot, R_MISC))[1] = p;
 }
 
+// The wavelength warps' tables (rt_logtab.h: 97 log rows of 3 doubles, 64 exp rows of 2) staged in LDS by the
+// kernels that evaluate the warps for every sample (k_generate: 8 atanh = 16 log rows; k_path_film: 8 cosh = 16
+// exp rows): the rows are indexed per lane, so from the constant arrays each is a divergent vector-memory load.
+#ifndef RT_WARP_LDS
+#define RT_WARP_LDS 1
+#endif
+__shared__ double g_logtab[rtm::kLogN][4];  // (row padded to 32 B: one ds_read_b128 + one ds_read_b64)
+__shared__ double g_exptab[64][2];
+struct WarpTabLds {
+    __device__ static const double* logrow(int j) { return g_logtab[j]; }
+    __device__ static const double* exprow(int j) { return g_exptab[j]; }
+};
+#if RT_WARP_LDS
+using WarpTab = WarpTabLds;
+#else
+using WarpTab = rtm::TabConst;
+#endif
+__device__ __forceinline__ void stage_warp_tables() {
+#if RT_WARP_LDS
+    for (int i = threadIdx.x; i < rtm::kLogN * 3; i += blockDim.x) g_logtab[i / 3][i % 3] = rtm::kLogTab[i / 3][i % 3];
+    for (int i = threadIdx.x; i < 64 * 2; i += blockDim.x) g_exptab[i / 2][i % 2] = rtm::kExp2Tab[i / 2][i % 2];
+    __syncthreads();
+#endif
+}
+
 // ===================================================================================== K1 generate
 // RayTracerTestApp.h:305-323: StartPixelSample → SampleVisible(Get1D) → filter.Sample(GetPixel2D) →
 // pixel + .5 + p → PerspectiveCamera::generateRay (Cameras.h:273-297) → Ray::Transform (Shapes.h:37-41).
 // 4 waves/SIMD (158 -> 128 VGPRs, 112 B/lane spill): +3 % on the Cornell box
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
                                                      DevFilm film, GenOut out) {
+    stage_warp_tables();
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nS; s += gridDim.x * blockDim.x) {
         int pixel, index, x, y;
         sample_of(ids, s, pixel, index);
@@ -433,8 +484,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         for (int i = 0; i < 8; ++i) {  // spectrum.h:322-336
             float up = u + float(i) / 8;
             if (up > 1) up -= 1;
-            lam[i] = sample_visible_wavelength(up);
-            pdf[i] = out.lean ? 0.f : visible_pdf(lam[i]);
+            lam[i] = sample_visible_wavelength<WarpTab>(up);
+            pdf[i] = out.lean ? 0.f : visible_pdf<WarpTab>(lam[i]);
         }
         float u0, u1;
         sm.get_pixel2d(smp, u0, u1);  // Sampler::GetPixel2D (RayTracerTestApp.h:316)
@@ -1412,7 +1463,7 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 #define RT_SHADE_PREFETCH 0  // single-leaf shade: the chunk's second item's slot and hit loaded with the first's
 #endif
 #ifndef RT_PAIR_APPEND
-#define RT_PAIR_APPEND 0  // single-leaf shade: one append per static chunk (two items) instead of per item
+#define RT_PAIR_APPEND 1  // single-leaf shade: one append per static chunk (two items) instead of per item (Cornell +3.5 %, r03)
 #endif
 #ifndef RT_SHADE1_WAVES
 #define RT_SHADE1_WAVES 4  // the single-leaf simple-path shade (Cornell)
@@ -1516,6 +1567,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_materials(DevScene sc, BinIO io)
     __shared__ int base[kMatClasses];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
+    const bool lds_mats = stage_materials(sc);
     int mx = 0;
 #pragma unroll
     for (int j = 0; j < kShards; ++j) {
@@ -1534,7 +1586,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_materials(DevScene sc, BinIO io)
             if (idx < len) {
                 const int prim = io.hitPrim[j * io.q.S + idx];
                 if (prim >= 0)
-                    cls[r] = sc.materials[prim < sc.n_tris ? sc.triMaterial[prim] : sc.shapes[prim - sc.n_tris].material].cls;
+                    cls[r] = mat_at(sc, lds_mats, prim < sc.n_tris ? sc.triMaterial[prim] : sc.shapes[prim - sc.n_tris].material).cls;
             }
         }
 #pragma unroll
@@ -1759,6 +1811,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                     P0 = g_tri1[4 * prim]; P1 = g_tri1[4 * prim + 1]; P2 = g_tri1[4 * prim + 2]; mt = g_tri1[4 * prim + 3];
                 } else {
                     P0 = sc.triWorld[3 * prim]; P1 = sc.triWorld[3 * prim + 1]; P2 = sc.triWorld[3 * prim + 2];
+                    // (the material table stays in global memory here: staged in LDS, CFG3 -3.5 %, r03 A/B)
                     const DevMaterial dm = sc.materials[sc.triMaterial[prim]];
                     mt = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
                 }
@@ -2001,6 +2054,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
     const float InvPi = 0.31830988618379067154f;
     __shared__ int lds[kBlock / 64 + 1];
     if constexpr (MC != 2) stage_spectra(sp);  // (the mirror / glass bin reads no spectrum table)
+    const bool lds_mats = stage_materials(sc);
     const int nee_f4 = nee_stride(sc.n_lights);
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = QCAP != 1;
@@ -2040,7 +2094,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                     nrm = ng;
                     if (vdot(nrm, rayd) > 0) nrm = v3(-ng.x, -ng.y, -ng.z);
                     mid = sc.triMaterial[prim];
-                    lidx = sc.materials[mid].light;
+                    lidx = mat_at(sc, lds_mats, mid).light;
                 } else {
                     const DevShape& s = sc.shapes[prim - sc.n_tris];
                     V3 rdo = vnorm(m4_dir(s.r2o, rdw));
@@ -2056,7 +2110,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(
                     mid = s.material;
                     lidx = s.light;
                 }
-                const DevMaterial mt = sc.materials[mid];
+                const DevMaterial mt = mat_at(sc, lds_mats, mid);
                 float prevPdf = rec_prev_pdf(io.rec, slot);
                 if (MC != 2 && mt.emit > 0) {  // one-sided pure emitter, ends the path
                     if (front) {
@@ -2332,6 +2386,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
 __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevFilm film, PathFilmIO io,
                                                       unsigned long long* ctr) {
     stage_spectra(sp);
+    if (io.lean) stage_warp_tables();  // (block-uniform)
     ctr_t ns = 0;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < io.n_pixels; j += gridDim.x * blockDim.x) {
         int pixel = io.work_pixels[j];
@@ -2342,7 +2397,7 @@ __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevF
             rload8(io.rec, s, R_LAM, lam);
             if (io.lean) {
 #pragma unroll
-                for (int w = 0; w < 8; ++w) pdf[w] = visible_pdf(lam[w]);  // the value k_generate would have stored
+                for (int w = 0; w < 8; ++w) pdf[w] = visible_pdf<WarpTab>(lam[w]);  // the value k_generate would have stored
             } else {
                 load8(io.pdfA, io.pdfB, s, pdf);
             }

@@ -9,7 +9,7 @@
 //   per pass of <= 8 key bits:
 //   k_rs_hist     block b counts the digits of its chunk of the (concatenated) queue in LDS;
 //   k_rs_offsets  block = digit: the exclusive scan of the digit's counts over the blocks and the digit's total;
-//   k_rs_scatter  block b scans the digit totals into digit starts, then walks its chunk in tiles of 256 items in
+//   k_rs_scatter  block b scans the digit totals into digit starts, then walks its chunk in tiles of kRsTile items in
 //                 order; a wave ranks its items among the same
 //                 digit with kRsBits ballots (stable: lane order), the tile's waves are prefixed per digit through
 //                 LDS, and a running count per digit (one digit per thread) carries the order across tiles.  The
@@ -25,10 +25,14 @@
 namespace rtmi {
 namespace {
 
-constexpr int kRsMaxBits = 8, kRsBins = 1 << kRsMaxBits;
+#ifndef RT_RS_BITS
+#define RT_RS_BITS 8  // digit width (variant builds: 9 = 512 digits, 512-thread blocks)
+#endif
+constexpr int kRsMaxBits = RT_RS_BITS, kRsBins = 1 << kRsMaxBits;
 constexpr int kRsGrid = 1024;          // blocks of the histogram / scatter kernels (4 per CU)
-constexpr int kRsTile = kBlockThreads;  // items per tile: one per thread
-static_assert(kRsTile == kRsBins, "one digit per thread in k_rs_scatter / k_rs_offsets");
+constexpr int kRsThreads = kRsBins;    // threads per histogram / scatter block: one digit per thread
+constexpr int kRsTile = kRsThreads;    // items per tile: one per thread
+static_assert(kRsThreads % 64 == 0 && kRsThreads <= 1024, "whole waves");
 
 // meta: [0] n, [1 .. kShards + 1] the exclusive prefix of the shard lengths
 __global__ void k_rs_prep(const int* __restrict__ len, int* __restrict__ meta) {
@@ -99,7 +103,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 template <int SRC>
-__global__ void __launch_bounds__(kBlockThreads) k_rs_hist(RsPass p) {
+__global__ void __launch_bounds__(kRsThreads) k_rs_hist(RsPass p) {
     constexpr int U = 4;  // items in flight per thread
     __shared__ int h[kRsBins];
     h[threadIdx.x] = 0;
@@ -107,18 +111,18 @@ __global__ void __launch_bounds__(kBlockThreads) k_rs_hist(RsPass p) {
     const int n = p.meta[0], c = rs_chunk(n);
     const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
     const unsigned mask = (1u << p.nbits) - 1u;
-    for (int k0 = b0 + (int)threadIdx.x; k0 < b1; k0 += U * kBlockThreads) {
+    for (int k0 = b0 + (int)threadIdx.x; k0 < b1; k0 += U * kRsThreads) {
         unsigned key[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int k = k0 + u * kBlockThreads;
+            const int k = k0 + u * kRsThreads;
             int val;
             key[u] = 0;
             if (k < b1) rs_load<SRC>(p, k, key[u], val);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (k0 + u * kBlockThreads < b1) atomicAdd(&h[(key[u] >> p.shift) & mask], 1);
+            if (k0 + u * kRsThreads < b1) atomicAdd(&h[(key[u] >> p.shift) & mask], 1);
     }
     __syncthreads();
     p.hist[threadIdx.x * kRsGrid + blockIdx.x] = h[threadIdx.x];  // digit-major: k_rs_offsets scans a digit's row
@@ -151,15 +155,15 @@ __device__ __forceinline__ int rs_lane() {
 }
 
 template <int SRC, int DST>
-__global__ void __launch_bounds__(kBlockThreads) k_rs_scatter(RsPass p) {
-    constexpr int NW = kBlockThreads / 64;
+__global__ void __launch_bounds__(kRsThreads) k_rs_scatter(RsPass p) {
+    constexpr int NW = kRsThreads / 64;
     __shared__ int wcnt[NW][kRsBins];
     __shared__ int wpre[NW][kRsBins];
     const int n = p.meta[0], c = rs_chunk(n);
     const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
     const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
     const unsigned mask = (1u << p.nbits) - 1u;
-    {  // the digits' starts: exclusive scan of the digit totals (Hillis-Steele over the 256 digits, in wpre[0])
+    {  // the digits' starts: exclusive scan of the digit totals (Hillis-Steele over the kRsBins digits, in wpre[0])
         int* sc = wpre[0];
         sc[tid] = p.tot[tid];
         __syncthreads();
@@ -228,9 +232,9 @@ __global__ void __launch_bounds__(kBlockThreads) k_rs_scatter(RsPass p) {
 
 template <int SRC, int DST>
 void rs_launch(hipStream_t st, const RsPass& p) {
-    hipLaunchKernelGGL(k_rs_hist<SRC>, dim3(kRsGrid), dim3(kBlockThreads), 0, st, p);
+    hipLaunchKernelGGL(k_rs_hist<SRC>, dim3(kRsGrid), dim3(kRsThreads), 0, st, p);
     hipLaunchKernelGGL(k_rs_offsets, dim3(kRsBins), dim3(kRsGrid), 0, st, p.hist, p.tot);
-    hipLaunchKernelGGL((k_rs_scatter<SRC, DST>), dim3(kRsGrid), dim3(kBlockThreads), 0, st, p);
+    hipLaunchKernelGGL((k_rs_scatter<SRC, DST>), dim3(kRsGrid), dim3(kRsThreads), 0, st, p);
 }
 
 // the passes of a `bits`-bit key, <= kRsMaxBits each (split evenly), ping-ponging between the two arrays
