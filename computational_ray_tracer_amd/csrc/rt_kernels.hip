@@ -33,7 +33,10 @@ __shared__ uint2 g_bstk[kBvhStack * kBlock];
 static_assert(sizeof(uint2) * kBvhStack >= 2 * kLdsQ, "the BFS FIFO lives in the BVH stack's LDS");
 // The any-hit walks' stacks: child words only (nothing to cull with a fixed tMax), 24 per lane: 24 KB per block, so
 // the any-hit kernels (shade, NEE) are not held to 4 blocks per CU by LDS.  The BFS FIFO stays in g_bstk.
-static constexpr int kAnyStack = 24;
+#ifndef RT_ANY_STACK
+#define RT_ANY_STACK 24
+#endif
+static constexpr int kAnyStack = RT_ANY_STACK;
 __shared__ unsigned g_astk[kAnyStack * kBlock];
 
 // Single-leaf scenes, closest-hit waves without a shared dominant axis (bounce rays): pass 1 runs on a compacted list
@@ -216,6 +219,9 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
 
 // Block-aggregated append of a static chunk's two items (kStaticItems = 2): one atomicAdd and one round of barriers
 // for both; the block's first items take the lower positions, its second items the upper ones.  lds: 2 NW + 1 ints.
+#ifndef RT_APPEND_DB
+#define RT_APPEND_DB 0
+#endif
 __device__ __forceinline__ void block_append2(int* counter, bool p0, bool p1, int* lds, int& o0, int& o1) {
     constexpr int NW = kBlock / 64;
     const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
@@ -232,7 +238,10 @@ __device__ __forceinline__ void block_append2(int* counter, bool p0, bool p1, in
     __syncthreads();
     o0 = p0 ? lds[2 * NW] + lds[wave] + r0 : -1;
     o1 = p1 ? lds[2 * NW] + lds[NW + wave] + r1 : -1;
-    __syncthreads();
+#if !RT_APPEND_DB
+    __syncthreads();  // (double-buffered callers alternate lds between two arrays instead: the next call's two
+                      // barriers separate these reads from the rewrite two calls later)
+#endif
 }
 
 // Work distribution of the persistent queue kernels over a sharded queue (rt_internal.h QueueView).
@@ -1751,6 +1760,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     stage_scene<QCAP>(sc, 0);
     if constexpr (QCAP == 1) lds_tris = stage_tris1(sc);
     __shared__ int lds[2 * (kBlock / 64) + 1];
+#if RT_APPEND_DB
+    __shared__ int lds_db[2][2 * (kBlock / 64) + 1];  // the pair append's two alternating arrays
+    int par = 0;
+#endif
 #if RT_PAIR_APPEND
     // single leaf: the first item of a static chunk parks its bounce ray here; the second item appends both
     __shared__ float4 pend[QCAP == 1 ? 2 * kBlock : 1];
@@ -1944,7 +1957,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                 pend0 = wantNext;
             } else {
                 int p0, p1;
+#if RT_APPEND_DB
+                block_append2(io.nCount, pend0, wantNext, lds_db[par], p0, p1);
+                par ^= 1;
+#else
                 block_append2(io.nCount, pend0, wantNext, lds, p0, p1);
+#endif
                 if (pend0) {
                     const float4 o0 = pend[2 * threadIdx.x], d0v = pend[2 * threadIdx.x + 1];
                     io.nO[2 * p0] = o0; io.nD[2 * p0] = d0v;
@@ -2047,7 +2065,10 @@ __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const f
 // MC (material class): 0 every material; 1 the Lambert-or-emitter bin, 2 the mirror-or-dielectric bin (items of
 // io.bin_idx: hits only, the trace kernel dropped the misses) — each bin kernel holds only its materials' code.
 template <int QCAP, int MC>
-__global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_path_shade_full(DevScene sc, const DevSpectra* sp,
+#ifndef RT_FULL_WAVES
+#define RT_FULL_WAVES RT_MULTI_WAVES  // the mixed-scene shade (variant builds)
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCAP == 1 ? 1 : RT_FULL_WAVES))) k_path_shade_full(DevScene sc, const DevSpectra* sp,
                                                                               DevSampler smp, DevFilm film,
                                                                               SampleIds ids, PathIO io,
                                                                               NeeIO nee) {
