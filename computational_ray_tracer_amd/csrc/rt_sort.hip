@@ -6,10 +6,10 @@
 //
 // A hand-written stable LSD radix sort that runs entirely on the device (no host read of the queue length):
 //   k_rs_prep     the queue's shard lengths -> n and the shard prefix (meta), read by every later kernel;
-//   per pass of <= 8 key bits:
+//   per pass of one digit (RB bits: 9 for the 18-bit ray key, 8 for the 24-bit NEE key):
 //   k_rs_hist     block b counts the digits of its chunk of the (concatenated) queue in LDS;
 //   k_rs_offsets  block = digit: the exclusive scan of the digit's counts over the blocks and the digit's total;
-//   k_rs_scatter  block b scans the digit totals into digit starts, then walks its chunk in tiles of kRsTile items in
+//   k_rs_scatter  block b scans the digit totals into digit starts, then walks its chunk in tiles of one item per thread in
 //                 order; a wave ranks its items among the same
 //                 digit with kRsBits ballots (stable: lane order), the tile's waves are prefixed per digit through
 //                 LDS, and a running count per digit (one digit per thread) carries the order across tiles.  The
@@ -25,14 +25,17 @@
 namespace rtmi {
 namespace {
 
-#ifndef RT_RS_BITS
-#define RT_RS_BITS 8  // digit width (variant builds: 9 = 512 digits, 512-thread blocks)
+// Digit width per sort (RB bits: 1 << RB digits, one per thread of a 1 << RB-thread block, tiles of 1 << RB items):
+// the 18-bit ray key sorts in 2 passes of 9 bits (r03 A/B: CFG3 +0.6 % over 3 passes of 6), the 24-bit NEE key in 3
+// passes of 8 (with 9-bit digits its passes cost more: CFG4 -0.7 %).
+#ifndef RT_RS_RAY_BITS
+#define RT_RS_RAY_BITS 9
 #endif
-constexpr int kRsMaxBits = RT_RS_BITS, kRsBins = 1 << kRsMaxBits;
-constexpr int kRsGrid = 1024;          // blocks of the histogram / scatter kernels (4 per CU)
-constexpr int kRsThreads = kRsBins;    // threads per histogram / scatter block: one digit per thread
-constexpr int kRsTile = kRsThreads;    // items per tile: one per thread
-static_assert(kRsThreads % 64 == 0 && kRsThreads <= 1024, "whole waves");
+#ifndef RT_RS_NEE_BITS
+#define RT_RS_NEE_BITS 8
+#endif
+constexpr int kRsGrid = 1024;  // blocks of the histogram / scatter kernels (4 per CU)
+constexpr int kRsBinsMax = 512;
 
 // meta: [0] n, [1 .. kShards + 1] the exclusive prefix of the shard lengths
 __global__ void k_rs_prep(const int* __restrict__ len, int* __restrict__ meta) {
@@ -47,6 +50,7 @@ __global__ void k_rs_prep(const int* __restrict__ len, int* __restrict__ meta) {
     }
 }
 
+template <int kRsTile>
 __device__ __forceinline__ int rs_chunk(int n) {  // items per block: a multiple of the tile
     const int c = (n + kRsGrid - 1) / kRsGrid;
     return (c + kRsTile - 1) / kRsTile * kRsTile;
@@ -102,13 +106,14 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <int SRC>
-__global__ void __launch_bounds__(kRsThreads) k_rs_hist(RsPass p) {
+template <int SRC, int RB>
+__global__ void __launch_bounds__(1 << RB) k_rs_hist(RsPass p) {
+    constexpr int kRsBins = 1 << RB, kRsThreads = kRsBins;
     constexpr int U = 4;  // items in flight per thread
     __shared__ int h[kRsBins];
     h[threadIdx.x] = 0;
     __syncthreads();
-    const int n = p.meta[0], c = rs_chunk(n);
+    const int n = p.meta[0], c = rs_chunk<kRsThreads>(n);
     const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
     const unsigned mask = (1u << p.nbits) - 1u;
     for (int k0 = b0 + (int)threadIdx.x; k0 < b1; k0 += U * kRsThreads) {
@@ -154,12 +159,13 @@ __device__ __forceinline__ int rs_lane() {
     return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
-template <int SRC, int DST>
-__global__ void __launch_bounds__(kRsThreads) k_rs_scatter(RsPass p) {
+template <int SRC, int DST, int RB>
+__global__ void __launch_bounds__(1 << RB) k_rs_scatter(RsPass p) {
+    constexpr int kRsBins = 1 << RB, kRsThreads = kRsBins, kRsTile = kRsThreads;
     constexpr int NW = kRsThreads / 64;
     __shared__ int wcnt[NW][kRsBins];
     __shared__ int wpre[NW][kRsBins];
-    const int n = p.meta[0], c = rs_chunk(n);
+    const int n = p.meta[0], c = rs_chunk<kRsTile>(n);
     const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
     const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
     const unsigned mask = (1u << p.nbits) - 1u;
@@ -230,18 +236,19 @@ __global__ void __launch_bounds__(kRsThreads) k_rs_scatter(RsPass p) {
     }
 }
 
-template <int SRC, int DST>
+template <int SRC, int DST, int RB>
 void rs_launch(hipStream_t st, const RsPass& p) {
-    hipLaunchKernelGGL(k_rs_hist<SRC>, dim3(kRsGrid), dim3(kRsThreads), 0, st, p);
-    hipLaunchKernelGGL(k_rs_offsets, dim3(kRsBins), dim3(kRsGrid), 0, st, p.hist, p.tot);
-    hipLaunchKernelGGL((k_rs_scatter<SRC, DST>), dim3(kRsGrid), dim3(kRsThreads), 0, st, p);
+    hipLaunchKernelGGL((k_rs_hist<SRC, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
+    hipLaunchKernelGGL(k_rs_offsets, dim3(1 << RB), dim3(kRsGrid), 0, st, p.hist, p.tot);
+    hipLaunchKernelGGL((k_rs_scatter<SRC, DST, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
 }
 
-// the passes of a `bits`-bit key, <= kRsMaxBits each (split evenly), ping-ponging between the two arrays
-template <int SRC, int DST>
+// the passes of a `bits`-bit key, <= RB bits each (split evenly), ping-ponging between the two arrays
+template <int SRC, int DST, int RB>
 hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* kb, int* va, int* vb) {
+    static_assert(RB >= 6 && (1 << RB) <= kRsBinsMax, "digit width");
     // (the NEE queue is sorted in place: its first pass must finish reading the slots before any is rewritten)
-    const int passes = std::max((bits + kRsMaxBits - 1) / kRsMaxBits, DST == DST_NEEQ ? 2 : 1);
+    const int passes = std::max((bits + RB - 1) / RB, DST == DST_NEEQ ? 2 : 1);
     const int per = (bits + passes - 1) / passes;
     hipLaunchKernelGGL(k_rs_prep, dim3(1), dim3(64), 0, st, p.len, const_cast<int*>(p.meta));
     for (int i = 0; i < passes; ++i) {
@@ -250,10 +257,10 @@ hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* k
         const bool first = i == 0, last = i == passes - 1;
         p.keys_out = (i & 1) ? kb : ka;
         p.vals_out = (i & 1) ? vb : va;
-        if (first && last) rs_launch<SRC, DST>(st, p);
-        else if (first) rs_launch<SRC, DST_ARRAY>(st, p);
-        else if (last) rs_launch<SRC_ARRAY, DST>(st, p);
-        else rs_launch<SRC_ARRAY, DST_ARRAY>(st, p);
+        if (first && last) rs_launch<SRC, DST, RB>(st, p);
+        else if (first) rs_launch<SRC, DST_ARRAY, RB>(st, p);
+        else if (last) rs_launch<SRC_ARRAY, DST, RB>(st, p);
+        else rs_launch<SRC_ARRAY, DST_ARRAY, RB>(st, p);
         p.keys_in = p.keys_out;
         p.vals_in = p.vals_out;
     }
@@ -262,34 +269,34 @@ hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* k
 
 }  // namespace
 
-size_t sort_temp_bytes() { return sizeof(int) * ((size_t)kRsGrid * kRsBins + kRsBins + 64); }
+size_t sort_temp_bytes() { return sizeof(int) * ((size_t)kRsGrid * kRsBinsMax + kRsBinsMax + 64); }
 
 hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io) {
     RsPass p{};
     int* hist = static_cast<int*>(io.temp);
     p.hist = hist;
-    p.tot = hist + (size_t)kRsGrid * kRsBins;
-    p.meta = p.tot + kRsBins;
+    p.tot = hist + (size_t)kRsGrid * kRsBinsMax;
+    p.meta = p.tot + kRsBinsMax;
     p.S = io.S;
     p.qkey = io.qkey;
     p.nslot = io.perm;
     p.len = io.len;
     const int bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
-    return rs_sort<SRC_RAYQ, DST_PERM>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
+    return rs_sort<SRC_RAYQ, DST_PERM, RT_RS_RAY_BITS>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io) {
     RsPass p{};
     int* hist = static_cast<int*>(io.temp);
     p.hist = hist;
-    p.tot = hist + (size_t)kRsGrid * kRsBins;
-    p.meta = p.tot + kRsBins;
+    p.tot = hist + (size_t)kRsGrid * kRsBinsMax;
+    p.meta = p.tot + kRsBinsMax;
     p.S = io.S;
     p.qkey = io.key;
     p.qslot = io.slot;
     p.nslot = io.slot;  // in place: the first pass copied the slots into the values
     p.len = io.len;
-    return rs_sort<SRC_NEEQ, DST_NEEQ>(st, 3 * io.org_bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
+    return rs_sort<SRC_NEEQ, DST_NEEQ, RT_RS_NEE_BITS>(st, 3 * io.org_bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 }  // namespace rtmi
