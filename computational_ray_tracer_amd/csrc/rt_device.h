@@ -177,6 +177,9 @@ struct Pcg {  // rng.h:24-144
     RT_DEV void advance(uint64_t delta);
 };
 
+#ifndef RT_PCG_UNIFORM
+#define RT_PCG_UNIFORM 0
+#endif
 struct PcgJumpTable {
     uint64_t mult[64], plus[64];
 };
@@ -194,6 +197,25 @@ constexpr PcgJumpTable make_pcg_jump() {
 __constant__ constexpr PcgJumpTable kPcgJump = make_pcg_jump();
 
 RT_DEV void Pcg::advance(uint64_t delta) {
+#if RT_PCG_UNIFORM
+    // accPlus is inc times a value P(delta) of the jump table alone (the recurrence is linear in inc, mod 2^64), so
+    // the loop does not depend on the lane; when the wave shares delta (k_generate: one sample index per wave) it runs
+    // once per wave on the scalar unit, and each lane makes two 64-bit multiply-adds
+    const uint32_t lo = (uint32_t)delta, hi = (uint32_t)(delta >> 32);
+    const uint32_t lo0 = __builtin_amdgcn_readfirstlane(lo), hi0 = __builtin_amdgcn_readfirstlane(hi);
+    if (__ballot(lo != lo0 || hi != hi0) == 0) {
+        uint64_t d = (uint64_t)lo0 | ((uint64_t)hi0 << 32), M = 1u, P = 0u;
+        for (int i = 0; d > 0; ++i, d >>= 1) {
+            if (d & 1) {
+                const uint64_t cm = kPcgJump.mult[i];
+                M *= cm;
+                P = P * cm + kPcgJump.plus[i];
+            }
+        }
+        state = M * state + inc * P;
+        return;
+    }
+#endif
     uint64_t accMult = 1u, accPlus = 0u;
     for (int i = 0; delta > 0; ++i, delta >>= 1) {
         if (delta & 1) {
