@@ -178,7 +178,7 @@ struct Pcg {  // rng.h:24-144
 };
 
 #ifndef RT_PCG_UNIFORM
-#define RT_PCG_UNIFORM 0  // (r03 A/B: Cornell +0.5 %, k_generate -6 %; off in the round-3 build: see DESIGN §4)
+#define RT_PCG_UNIFORM 1  // (r03 A/B: Cornell +0.5 %, k_generate -6 %)
 #endif
 struct PcgJumpTable {
     uint64_t mult[64], plus[64];
