@@ -46,6 +46,9 @@ def parse():
                    help="cornell = BASELINE configs[1] (the metric's workload); cfg3..cfg5 = configs[2..4]")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    p.add_argument("--project-shards", type=int, default=8,
+                   help="N=1 only: render each of the N pixel-tile shards of an N-GPU run on this GPU alone and project "
+                        "the tile-parallel efficiency at N GPUs (0: off)")
     return p.parse_args()
 
 
@@ -80,11 +83,12 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=Fa
                     "total_ms": round(st["ms_shadow"], 3)}
     elif st["ms_shadow"] > 0:  # shadow rays in a kernel of their own, one launch per shade launch: the §8(d) 32 B
         # per shadow ray and the shadow scene terms move to it (k_path_nee: mixed scenes; k_path_shadow: shadow queue)
-        # k_path_nee also reads each vertex's NEE record (rt_internal.h NeeIO: 16 B + 16 B per light + 4 B weight
-        # per light + 32 B, i.e. 128 B with 4 lights) once for its n_lights shadow rays
-        rec = 16 * (1 + n_lights + (n_lights + 3) // 4 + 2)
+        # k_path_nee also reads each vertex's NEE record once (rt_internal.h NeeIO: po + material 16 B, the light
+        # samples 8 B and weights 4 B per light: 64 B with 4 lights) and the slot's λ, β, L (96 B), and writes L and
+        # β (64 B); vertices counted on the device (rt_stats nee_vertices)
+        rec = 16 * (1 + (n_lights + 1) // 2 + (n_lights + 3) // 4) + 96 + 64
         ks[shadow_kernel] = (st["ms_shadow"], st["launches_shade"],
-                             32 * st["shadow_rays"] + (rec * st["shadow_rays"] // max(1, n_lights)
+                             32 * st["shadow_rays"] + (rec * st.get("nee_vertices", 0)
                                                        if shadow_kernel == "k_path_nee" else 0),
                              32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"])
         ks["k_path_shade"] = (st["ms_shade"], st["launches_shade"], 312 * st["rays"], 0)
@@ -158,39 +162,105 @@ def single_lane_pass(cfg, world, rank, spp_per_step, steps):
     return st, dt
 
 
+def effective_cpus():
+    """CPUs this process may actually use: the affinity mask, capped by the cgroup CPU quota (cgroup v2 cpu.max or v1
+    cfs_quota_us / cfs_period_us).  os.cpu_count() reports the whole machine (256 on the GPU boxes) although a
+    one-GPU box's container gets a share of it."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota, src = None, "none"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        src = f"cgroup v2 cpu.max = {q} {per}"
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            src = f"cgroup v1 cfs_quota_us = {q}, cfs_period_us = {per}"
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    eff = aff if quota is None else max(1, min(aff, int(quota)))
+    return eff, {"affinity_cpus": aff, "nproc": os.cpu_count(), "cgroup_quota_cpus": quota, "cgroup": src}
+
+
+def project_shards(r, cfg, n, spp_per_step, steps, warmup, stream):
+    """Tile-parallel efficiency at n GPUs projected from one GPU (RayTracerTestApp.h:372-397 is the
+    dispatch this replaces): rank k of an n-GPU run renders shard k of rt_set_shard(32, n, k) — every n-th 32x32
+    tile — for spp_per_step * n sample indices per step (weak scaling: the same samples per GPU as the 1-GPU step).
+    Each shard is rendered here alone, for the same number of steps; a step of the n-GPU run lasts as long as its
+    slowest shard, so the efficiency is mean / max of the per-shard step times (the once-per-frame film reduce is
+    not included: 33 MB per frame at 1080p over xGMI)."""
+    W, H = cfg.film.res
+    film = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
+    per, spp = spp_per_step * n, cfg.sampler.spp()
+    rows = []
+    for k in range(n):
+        r.set_shard(32, n, k)
+        i0 = 0
+
+        def step():
+            nonlocal i0
+            if i0 + per > spp:
+                i0 = 0
+            r.render_pass_device(i0, min(spp, i0 + per), film.data_ptr(), stream.cuda_stream)
+            i0 += per
+
+        for _ in range(max(1, warmup)):
+            step()
+        torch.cuda.synchronize()
+        r.reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        rows.append({"shard": k, "ms_per_step": round(dt * 1e3, 3), "samples_per_step": int(r.stats()["samples"] / steps)})
+    ms = [x["ms_per_step"] for x in rows]
+    return {"n": n, "efficiency": round(sum(ms) / len(ms) / max(ms), 4), "max_ms": max(ms),
+            "mean_ms": round(sum(ms) / len(ms), 3), "shards": rows,
+            "basis": f"each shard of rt_set_shard(32, {n}, k) alone on this GPU, {per} indices per step "
+                     f"({steps} steps after {max(1, warmup)} warmup): mean / max step time"}
+
+
 def cpu_baseline(cfg, seconds):
-    """Oracle (C++ restatement, `port`) on every host thread (hardware_concurrency, as RayTracerTestApp.h:372-397
-    spawns), built -O3 -march=native on this host; bounded sample: a horizontal band of full rows of
-    the same frame, 1 sample index, sized to ~`seconds` of CPU work."""
+    """Oracle (C++ restatement, `port`) on the host threads this process may use, as RayTracerTestApp.h:372-397
+    spawns hardware_concurrency() threads; built -O3 -march=native on this host; bounded sample: a
+    horizontal band of full rows of the same frame, sized per thread count to a share of `seconds` of wall time.
+    A thread sweep (1, 8, the effective CPU count E, 2E) shows where the host saturates; `value` and `cores` are the
+    E-thread point (E = the affinity mask capped by the cgroup CPU quota, effective_cpus)."""
     from oracle import oracle
     oracle.use_native()
-    OracleScene = oracle.OracleScene
-    threads = min(os.cpu_count() or 1, 512)  # the pool's per-box task limit is 1024
-    o = OracleScene(cfg)
+    o = oracle.OracleScene(cfg)
     W, H = cfg.film.res
-    spp = cfg.sampler.spp()
-    rows, nidx = 8, 1
-    while True:
-        y0 = H // 2 - rows // 2
-        pix = np.arange(y0 * W, (y0 + rows) * W, dtype=np.int32)
-        t0 = time.perf_counter()
-        o.render(0, nidx, nthreads=threads, pixel_ids=pix)
-        dt = time.perf_counter() - t0
-        if dt > seconds * 0.5 or (rows >= H and nidx >= spp):
-            break
-        grow = max(2.0, seconds / max(dt, 1e-3))
-        if rows < H:
-            rows = min(H, int(rows * grow))
-        else:
-            nidx = min(spp, int(nidx * grow))
-    n = len(pix) * nidx
-    ms = n / dt / 1e6
-    # single-thread figure (SURVEY §8d): the same band's first rows on one thread, ~1/8 of the budget
-    r1 = max(1, min(rows, int(rows / threads / 8)))
-    p1 = pix[: r1 * W]
-    t0 = time.perf_counter()
-    o.render(0, nidx, nthreads=1, pixel_ids=p1)
-    dt1 = time.perf_counter() - t0
+    eff, cpuinfo = effective_cpus()
+
+    def run(threads, budget):
+        rows = max(1, min(H, threads))
+        while True:
+            y0 = H // 2 - rows // 2
+            pix = np.arange(y0 * W, (y0 + rows) * W, dtype=np.int32)
+            t0 = time.perf_counter()
+            o.render(0, 1, nthreads=threads, pixel_ids=pix)
+            dt = time.perf_counter() - t0
+            if dt > budget * 0.5 or rows >= H:
+                return len(pix) / dt / 1e6, len(pix), dt
+            rows = min(H, int(rows * max(2.0, budget / max(dt, 1e-3))))
+
+    points = sorted({1, min(8, eff), eff, min(2 * eff, 512)})
+    share = {t: (0.5 if t == eff else 0.15) for t in points}
+    sweep, main = [], None
+    for t in points:
+        v, n, dt = run(t, seconds * share[t])
+        sweep.append({"threads": t, "msamples_s": round(v, 4), "samples": n, "seconds": round(dt, 2)})
+        if t == eff:
+            main = (v, n, dt)
+    v1 = sweep[0]["msamples_s"]
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -199,17 +269,15 @@ def cpu_baseline(cfg, seconds):
                 break
     except OSError:
         pass
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
-    return {"value": round(ms, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "nproc": os.cpu_count(), "affinity_cpus": affinity,
-            "single_thread": round(len(p1) * nidx / dt1 / 1e6, 4), "cpu_model": model,
+    v, n, dt = main
+    return {"value": round(v, 4), "unit": "Msamples/s", "cores": eff, "kind": "port",
+            "effective_cpus": eff, **cpuinfo, "thread_sweep": sweep,
+            "speedup_at_cores": round(v / v1, 2) if v1 else None,
+            "single_thread": v1, "cpu_model": model,
             "build": "g++ -O3 -march=native -ffp-contract=off (built on this host)",
-            "sample": f"oracle C++ restatement (same octree BFS, watertight test, path integrator), {n} samples = "
-                      f"{rows} full rows of the {W}x{H} frame x sample indices 0..{nidx - 1}, "
-                      f"{threads} threads (os.cpu_count), {dt:.1f} s"}
+            "sample": f"oracle C++ restatement (same octree BFS, watertight test, path integrator): {n} samples = "
+                      f"{n // W} full rows of the {W}x{H} frame x sample index 0 on {eff} threads "
+                      f"(affinity capped by the cgroup quota), {dt:.1f} s"}
 
 
 def main():
@@ -269,11 +337,11 @@ def main():
             cstat["status"] = "stale (another build): traffic / valu omitted"
     else:
         cstat = {"status": "none: traffic / valu omitted", "loaded_lib_sha16": loaded}
-    roofline = {}
+    roofline, st1 = {}, None
     if rank == 0:
         st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
         rl = kernel_rooflines(st1, counters, "k_path_nee" if a.config in ("cfg4", "cfg5") else "k_path_shadow",
-                              sorted_bounces=a.config != "cornell" and os.environ.get("RTMI_SORT", "1") != "0",
+                              sorted_bounces=st1["ms_sort"] > 0,
                               n_lights=len(cfg.model.lights))
         dom = max(rl, key=lambda k: rl[k]["total_ms"])
         roofline = dict(rl[dom])
@@ -301,11 +369,20 @@ def main():
                    "res": [W, H], "spp_total": spp, "spp_per_step_per_gpu": a.spp_per_step, "max_depth": 5,
                    "parallelism": f"pixel-tile shards x{world} (32x32 tiles) + RCCL film reduce"},
         "roofline": roofline,
-        "stage_ms": {k: round(st[k], 2) for k in ("ms_generate", "ms_sort", "ms_trace", "ms_shade", "ms_shadow", "ms_film")},
+        # per-stage GPU time per step from the single-lane pass (HIP events around each stage on the one stream: they
+        # sum to at most that pass's ms_per_step); the two-lane timed region overlaps the lanes' stages, so its
+        # event spans include the other lane's kernels and are not per-stage times
+        "stage_ms": ({k: round(st1[k] / a.steps, 3) for k in ("ms_generate", "ms_sort", "ms_trace", "ms_shade",
+                                                               "ms_shadow", "ms_film")} | {
+            "basis": "single-lane pass, ms per step (sum <= roofline.ms_per_step_single_lane)"} if rank == 0 else None),
         "counters": {k: st[k] for k in ("samples", "rays", "shadow_rays", "nodes_tested", "tris_tested",
                                         "shadow_nodes_tested", "shadow_tris_tested", "hits", "fallback_rays",
                                         "shadow_fallback_rays")},
     }
+    if world == 1 and a.project_shards > 1:
+        pj = project_shards(r, cfg, a.project_shards, a.spp_per_step, a.steps, a.warmup, stream)
+        out[f"projected_tile_efficiency_{a.project_shards}"] = pj["efficiency"]
+        out["shard_projection"] = pj
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds)
         out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)

@@ -25,8 +25,9 @@ RT_SENSOR_XYZ, RT_SENSOR_CANON_EOS_100D, RT_SENSOR_COUNT = 0, 1, 18
 RT_OCTREE_BUILD_DEVICE, RT_OCTREE_BUILD_HOST = 0, 1
 RT_ILLUM_D65, RT_ILLUM_A, RT_ILLUM_D50, RT_ILLUM_F1, RT_ILLUM_ACES_D60, RT_ILLUM_COUNT = 0, 1, 2, 3, 15, 16
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 RT_MAX_DEVICES = 16
+QUEUE_SHARDS = 8  # RT_QUEUE_SHARDS
 
 F16 = C.c_float * 16
 F9 = C.c_float * 9
@@ -102,7 +103,7 @@ class rt_stats(C.Structure):
                 ("ms_generate", C.c_double), ("ms_trace", C.c_double), ("ms_shade", C.c_double),
                 ("ms_shadow", C.c_double), ("ms_film", C.c_double), ("launches_trace", C.c_int64),
                 ("launches_shade", C.c_int64), ("fallback_rays", C.c_int64), ("shadow_fallback_rays", C.c_int64),
-                ("ms_sort", C.c_double)]
+                ("ms_sort", C.c_double), ("nee_vertices", C.c_int64)]
 
 
 class rt_sample_record(C.Structure):
@@ -126,7 +127,7 @@ EXPORTS = [
     "rt_scene_upload", "rt_camera_set", "rt_sampler_set", "rt_film_set", "rt_integrator_set", "rt_set_shard",
     "rt_render_pass", "rt_render_pass_device", "rt_film_resolve",
     "rt_get_stats", "rt_reset_stats", "rt_octree_get_info", "rt_octree_export", "rt_bvh_export", "rt_debug_bvh_build",
-    "rt_debug_trace", "rt_debug_occluded", "rt_debug_samples",
+    "rt_debug_trace", "rt_debug_occluded", "rt_debug_samples", "rt_debug_sort",
     "rt_film_resolve_srgb", "rt_load_obj", "rt_mesh_free", "rt_image_write", "rt_rgb_to_sigmoid", "rt_rgb_fit_sigmoid",
     "rt_sensor_name", "rt_film_matrices",
 ]
@@ -188,6 +189,8 @@ def load_library(path=None):
         "rt_debug_trace": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), C.c_int, P(C.c_int32), P(C.c_float)], C.c_int),
         "rt_debug_occluded": ([C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_int32)], C.c_int),
         "rt_debug_samples": ([C.c_void_p, C.c_int, P(C.c_int32), P(C.c_int32), P(rt_sample_record)], C.c_int),
+        "rt_debug_sort": ([C.c_void_p, C.c_int, C.c_int, P(C.c_int32), P(C.c_uint32), P(C.c_int32), C.c_int, C.c_int,
+                           P(C.c_int32), P(C.c_int32)], C.c_int),
         "rt_film_resolve_srgb": ([C.c_void_p, P(rt_pixel), P(C.c_uint8)], C.c_int),
         "rt_load_obj": ([C.c_char_p, P(P(rt_mesh))], C.c_int),
         "rt_mesh_free": ([P(rt_mesh)], None),
@@ -197,11 +200,16 @@ def load_library(path=None):
         "rt_sensor_name": ([C.c_int], C.c_char_p),
         "rt_film_matrices": ([C.c_void_p, P(C.c_float), P(C.c_float)], C.c_int),
     }
+    # RTMI_AB_COMPAT=1 (A/B tooling only: scripts/gpu_ab_sets.sh timing an earlier build through RTMI_LIB) accepts an
+    # older ABI and skips entry points it lacks; the rt_stats fields it predates read as 0
+    compat = os.environ.get("RTMI_AB_COMPAT") == "1"
     for name, (args, res) in sig.items():
+        if compat and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
-    if lib.rt_abi_version() != ABI_VERSION:
+    if lib.rt_abi_version() != ABI_VERSION and not compat:
         raise RuntimeError("librtmi355x ABI version mismatch")
     if path is None:
         _lib = lib

@@ -21,7 +21,10 @@
 // The top kBvhTopLevels levels are laid out breadth-first at the front (nodes [0, kBvhTopNodes), staged in LDS by
 // the kernels), every deeper subtree depth-first after them: a node's internal children are one contiguous block,
 // its leaf children's tiles one contiguous run, in the same depth-first order as the nodes (treelet-contiguous).
-// Tiles: 3 float4 per triangle in the octree tiles' format (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0).
+// Tiles (compact, round 4): 9 floats (36 B) per triangle, p0.xyz p1.xyz p2.xyz, packed back to back in leaf order, and
+// the triangle id of each tile in a parallel int array (read once per ray, for the winning tile only).  The octree
+// tiles' 48-B format (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0) remains the exported, logical view
+// (bvh_tiles_logical): CFG3's closest-hit tiles shrink from 4.7 MB to 3.5 MB + 0.4 MB of ids.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -211,7 +214,7 @@ struct Collapse {
         }
         unsigned qlo[3][8] = {}, qhi[3][8] = {};
         unsigned imask = 0, valid = 0, counts = 0;
-        const int tile_base = (int)(out.tiles.size() / 3);
+        const int tile_base = (int)out.tid.size();
         int ci = 0;
         for (size_t k = 0; k < ch.size(); ++k) {
             const Node2& c = B.nodes[ch[k]];
@@ -231,11 +234,8 @@ struct Collapse {
                 for (int i = c.first; i < c.first + c.count; ++i) {
                     const int p = B.perm[i];
                     const float* v = tri9 + 9 * (size_t)p;
-                    float fid;
-                    std::memcpy(&fid, &ids[p], 4);
-                    out.tiles.push_back(make_float4(v[0], v[1], v[2], v[3]));
-                    out.tiles.push_back(make_float4(v[4], v[5], v[6], v[7]));
-                    out.tiles.push_back(make_float4(v[8], fid, 0.f, 0.f));
+                    out.tiles.insert(out.tiles.end(), v, v + 9);
+                    out.tid.push_back(ids[p]);
                 }
                 out.max_leaf = std::max(out.max_leaf, c.count);
             }
@@ -302,6 +302,7 @@ struct Collapse {
 void build_bvh8(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out, int max_leaf) {
     out.nodes.clear();
     out.tiles.clear();
+    out.tid.clear();
     out.max_leaf = 0;
     out.depth = 0;
     if (n == 0) {  // an empty root: no valid child
@@ -325,9 +326,19 @@ void build_bvh8(const float* tri9, const int* ids, int n, float pad, float node_
     B.build(0, n);
     Collapse C{B, tri9, ids, (double)pad, out};
     out.nodes.reserve((size_t)kBvhNodeF4 * (n / 4 + 1));
-    out.tiles.reserve(3 * (size_t)n);
+    out.tiles.reserve(9 * (size_t)n);
+    out.tid.reserve((size_t)n);
     C.emit_root(0);
     out.depth = C.depth_max;
+}
+
+void bvh_tiles_logical(const float* t9, const int* tid, int n, float* out12) {
+    for (int i = 0; i < n; ++i) {
+        float* o = out12 + 12 * (size_t)i;
+        std::memcpy(o, t9 + 9 * (size_t)i, 9 * sizeof(float));
+        std::memcpy(o + 9, &tid[i], 4);
+        o[10] = o[11] = 0.f;
+    }
 }
 
 }  // namespace rtmi

@@ -177,9 +177,6 @@ struct Pcg {  // rng.h:24-144
     RT_DEV void advance(uint64_t delta);
 };
 
-#ifndef RT_PCG_UNIFORM
-#define RT_PCG_UNIFORM 1  // (r03 A/B: Cornell +0.5 %, k_generate -6 %)
-#endif
 struct PcgJumpTable {
     uint64_t mult[64], plus[64];
 };
@@ -197,7 +194,7 @@ constexpr PcgJumpTable make_pcg_jump() {
 __constant__ constexpr PcgJumpTable kPcgJump = make_pcg_jump();
 
 RT_DEV void Pcg::advance(uint64_t delta) {
-#if RT_PCG_UNIFORM
+    // (r03 A/B: Cornell +0.5 %, k_generate -6 %)
     // accPlus is inc times a value P(delta) of the jump table alone (the recurrence is linear in inc, mod 2^64), so
     // the loop does not depend on the lane; when the wave shares delta (k_generate: one sample index per wave) it runs
     // once per wave on the scalar unit, and each lane makes two 64-bit multiply-adds
@@ -215,7 +212,6 @@ RT_DEV void Pcg::advance(uint64_t delta) {
         state = M * state + inc * P;
         return;
     }
-#endif
     uint64_t accMult = 1u, accPlus = 0u;
     for (int i = 0; delta > 0; ++i, delta >>= 1) {
         if (delta & 1) {

@@ -492,6 +492,7 @@ struct rt_ctx {
     int* d_work = nullptr;
     // batch workspaces, one per lane (path mode runs kLanes batches concurrently on separate streams)
     Work ws[kLanes];
+    bool warned_eye = false;    // check_ready: the camera-eye-beyond-oguard warning was printed
     bool stage_events = true;   // per-stage HIP events (rt_stats ms_*); RTMI_NO_STAGE_EVENTS=1 turns them off
     int lanes = kDefaultLanes;  // batches in flight in path mode (RTMI_LANES overrides)
     // multi-level simple path scenes: NEE rays traced by k_path_shadow (RTMI_SHADOW_QUEUE=1; measured slower than
@@ -502,8 +503,11 @@ struct rt_ctx {
     float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
     int bvh_max_leaf = kBvhMaxLeaf;  // triangles per BVH leaf at most (RTMI_BVH_LEAF)
     int bvh_count[3][2] = {};  // per BVH (set 0, set 1, any-hit): nodes, tiles (rt_bvh_export)
-    float bvh_any_cost = 2.f;  // the any-hit BVH's SAH node cost and leaf size (RTMI_BVH_ANY="cost/leaf"; r03 A/B:
-    int bvh_any_leaf = 4;      // 2/4 halves the shadow rays' triangle tests against 3/8: CFG4 +5 %)
+    // the any-hit walks' BVH: 0 = the closest-hit BVH of set 0 itself (one node + tile working set for both queries,
+    // round 4); RTMI_BVH_ANY="cost/leaf" builds a separate one (round 3: 2/4, which halved the shadow rays' triangle
+    // tests while the closest-hit leaves held 8 triangles)
+    float bvh_any_cost = 0.f;
+    int bvh_any_leaf = 4;
     int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
     int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
@@ -990,6 +994,17 @@ int check_ready(rt_ctx* c) {
     if (!c) return RT_E_ARG;
     if (!c->have_scene || !c->have_cam || !c->have_smp || !c->have_film || !c->have_integ)
         return fail(c, RT_E_STATE, "scene, camera, sampler, film and integrator must be set before rendering");
+    // The multi-level BVH decides rays whose origin lies within oguard = 8 M of the scene's vertices' extent M
+    // (scene_bvh); a camera eye farther out sends every camera ray to the exact octree BFS.  Correct, but a large
+    // performance cliff that only the fallback counter shows: say so once per context.
+    if (c->dsc.oguard > 0.f && !c->warned_eye) {
+        const float* t = c->cam.camera_to_world + 12;  // column-major: the translation column
+        if (std::max(std::fabs(t[0]), std::max(std::fabs(t[1]), std::fabs(t[2]))) > c->dsc.oguard) {
+            std::fprintf(stderr, "rtmi355x: the camera eye lies beyond the BVH's origin guard (8x the scene extent): "
+                                 "every camera ray takes the exact octree BFS (slow, still exact)\n");
+            c->warned_eye = true;
+        }
+    }
     return RT_OK;
 }
 
@@ -1873,7 +1888,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     if (qcap != 1) {
         for (int st = 0; st < (c->cull ? 2 : 1); ++st)
             scene_bvh(sw, st, c->bvh_node_cost, c->bvh_max_leaf, bvh[st], wabs, oguard);
-        scene_bvh(sw, 0, c->bvh_any_cost, c->bvh_any_leaf, bvh[kBvhAny], wabs, oguard);
+        if (c->bvh_any_cost > 0) scene_bvh(sw, 0, c->bvh_any_cost, c->bvh_any_leaf, bvh[kBvhAny], wabs, oguard);
     }
     c->info.n_nodes = nn;
     c->info.n_leaf_refs = (int)c->h_refs.size();
@@ -2004,22 +2019,29 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         return rc;
     void* pbv[3] = {nullptr, nullptr, nullptr};
     void* pbt[3] = {nullptr, nullptr, nullptr};
+    void* pbi[3] = {nullptr, nullptr, nullptr};
     const int bvh_nodes0 = (int)(bvh[0].nodes.size() / kBvhNodeF4);
     for (int st = 0; st < 3; ++st) {
-        c->bvh_count[st][0] = (int)(bvh[st].nodes.size() / kBvhNodeF4);
-        c->bvh_count[st][1] = (int)(bvh[st].tiles.size() / 3);
+        // a BVH not built here (no culled set; the any-hit walks on the closest-hit BVH of set 0) uses set 0's arrays
+        const int src = bvh[st].nodes.empty() ? 0 : st;
+        c->bvh_count[st][0] = (int)(bvh[src].nodes.size() / kBvhNodeF4);
+        c->bvh_count[st][1] = (int)bvh[src].tid.size();
         if (bvh[st].nodes.empty()) continue;
         // the kernels stage nodes [0, kBvhTopNodes) in LDS unconditionally: pad with empty nodes
         if (bvh[st].nodes.size() < kBvhNodeF4 * (size_t)kBvhTopNodes)
             bvh[st].nodes.resize(kBvhNodeF4 * (size_t)kBvhTopNodes, make_float4(0.f, 0.f, 0.f, 0.f));
+        bvh[st].tiles.resize(bvh[st].tiles.size() + 4, 0.f);  // (an empty BVH still gets a buffer)
+        bvh[st].tid.push_back(-1);
         if ((rc = up(bvh[st].nodes.data(), bvh[st].nodes.size() * 16, &pbv[st])) ||
-            (rc = up(bvh[st].tiles.data(), bvh[st].tiles.size() * 16, &pbt[st])))
+            (rc = up(bvh[st].tiles.data(), bvh[st].tiles.size() * 4, &pbt[st])) ||
+            (rc = up(bvh[st].tid.data(), bvh[st].tid.size() * 4, &pbi[st])))
             return rc;
     }
     DevScene& d = c->dsc;
     for (int st = 0; st < 3; ++st) {
         d.bvh[st] = (const float4*)(pbv[st] ? pbv[st] : pbv[0]);
-        d.btiles[st] = (const float4*)(pbt[st] ? pbt[st] : pbt[0]);
+        d.btiles[st] = (const float*)(pbt[st] ? pbt[st] : pbt[0]);
+        d.btid[st] = (const int*)(pbi[st] ? pbi[st] : pbi[0]);
     }
     d.wabs = wabs;
     d.oguard = oguard;
@@ -2221,6 +2243,7 @@ static int get_stats_one(rt_ctx* c, rt_stats* out) {
     s.samples = (int64_t)h[C_SAMPLES];
     s.fallback_rays = (int64_t)h[C_FALLBACK];
     s.shadow_fallback_rays = (int64_t)h[C_SFALLBACK];
+    s.nee_vertices = (int64_t)h[C_NEEVTX];
 #if RT_SIMD_STATS
     unsigned long long sm[8];
     simd_stats_read(sm);
@@ -2271,8 +2294,14 @@ static int impl_rt_bvh_export(rt_ctx* c, int set, int* n_nodes, int* n_tiles, fl
     hipSetDevice(c->device);
     if (nodes && c->bvh_count[set][0])
         HIPCHK(c, hipMemcpy(nodes, c->dsc.bvh[set], (size_t)c->bvh_count[set][0] * kBvhNodeF4 * 16, hipMemcpyDeviceToHost));
-    if (tiles && c->bvh_count[set][1])
-        HIPCHK(c, hipMemcpy(tiles, c->dsc.btiles[set], (size_t)c->bvh_count[set][1] * 48, hipMemcpyDeviceToHost));
+    if (tiles && c->bvh_count[set][1]) {  // the device's compact tiles + ids, exported in the 12-float view
+        const int nt = c->bvh_count[set][1];
+        std::vector<float> t9(9 * (size_t)nt);
+        std::vector<int> tid(nt);
+        HIPCHK(c, hipMemcpy(t9.data(), c->dsc.btiles[set], t9.size() * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(tid.data(), c->dsc.btid[set], tid.size() * 4, hipMemcpyDeviceToHost));
+        bvh_tiles_logical(t9.data(), tid.data(), nt, tiles);
+    }
     return RT_OK;
 }
 
@@ -2289,13 +2318,11 @@ static int impl_rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes
     int leaf = kBvhMaxLeaf;
     if (const char* e = std::getenv("RTMI_BVH_CI")) cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_BVH_LEAF")) leaf = std::max(1, std::min(15, std::atoi(e)));
-    if (set == kBvhAny) {  // rt_create's defaults / RTMI_BVH_ANY for the any-hit BVH
-        cost = 2.f;
-        leaf = 4;
+    if (set == kBvhAny) {  // rt_create's default (set 0's closest-hit BVH) / RTMI_BVH_ANY for the any-hit BVH
         if (const char* e = std::getenv("RTMI_BVH_ANY")) {
-            float ac = 2.f;
+            float ac = 0.f;
             int al = 4;
-            if (std::sscanf(e, "%f/%d", &ac, &al) == 2) { cost = ac; leaf = std::max(1, std::min(15, al)); }
+            if (std::sscanf(e, "%f/%d", &ac, &al) == 2 && ac > 0) { cost = ac; leaf = std::max(1, std::min(15, al)); }
         }
     }
     SceneWorld sw;
@@ -2304,10 +2331,10 @@ static int impl_rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes
     float wabs = 0.f, oguard = 0.f;
     scene_bvh(sw, set == 1 && s->cull_backfaces ? 1 : 0, cost, leaf, b, wabs, oguard);
     if (n_nodes) *n_nodes = (int)(b.nodes.size() / kBvhNodeF4);
-    if (n_tiles) *n_tiles = (int)(b.tiles.size() / 3);
+    if (n_tiles) *n_tiles = (int)b.tid.size();
     if (consts) { consts[0] = wabs; consts[1] = oguard; }
     if (nodes) std::memcpy(nodes, b.nodes.data(), b.nodes.size() * 16);
-    if (tiles) std::memcpy(tiles, b.tiles.data(), b.tiles.size() * 16);
+    if (tiles) bvh_tiles_logical(b.tiles.data(), b.tid.data(), (int)b.tid.size(), tiles);
     return RT_OK;
 }
 
@@ -2366,6 +2393,63 @@ static int impl_rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float
          hipMemcpy(occluded, dP, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
         rc = fail(c, RT_E_HIP, std::string("debug occlusion: ") + hipGetErrorString(hipGetLastError()));
     hipFree(dO); hipFree(dD); hipFree(dP);
+    return rc;
+}
+
+// The coherence sorts alone (rt_sort.hip) on a synthetic sharded queue: kShards shards of stride S, shard j holding
+// shard_len[j] items at positions [j S, j S + shard_len[j]) with keys[pos] (and, for the NEE sort, slots[pos]).
+// which 0: the ray sort (key bits 3 + 2 bits_a + 3 bits_b; out[pos'] = the queue position of sorted item pos'),
+// 1: the NEE sort (key bits 3 bits_a; out = the slots sorted in place).  Sorted item k' sits at position
+// (k' / S2) S + k' % S2 with S2 = shard_stride(n, kShards); out_len[j] receives the rewritten shard lengths.
+static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_len, const uint32_t* keys,
+                              const int32_t* slots, int bits_a, int bits_b, int32_t* out, int32_t* out_len) {
+    if (!c || (which != 0 && which != 1) || S < 64 || S % 64 || !shard_len || !keys || !out || !out_len ||
+        (which == 1 && !slots))
+        return c ? fail(c, RT_E_ARG, "debug sort: bad arguments") : RT_E_ARG;
+    for (int j = 0; j < kShards; ++j)
+        if (shard_len[j] < 0 || shard_len[j] > S) return fail(c, RT_E_ARG, "debug sort: shard length out of range");
+    const int kb = which == 0 ? 3 + 2 * bits_a + 3 * bits_b : 3 * bits_a;
+    if (bits_a < 0 || bits_a > (which == 0 ? 4 : 9) || bits_b < 0 || bits_b > 9 || kb < 1 || kb > 30)
+        return fail(c, RT_E_ARG, "debug sort: key bits out of range");
+    hipSetDevice(c->device);
+    int rc = order_after_previous(c, c->stream);
+    if (rc) return rc;
+    const size_t cap = (size_t)kShards * S;
+    unsigned *dkey = nullptr, *k0 = nullptr, *k1 = nullptr;
+    int *dslot = nullptr, *dlen = nullptr, *dout = nullptr, *v0 = nullptr, *v1 = nullptr;
+    void* temp = nullptr;
+    if (dalloc(&dkey, cap) || dalloc(&dslot, cap) || dalloc(&dlen, (size_t)kShards * kQStride) || dalloc(&dout, cap) ||
+        dalloc(&k0, cap) || dalloc(&k1, cap) || dalloc(&v0, cap) || dalloc(&v1, cap) ||
+        hipMalloc(&temp, sort_temp_bytes()) != hipSuccess)
+        rc = fail(c, RT_E_OOM, "debug sort buffers");
+    if (!rc) {
+        std::vector<int> hlen((size_t)kShards * kQStride, 0);
+        for (int j = 0; j < kShards; ++j) hlen[(size_t)j * kQStride] = shard_len[j];
+        std::vector<int> hs(cap, -1);
+        if (which == 1) std::memcpy(hs.data(), slots, cap * 4);
+        hipError_t e = hipMemcpy(dkey, keys, cap * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dslot, hs.data(), cap * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dlen, hlen.data(), hlen.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(dout, 0xff, cap * 4);
+        if (e == hipSuccess) {
+            if (which == 0) {
+                SortRaysIO so{dkey, dout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S};
+                e = launch_sort_rays(c->stream, so);
+            } else {
+                SortNeeIO so{dslot, dlen, S, dkey, k0, k1, v0, v1, temp, bits_a};
+                e = launch_sort_nee(c->stream, so);
+            }
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = hipMemcpy(out, which == 0 ? dout : dslot, cap * 4, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(hlen.data(), dlen, hlen.size() * 4, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(c, RT_E_HIP, std::string("debug sort: ") + hipGetErrorString(e));
+        else
+            for (int j = 0; j < kShards; ++j) out_len[j] = hlen[(size_t)j * kQStride];
+    }
+    hipFree(dkey); hipFree(dslot); hipFree(dlen); hipFree(dout);
+    hipFree(k0); hipFree(k1); hipFree(v0); hipFree(v1); hipFree(temp);
+    if (!rc) rc = mark_done(c, c->stream);
     return rc;
 }
 
@@ -2525,6 +2609,7 @@ static int impl_rt_get_stats(rt_ctx* c, rt_stats* out) {
         sum.ms_shadow += s.ms_shadow; sum.ms_film += s.ms_film; sum.ms_sort += s.ms_sort;
         sum.launches_trace += s.launches_trace; sum.launches_shade += s.launches_shade;
         sum.fallback_rays += s.fallback_rays; sum.shadow_fallback_rays += s.shadow_fallback_rays;
+        sum.nee_vertices += s.nee_vertices;
         return RT_OK;
     });
     if (!rc) *out = sum;
@@ -2581,6 +2666,11 @@ int rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float* rd, const 
 }
 int rt_debug_samples(rt_ctx* c, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out) {
     return guarded([&] { return impl_rt_debug_samples(c, n, pixel_ids, indices, out); }, [&](const std::string& m) { set_error(c, m); });
+}
+int rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_len, const uint32_t* keys, const int32_t* slots,
+                  int bits_a, int bits_b, int32_t* out, int32_t* out_len) {
+    return guarded([&] { return impl_rt_debug_sort(c, which, S, shard_len, keys, slots, bits_a, bits_b, out, out_len); },
+                   [&](const std::string& m) { set_error(c, m); });
 }
 int rt_create(const rt_options* opt, rt_ctx** out) {
     return guarded([&] { return impl_rt_create(opt, out); }, [&](const std::string& m) { set_error(nullptr, m); });

@@ -136,10 +136,11 @@ struct DevScene {
     int ring_mask;
     int ring_threads;               // launches with qcap == 0 are clamped to this many threads
     // multi-level octrees (qcap != 1): the fast traversal's 8-wide compressed BVH per tile set (rt_bvh.cpp:
-    // kBvhNodeF4 float4 per node) and its leaf-ordered triangle tiles; rays it finds ambiguous fall back to the
-    // octree BFS
-    const float4* bvh[3];           // [0], [1]: closest-hit BVH of tile set 0 / 1; [kBvhAny]: the any-hit BVH (set 0,
-    const float4* btiles[3];        // smaller leaves: shadow rays test fewer triangles)
+    // kBvhNodeF4 float4 per node) and its leaf-ordered triangle tiles (9 floats each, packed) with their triangle
+    // ids; rays it finds ambiguous fall back to the octree BFS
+    const float4* bvh[3];           // [0], [1]: closest-hit BVH of tile set 0 / 1; [kBvhAny]: the any-hit walks' BVH
+    const float* btiles[3];         // (by default the same arrays as [0]: one working set for both queries;
+    const int* btid[3];             // RTMI_BVH_ANY="cost/leaf" builds a separate one, set 0)
     float wabs;                     // canonical-rule window W(t) = t 2^-16 + wabs
     float oguard;                   // rays whose origin has a coordinate beyond +-oguard are ambiguous (the box
                                     // padding covers the slab test's rounding only for origins inside 8 M)
@@ -154,7 +155,7 @@ struct DevScene {
 void simd_stats_read(unsigned long long* out);  // rt_kernels.hip (measurement builds)
 #endif
 enum { C_NODES = 0, C_TRIS, C_HITS, C_RAYS, C_SHADOW, C_SAMPLES, C_SNODES, C_STRIS, C_FALLBACK, C_SFALLBACK,
-       C_NCOUNTERS = 16 };
+       C_NEEVTX, C_NCOUNTERS = 16 };
 constexpr int kCtrSubs = 32;   // words per counter slot
 constexpr int kCtrLine = 32;   // u64 between words: 256 B
 constexpr size_t kCtrWords = (size_t)C_NCOUNTERS * kCtrSubs * kCtrLine;
@@ -173,11 +174,15 @@ static const int kBvhMaxLeaf = 4;  // triangles per closest-hit leaf (SAH may st
                                    // walk: 4 vs 8 CFG3 +1 %, CFG4 +1.1 %; 5, 6 between)
 static const int kBvhAny = 2;                         // DevScene bvh / btiles index of the any-hit BVH
 struct BvhData {
-    std::vector<float4> nodes, tiles;
+    std::vector<float4> nodes;
+    std::vector<float> tiles;  // 9 floats per tile (p0, p1, p2), leaf order
+    std::vector<int> tid;      // triangle id per tile
     int depth = 0, max_leaf = 0;
 };
 void build_bvh8(const float* tri9, const int* ids, int n, float pad, float node_cost, BvhData& out,
                 int max_leaf = kBvhMaxLeaf);
+// compact tiles (9 floats + id) -> the exported 12-float view (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0)
+void bvh_tiles_logical(const float* t9, const int* tid, int n, float* out12);
 
 }  // namespace rtmi
 
@@ -272,7 +277,7 @@ struct TraceIO {
 
 // Material binning of a mixed multi-level scene's bounce (k_bin_materials, after the trace): every hit's queue
 // position is appended to the index list of its material class (idx[c], sharded like the queue, shard lengths at
-// len + c kShards kQStride); misses end their paths there.
+// len + c kShards kQStride); misses are appended to no bin (no miss work in the full path integrator).
 struct BinIO {
     QueueView q;             // the traced queue
     const int* hitPrim;
@@ -326,14 +331,18 @@ struct ShadowQueueIO {
 };
 
 // Deferred NEE of the mixed-scene shade: k_path_shade_full samples every light at a Lambert vertex (same sampler
-// dimensions and order as inline) and leaves one NEE record per slot — {po.xyz, -}, per light {wi.xyz, tMax}
-// (tMax < 0: the light is skipped), the light weights 4 per float4, then x[8] = β (R / π) — and appends the slot to
-// the NEE queue (sharded like the ray queues, counters at kQShadowLen / kQShadowTicket); k_path_nee traces a
-// vertex's shadow rays in light order and adds the visible lights' terms to L in that order, so L is bit-identical
-// to the inline loop.  The traversals no longer share a kernel with the path state (CFG4: 198 VGPRs unbudgeted,
-// 464-656 B/lane spill under the 4-wave budget).
-inline __host__ __device__ int nee_stride(int n_lights) { return 3 + n_lights + (n_lights + 3) / 4; }  // float4s
-enum { N_PO = 0, N_RAY = 1 };  // N_WGT = 1 + n, N_X = 1 + n + ceil(n / 4)
+// dimensions and order as inline) and leaves one NEE record per slot — {po.xyz, bits(material | bounced << 31)}, the
+// lights' sample points (u0, u1) two per float4, then the light weights four per float4 (< 0: the light is skipped,
+// cos <= 0) — and appends the slot to the NEE queue (sharded like the ray queues, counters at kQShadowLen /
+// kQShadowTicket).  k_path_nee re-derives each light's shadow ray (wi, tMax) from (po, u0, u1) with the same code,
+// traces a vertex's shadow rays in light order and adds the visible lights' terms to L in that order, so L is
+// bit-identical to the inline loop.  It also owns the vertex's throughput update: the shade kernel leaves β as it
+// was, k_path_nee forms x = β (R / π) for the light terms (R = the material's reflectance at λ) and, when the cosine
+// bounce continued the path (`bounced`), stores β R.  A 4-light record is 64 B (round 3: 128 B of rays and x[8]).
+// The traversals do not share a kernel with the path state (CFG4: 198 VGPRs unbudgeted, 464-656 B/lane spill under
+// the 4-wave budget).
+inline __host__ __device__ int nee_stride(int n_lights) { return 1 + (n_lights + 1) / 2 + (n_lights + 3) / 4; }  // float4s
+enum { N_PO = 0, N_UV = 1 };  // the weights at N_UV + ceil(n / 2)
 struct NeeIO {
     float4* rec;   // NEE records, nee_stride(n_lights) float4s per slot; nullptr: inline NEE (not used)
     int* slot;     // NEE queue: slot per position (same shard stride as the ray queues)

@@ -114,26 +114,17 @@ __device__ __forceinline__ bool stage_tris1(const DevScene& sc) {
 // Mixed-scene material table in LDS (<= kLdsMats entries, 32 B each): the shade and binning kernels look up the
 // material of every hit (prim -> triMaterial -> material), so staging the table removes the chain's last global
 // round trip.  Larger tables stay in global memory (mat_at reads through the pointer).
-#ifndef RT_MAT_LDS
-#define RT_MAT_LDS 1
-#endif
 static constexpr int kLdsMats = 64;
 __shared__ DevMaterial g_mat[kLdsMats];
 __device__ __forceinline__ bool stage_materials(const DevScene& sc) {
-#if RT_MAT_LDS
     const bool ok = sc.n_materials <= kLdsMats;
     if (ok)
         for (int i = threadIdx.x; i < sc.n_materials; i += blockDim.x) g_mat[i] = sc.materials[i];
     __syncthreads();
     return ok;
-#else
-    return false;
-#endif
 }
 __device__ __forceinline__ DevMaterial mat_at(const DevScene& sc, bool lds, int m) {
-#if RT_MAT_LDS
     if (lds) return g_mat[m];
-#endif
     return sc.materials[m];
 }
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
@@ -219,9 +210,6 @@ __device__ __forceinline__ int block_append(int* counter, bool pred, int* lds) {
 
 // Block-aggregated append of a static chunk's two items (kStaticItems = 2): one atomicAdd and one round of barriers
 // for both; the block's first items take the lower positions, its second items the upper ones.  lds: 2 NW + 1 ints.
-#ifndef RT_APPEND_DB
-#define RT_APPEND_DB 0
-#endif
 __device__ __forceinline__ void block_append2(int* counter, bool p0, bool p1, int* lds, int& o0, int& o1) {
     constexpr int NW = kBlock / 64;
     const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
@@ -238,10 +226,7 @@ __device__ __forceinline__ void block_append2(int* counter, bool p0, bool p1, in
     __syncthreads();
     o0 = p0 ? lds[2 * NW] + lds[wave] + r0 : -1;
     o1 = p1 ? lds[2 * NW] + lds[NW + wave] + r1 : -1;
-#if !RT_APPEND_DB
-    __syncthreads();  // (double-buffered callers alternate lds between two arrays instead: the next call's two
-                      // barriers separate these reads from the rewrite two calls later)
-#endif
+    __syncthreads();
 }
 
 // Work distribution of the persistent queue kernels over a sharded queue (rt_internal.h QueueView).
@@ -452,26 +437,17 @@ __device__ __forceinline__ void rec_set_prev_pdf(const RecView& r, int slot, flo
 // The wavelength warps' tables (rt_logtab.h: 97 log rows of 3 doubles, 64 exp rows of 2) staged in LDS by the
 // kernels that evaluate the warps for every sample (k_generate: 8 atanh = 16 log rows; k_path_film: 8 cosh = 16
 // exp rows): the rows are indexed per lane, so from the constant arrays each is a divergent vector-memory load.
-#ifndef RT_WARP_LDS
-#define RT_WARP_LDS 1
-#endif
 __shared__ double g_logtab[rtm::kLogN][4];  // (row padded to 32 B: one ds_read_b128 + one ds_read_b64)
 __shared__ double g_exptab[64][2];
 struct WarpTabLds {
     __device__ static const double* logrow(int j) { return g_logtab[j]; }
     __device__ static const double* exprow(int j) { return g_exptab[j]; }
 };
-#if RT_WARP_LDS
 using WarpTab = WarpTabLds;
-#else
-using WarpTab = rtm::TabConst;
-#endif
 __device__ __forceinline__ void stage_warp_tables() {
-#if RT_WARP_LDS
     for (int i = threadIdx.x; i < rtm::kLogN * 3; i += blockDim.x) g_logtab[i / 3][i % 3] = rtm::kLogTab[i / 3][i % 3];
     for (int i = threadIdx.x; i < 64 * 2; i += blockDim.x) g_exptab[i / 2][i % 2] = rtm::kExp2Tab[i / 2][i % 2];
     __syncthreads();
-#endif
 }
 
 // ===================================================================================== K1 generate
@@ -582,24 +558,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
 // over 360..830 nm, so a dense_query from global memory is a gather over ~15 cache lines per wave-instruction, and
 // the sensor conversion makes 24 of them per sample; from LDS it is one ds_read_b128 per wavelength.  Same values,
 // same index (spectrum.h:386-398: lround(λ) - 360, 0 outside the table), same arithmetic order: bit-identical.
-#ifndef RT_SPEC_LDS
-#define RT_SPEC_LDS 1
-#endif
 __shared__ float4 g_spk[kSpecN];
 __device__ __forceinline__ void stage_spectra(const DevSpectra* sp) {
-#if RT_SPEC_LDS
     for (int i = threadIdx.x; i < kSpecN; i += blockDim.x) g_spk[i] = sp->SPK[i];
     __syncthreads();
-#endif
 }
 __device__ __forceinline__ float4 spk_query(const DevSpectra* sp, float lambda) {
     long off = (long)roundf(lambda) - 360;  // std::lround: half away from zero
     if (off < 0 || off >= kSpecN) return make_float4(0.f, 0.f, 0.f, 0.f);
-#if RT_SPEC_LDS
     return g_spk[off];
-#else
-    return sp->SPK[off];
-#endif
 }
 __device__ __forceinline__ float d65_query(const DevSpectra* sp, float lambda) { return spk_query(sp, lambda).w; }
 // pixelsensor.h:81-87 (to_sensor_rgb, rt_device.h) over the staged table: per channel the same sum in the same order
@@ -1102,18 +1069,13 @@ __device__ __forceinline__ void kswap(unsigned& a, unsigned& b) {
     a = lo; b = hi;
 }
 static constexpr unsigned kNoChild = 0xffffffffu;
-#ifndef RT_SPEC
-#define RT_SPEC 1
-#endif
-#ifndef RT_LEAF_STEP
-#define RT_LEAF_STEP 8
-#endif
-#ifndef RT_POP_OPEN
-#define RT_POP_OPEN 1
-#endif
-#ifndef RT_TRI_PREFETCH
-#define RT_TRI_PREFETCH 1
-#endif
+// Four consecutive floats at a 4-byte aligned address (the BVH's packed 36-B triangle tiles): one global_load_dwordx4
+typedef float rt_f4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ float4 ld_f4u(const float* p) {
+    const rt_f4u v = *reinterpret_cast<const rt_f4u*>(p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+static constexpr int kLeafStep = 8;  // triangles per leaf phase of the BVH walk (a held leaf's rest stays held)
 
 // One 8-wide node against the ray: the sorted child keys k[0] <= ... <= k[7].  Key of a child whose slab interval
 // [tn, tf] is non-empty within [0, tcut]: (bits(tn) with the low 3 bits cleared) | slot — tn >= 0, so the keys
@@ -1190,7 +1152,6 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
     int sp = 0;
     bool overflow = false;
     int lf = 0, lc = 0;
-#if RT_SPEC
     // Speculative while-while (Aila & Laine 2009): a lane that holds a leaf keeps opening nodes while other lanes
     // of its wave are still looking for theirs, so the node steps the wave executes anyway do useful work (CFG3:
     // 29 % of the lanes of a node step were busy without it).  node: an internal node to open (>= 0), none (-1), or
@@ -1203,7 +1164,6 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
             const bool more = node >= 0 || (node == -1 && sp > 0);
             if (__ballot(lc == 0 && more) == 0) break;  // every lane holds a leaf or is done
             if (!more) continue;
-#if RT_POP_OPEN
             // pop, then open a popped internal node in the same step (the lanes popping and the lanes holding a
             // node open theirs together instead of in alternating steps)
             if (node == -1) {
@@ -1221,18 +1181,6 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
                 }
             }
             if (node >= 0) {
-#else
-            if (node == -1) {
-                if constexpr (ANY) {
-                    --sp;
-                    node = (int)stw[sp * kBlock];
-                } else {
-                    const uint2 e = stk[--sp * kBlock];
-                    if (__uint_as_float(e.y & 0x7ffffff8u) > cut) continue;  // entered beyond the current cut
-                    node = (int)e.x;
-                }
-            } else {
-#endif
                 RT_SIMD_TICK(ANY ? 4 : 0);
                 const BvhNode8 bn = load_node8(nodes, node);
                 nn += __popc(bn.N1.w);
@@ -1254,8 +1202,8 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
             }
         }
         if (lc == 0) break;  // nothing held, nothing left: this lane's walk is over
-        // at most RT_LEAF_STEP triangles per leaf phase (the rest stays held)
-        const int m = lc < RT_LEAF_STEP ? lc : RT_LEAF_STEP;
+        // at most kLeafStep triangles per leaf phase (the rest stays held)
+        const int m = lc < kLeafStep ? lc : kLeafStep;
         const bool done = leaf(lf, m);
         lf += m;
         lc -= m;
@@ -1265,51 +1213,6 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
             node = -1;
         }
     }
-#else
-    int node = 0;
-    while (true) {
-        // node phase ("while-while"): open internal nodes nearest-first until this lane holds a leaf
-        while (lc == 0) {
-            if (node < 0) {
-                if (sp == 0) break;
-                int w;
-                if constexpr (ANY) {
-                    --sp;
-                    w = (int)stw[sp * kBlock];
-                } else {
-                    const uint2 e = stk[--sp * kBlock];
-                    if (__uint_as_float(e.y & 0x7ffffff8u) > cut) continue;  // entered beyond the current cut
-                    w = (int)e.x;
-                }
-                if (w >= 0) node = w;
-                else decode_leaf(w, lf, lc);
-                continue;
-            }
-            RT_SIMD_TICK(ANY ? 4 : 0);
-            const BvhNode8 bn = load_node8(nodes, node);
-            nn += __popc(bn.N1.w);
-            unsigned k[8];
-            node_keys(bn, r, cut, k, sort);
-            node = -1;
-#pragma unroll
-            for (int i = 7; i >= 1; --i)
-                if (k[i] != kNoChild) {
-                    if (sp >= CAP) overflow = true;
-                    else if constexpr (ANY) stw[sp++ * kBlock] = (unsigned)child_word(bn, k[i]);
-                    else stk[sp++ * kBlock] = make_uint2((unsigned)child_word(bn, k[i]), k[i]);
-                }
-            if (k[0] != kNoChild) {
-                const int w = child_word(bn, k[0]);
-                if (w >= 0) node = w;
-                else decode_leaf(w, lf, lc);
-            }
-        }
-        if (lc == 0) break;
-        const bool done = leaf(lf, lc);
-        lc = 0;
-        if (done) break;
-    }
-#endif
     return !overflow;
 }
 
@@ -1321,50 +1224,44 @@ __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3
         amb = true;
         return -1;
     }
-    const float4* __restrict__ tiles = sc.btiles[set];
+    const float* __restrict__ tiles = sc.btiles[set];
     Bvh8Ray r;
     r.inv = bvh_inv(d);
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
     const TriRay R = make_triray<KZ>(o, d);
     float cut = tMaxInit, t2 = __builtin_inff();
-    int best = -1, second = -1;
+    int best = -1, second = -1;  // tile indices (the winner's triangle id is read once, after the walk)
     const bool ok = bvh8_walk<false>(sc.bvh[set], r, cut, nn, true, [&](int lf, int lc) {
-#if RT_TRI_PREFETCH
         // the next triangle's tile is loaded while this one is tested (a leaf's tiles are contiguous)
-        const float4* tp = tiles + 3 * lf;
-        float4 A = tp[0], B = tp[1], Cc = tp[2];
+        const float* tp = tiles + 9 * lf;
+        float4 A = ld_f4u(tp), B = ld_f4u(tp + 4);
+        float C = tp[8];
         for (int k = 0; k < lc; ++k) {
-            float4 nA = A, nB = B, nC = Cc;
-            if (k + 1 < lc) { nA = tp[3 * k + 3]; nB = tp[3 * k + 4]; nC = tp[3 * k + 5]; }
-#else
-        for (int k = 0; k < lc; ++k) {
-            const float4* tp = tiles + 3 * (lf + k);
-            const float4 A = tp[0], B = tp[1], Cc = tp[2];
-#endif
+            float4 nA = A, nB = B;
+            float nC = C;
+            if (k + 1 < lc) { nA = ld_f4u(tp + 9 * k + 9); nB = ld_f4u(tp + 9 * k + 13); nC = tp[9 * k + 17]; }
             ++nt;
             RT_SIMD_TICK(2);
             float b0, b1, b2, t;
-            if (tri_intersect<KZ>(R, cut, A, B, Cc, b0, b1, b2, t) && t < cut) {
+            if (tri_intersect<KZ>(R, cut, A, B, make_float4(C, 0.f, 0.f, 0.f), b0, b1, b2, t) && t < cut) {
                 if (best < 0 || t < rt) {
                     t2 = best < 0 ? t2 : rt;
                     second = best;
-                    best = __float_as_int(Cc.y);
+                    best = lf + k;
                     rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
                     const float c2 = t + 2.f * canon_window(t, sc.wabs);
                     cut = c2 < cut ? c2 : cut;
                 } else if (t < t2) {
-                    second = __float_as_int(Cc.y);
+                    second = lf + k;
                     t2 = t;
                 }
             }
-#if RT_TRI_PREFETCH
-            A = nA; B = nB; Cc = nC;
-#endif
+            A = nA; B = nB; C = nC;
         }
         return false;
     });
     amb = !ok || (second >= 0 && t2 <= rt + canon_window(rt, sc.wabs));
-    return best;
+    return best >= 0 ? sc.btid[set][best] : -1;
 }
 
 // any hit over the BVH with a fixed tMax: 0 = occluded, -1 = not; amb = only window hits were found
@@ -1375,7 +1272,7 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
         amb = true;
         return -1;
     }
-    const float4* __restrict__ tiles = sc.btiles[kBvhAny];  // (shadow rays: every triangle, set 0)
+    const float* __restrict__ tiles = sc.btiles[kBvhAny];  // (shadow rays: every triangle, set 0)
     Bvh8Ray r;
     r.inv = bvh_inv(d);
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
@@ -1384,33 +1281,22 @@ __device__ __forceinline__ int bvh_anyhit(const DevScene& sc, int set, V3 o, V3 
     bool window = false, occluded = false;
     float cut = tMax;
     const bool ok = bvh8_walk<true>(sc.bvh[kBvhAny], r, cut, nn, true, [&](int lf, int lc) {
-#if RT_TRI_PREFETCH
-        const float4* tp = tiles + 3 * lf;
-        float4 A = tp[0], B = tp[1], Cc = tp[2];
+        const float* tp = tiles + 9 * lf;
+        float4 A = ld_f4u(tp), B = ld_f4u(tp + 4);
+        float C = tp[8];
         for (int k = 0; k < lc; ++k) {
-            float4 nA = A, nB = B, nC = Cc;
-            if (k + 1 < lc) { nA = tp[3 * k + 3]; nB = tp[3 * k + 4]; nC = tp[3 * k + 5]; }
+            float4 nA = A, nB = B;
+            float nC = C;
+            if (k + 1 < lc) { nA = ld_f4u(tp + 9 * k + 9); nB = ld_f4u(tp + 9 * k + 13); nC = tp[9 * k + 17]; }
             ++nt;
             RT_SIMD_TICK(6);
             float b0, b1, b2, t;
-            if (tri_intersect<KZ>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+            if (tri_intersect<KZ>(R, tMax, A, B, make_float4(C, 0.f, 0.f, 0.f), b0, b1, b2, t) && t < tMax) {
                 if (t < sure) { occluded = true; return true; }
                 window = true;
             }
-            A = nA; B = nB; Cc = nC;
+            A = nA; B = nB; C = nC;
         }
-#else
-        for (int k = 0; k < lc; ++k) {
-            const float4* tp = tiles + 3 * (lf + k);
-            ++nt;
-            RT_SIMD_TICK(6);
-            float b0, b1, b2, t;
-            if (tri_intersect<KZ>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax) {
-                if (t < sure) { occluded = true; return true; }
-                window = true;
-            }
-        }
-#endif
         return false;
     });
     if (occluded) { amb = false; return 0; }
@@ -1464,16 +1350,13 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 // Register budgets (amdgpu_waves_per_eu) of the multi-level instantiations: 4 waves/SIMD (128 VGPRs) on the trace,
 // path shade and mixed-scene shade kernels (CFG3 121 -> 144, CFG4 87 -> 111 Msamples/s; 5 waves spill too much).
 // The single-leaf instantiations (107 / 123 VGPRs) are unbudgeted (5 waves: trace -2 %, shade -7 %).
+// These budgets (RT_*_WAVES), the any-hit stack depth (RT_ANY_STACK), the radix digit widths (rt_sort.hip) and the
+// staged BVH levels (rt_internal.h) are numeric tuning constants a variant build may override (Makefile
+// `variants`); RT_SIMD_STATS selects the SIMD-efficiency measurement build.  No code path is switched by a macro.
 #ifndef RT_MULTI_WAVES
-#define RT_MULTI_WAVES 4  // the one tuning macro left: variant builds for A/B (Makefile `variants`)
+#define RT_MULTI_WAVES 4
 #endif
 #define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_MULTI_WAVES)))
-#ifndef RT_SHADE_PREFETCH
-#define RT_SHADE_PREFETCH 0  // single-leaf shade: the chunk's second item's slot and hit loaded with the first's
-#endif
-#ifndef RT_PAIR_APPEND
-#define RT_PAIR_APPEND 1  // single-leaf shade: one append per static chunk (two items) instead of per item (Cornell +3.5 %, r03)
-#endif
 #ifndef RT_SHADE1_WAVES
 #define RT_SHADE1_WAVES 4  // the single-leaf simple-path shade (Cornell)
 #endif
@@ -1564,7 +1447,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
 }
 
 // Material bins of a mixed multi-level scene's bounce (BinIO): every hit's queue position is appended to the index
-// list of its material class, shard by shard, in queue order within a chunk; misses end their paths here.  A pass
+// list of its material class, shard by shard, in queue order within a chunk; misses go to no bin (the full path integrator has no miss work).  A pass
 // over the hit ids of its own (in the trace kernel the appends cost registers the traversal needs).  A block takes
 // chunks of kBinItems x 256 consecutive positions of one shard: it counts each class (wave ballots, LDS), makes ONE
 // atomic per class and chunk (per-wave appends on the 16 shard counters saturated them: 313 us per launch), then
@@ -1760,15 +1643,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     stage_scene<QCAP>(sc, 0);
     if constexpr (QCAP == 1) lds_tris = stage_tris1(sc);
     __shared__ int lds[2 * (kBlock / 64) + 1];
-#if RT_APPEND_DB
-    __shared__ int lds_db[2][2 * (kBlock / 64) + 1];  // the pair append's two alternating arrays
-    int par = 0;
-#endif
-#if RT_PAIR_APPEND
-    // single leaf: the first item of a static chunk parks its bounce ray here; the second item appends both
+    // single leaf: the first item of a static chunk parks its bounce ray here; the second item appends both (one
+    // atomic and one round of barriers per chunk: Cornell +3.5 %, r03)
     __shared__ float4 pend[QCAP == 1 ? 2 * kBlock : 1];
     bool pend0 = false;
-#endif
     ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
@@ -1778,9 +1656,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<WAVE>> items(io.ticket, io.q);
     int qj, qidx;
     bool live;
-#if RT_SHADE_PREFETCH
-    int nslot = -1, nprim = -1;  // single leaf: the chunk's second item's (slot, hit), loaded with the first item's
-#endif
     while (items.next(qj, qidx, live)) {
         const int k = qj * io.q.S + qidx;  // queue position
         bool wantShadow = false, wantNext = false, storedL = false;
@@ -1789,27 +1664,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         float stmax = 0.f;
         float Ld[8];
         int slot = -1;
-#if RT_SHADE_PREFETCH
-        int prim = -1;
-        if constexpr (QCAP == 1) {
-            if (items.r == 1) {
-                if (live) { slot = __float_as_int(io.rayO[2 * k].w); prim = io.hitPrim[k]; }
-                const int k1 = k + kBlock;
-                if (k1 < items.n) { nslot = __float_as_int(io.rayO[2 * k1].w); nprim = io.hitPrim[k1]; }
-            } else {
-                slot = live ? nslot : -1;
-                prim = live ? nprim : -1;
-            }
-        } else if (live) {
-            slot = __float_as_int(io.rayO[2 * k].w);
-            prim = io.hitPrim[k];
-        }
-        if (live) {
-#else
         if (live) {
             slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
             const int prim = io.hitPrim[k];
-#endif
             if (prim >= 0) {
                 float lam[8], beta[8];
                 rload8(io.rec, slot, R_LAM, lam);
@@ -1949,7 +1806,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
             const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             rstore8(io.rec, slot, R_L, z);
         }
-#if RT_PAIR_APPEND
         if constexpr (QCAP == 1) {
             nO.w = __int_as_float(slot);  // the ray's origin carries its slot
             if (items.r == 1) {  // first item of the chunk
@@ -1957,12 +1813,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                 pend0 = wantNext;
             } else {
                 int p0, p1;
-#if RT_APPEND_DB
-                block_append2(io.nCount, pend0, wantNext, lds_db[par], p0, p1);
-                par ^= 1;
-#else
                 block_append2(io.nCount, pend0, wantNext, lds, p0, p1);
-#endif
                 if (pend0) {
                     const float4 o0 = pend[2 * threadIdx.x], d0v = pend[2 * threadIdx.x + 1];
                     io.nO[2 * p0] = o0; io.nD[2 * p0] = d0v;
@@ -1975,7 +1826,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
             }
             continue;
         }
-#endif
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // the ray's origin carries its slot
@@ -2062,8 +1912,43 @@ __global__ void __launch_bounds__(kBlock) k_occluded(DevScene sc, int n, const f
     count_add(ctr, C_SFALLBACK, nfb);
 }
 
+// The shadow ray toward one light sample (Lights.h semantics): area lights (quad: p + u0 e1 + u1 e2;
+// disk: the concentric mapping of the Disk shape) and point lights aim at the point, tMax = 0.999 dist; a distant
+// light's direction is fixed (tMax = FLT_MAX; u0, u1 are drawn and unused).  k_path_shade_full evaluates it for the
+// light weights and k_path_nee again for the ray: the same code on the same inputs, so the same bits.
+struct LightRay {
+    V3 wi;
+    float tmax, dist2;
+};
+__device__ __forceinline__ LightRay light_ray(const DevLight& Lt, V3 po, float u0, float u1) {
+    LightRay r;
+    if (Lt.type == 3) {
+        r.wi = v3(Lt.dir[0], Lt.dir[1], Lt.dir[2]);
+        r.tmax = 3.402823466e+38f;
+        r.dist2 = 1.0f;
+        return r;
+    }
+    V3 pl;
+    if (Lt.type == 0) {
+        pl = vadd(vadd(v3(Lt.p[0], Lt.p[1], Lt.p[2]), vmul(v3(Lt.e1[0], Lt.e1[1], Lt.e1[2]), u0)),
+                  vmul(v3(Lt.e2[0], Lt.e2[1], Lt.e2[2]), u1));
+    } else if (Lt.type == 1) {
+        float dx, dy;
+        disk_concentric(u0, u1, dx, dy);
+        pl = m4_point(Lt.o2r, v3(Lt.ro * dx, Lt.ro * dy, Lt.h));
+    } else {
+        pl = v3(Lt.p[0], Lt.p[1], Lt.p[2]);
+    }
+    const V3 wv = vsub(pl, po);
+    r.dist2 = vdot(wv, wv);
+    const float dist = sqrtf(r.dist2);
+    r.wi = vmul(wv, 1.0f / dist);
+    r.tmax = dist * 0.999f;
+    return r;
+}
+
 // MC (material class): 0 every material; 1 the Lambert-or-emitter bin, 2 the mirror-or-dielectric bin (items of
-// io.bin_idx: hits only, the trace kernel dropped the misses) — each bin kernel holds only its materials' code.
+// io.bin_idx: hits only: k_bin_materials appends no miss to any bin) — each bin kernel holds only its materials' code.
 template <int QCAP, int MC>
 #ifndef RT_FULL_WAVES
 #define RT_FULL_WAVES RT_MULTI_WAVES  // the mixed-scene shade (variant builds)
@@ -2208,80 +2093,52 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         } else if constexpr (MC != 2) {  // Lambert: NEE per light (k_path_nee), then a cosine bounce
                             V3 po = vadd(p, vmul(nrm, off));
                             float4* nr = nee.rec + (size_t)slot * nee_f4;
-                            float* nwgt = reinterpret_cast<float*>(nr + N_RAY + sc.n_lights);
-                            nr[N_PO] = make_float4(po.x, po.y, po.z, 0.f);
+                            float* nuv = reinterpret_cast<float*>(nr + N_UV);
+                            float* nwgt = nuv + 4 * ((sc.n_lights + 1) / 2);
                             if (nee.key) neeKey = morton_key(po.x, po.y, po.z, nee.lo, nee.scale, nee.key_bits);
                             for (int li = 0; li < sc.n_lights; ++li) {
                                 const DevLight Lt = ldconst(sc.lights, li);
                                 float u0, u1;
                                 sm.get2d(smp, u0, u1);
-                                V3 wi;
-                                float tmax, wgt;
+                                const LightRay lr = light_ray(Lt, po, u0, u1);
+                                const float cs = vdot(nrm, lr.wi);
                                 bool ok;
+                                float wgt;
                                 if (Lt.type <= 1) {
-                                    V3 pl;
-                                    if (Lt.type == 0) {
-                                        pl = vadd(vadd(v3(Lt.p[0], Lt.p[1], Lt.p[2]), vmul(v3(Lt.e1[0], Lt.e1[1], Lt.e1[2]), u0)),
-                                                  vmul(v3(Lt.e2[0], Lt.e2[1], Lt.e2[2]), u1));
-                                    } else {
-                                        float dx, dy;
-                                        disk_concentric(u0, u1, dx, dy);
-                                        pl = m4_point(Lt.o2r, v3(Lt.ro * dx, Lt.ro * dy, Lt.h));
-                                    }
-                                    V3 wv = vsub(pl, po);
-                                    float dist2 = vdot(wv, wv);
-                                    float dist = sqrtf(dist2);
-                                    wi = vmul(wv, 1.0f / dist);
-                                    float cs = vdot(nrm, wi);
-                                    float cl = -vdot(v3(Lt.n[0], Lt.n[1], Lt.n[2]), wi);
+                                    float cl = -vdot(v3(Lt.n[0], Lt.n[1], Lt.n[2]), lr.wi);
                                     ok = cs > 0 && cl > 0;
-                                    tmax = dist * 0.999f;
-                                    float G = (cs * cl) / dist2;
+                                    float G = (cs * cl) / lr.dist2;
                                     wgt = G * Lt.area;
-                                    if (sc.mis) wgt = wgt * power_heuristic(dist2 / (cl * Lt.area), cs * InvPi);
+                                    if (sc.mis) wgt = wgt * power_heuristic(lr.dist2 / (cl * Lt.area), cs * InvPi);
                                 } else {
-                                    float fall;
-                                    if (Lt.type == 2) {
-                                        V3 wv = vsub(v3(Lt.p[0], Lt.p[1], Lt.p[2]), po);
-                                        float dist2 = vdot(wv, wv);
-                                        float dist = sqrtf(dist2);
-                                        wi = vmul(wv, 1.0f / dist);
-                                        tmax = dist * 0.999f;
-                                        fall = 1.0f / dist2;
-                                    } else {
-                                        wi = v3(Lt.dir[0], Lt.dir[1], Lt.dir[2]);
-                                        tmax = 3.402823466e+38f;
-                                        fall = 1.0f;
-                                    }
-                                    float cs = vdot(nrm, wi);
                                     ok = cs > 0;
-                                    wgt = cs * fall;
+                                    wgt = cs * (Lt.type == 2 ? 1.0f / lr.dist2 : 1.0f);
                                 }
-                                nr[N_RAY + li] = make_float4(wi.x, wi.y, wi.z, ok ? tmax : -1.0f);
-                                nwgt[li] = wgt;
+                                nuv[2 * li] = u0;
+                                nuv[2 * li + 1] = u1;
+                                nwgt[li] = ok ? wgt : -1.0f;  // (an accepted light's weight is >= 0 or NaN)
                                 wantNee = wantNee || ok;
-                            }
-                            if (wantNee) {
-                                float x[8];
-#pragma unroll
-                                for (int i = 0; i < 8; ++i) x[i] = beta[i] * (R[i] * InvPi);
-                                nr[nee_f4 - 2] = make_float4(x[0], x[1], x[2], x[3]);
-                                nr[nee_f4 - 1] = make_float4(x[4], x[5], x[6], x[7]);
                             }
                             // cosine-hemisphere bounce (Sampling.h:449-454), pbrt CoordinateSystem frame
                             float u0, u1;
                             sm.get2d(smp, u0, u1);
                             V3 wi;
                             float z;
-                            if (cosine_bounce(u0, u1, nrm, wi, z)) {
+                            const bool bounced = cosine_bounce(u0, u1, nrm, wi, z);
+                            if (bounced) {
+                                if (!wantNee) {  // (with NEE, k_path_nee forms β R after the light terms)
 #pragma unroll
-                                for (int i = 0; i < 8; ++i) beta[i] *= R[i];
-                                rstore8(io.rec, slot, R_BETA, beta);
+                                    for (int i = 0; i < 8; ++i) beta[i] *= R[i];
+                                    rstore8(io.rec, slot, R_BETA, beta);
+                                }
                                 wantNext = true;
                                 nO = make_float4(po.x, po.y, po.z, 0.f);
                                 nD = make_float4(wi.x, wi.y, wi.z, 0.f);
                                 rec_set_prev_pdf(io.rec, slot, z * InvPi);
                             }
+                            if (wantNee)
+                                nr[N_PO] = make_float4(po.x, po.y, po.z,
+                                                       __uint_as_float((unsigned)mid | (bounced ? 0x80000000u : 0u)));
                         }
                         save_sampler(io, slot, sm);
                     }
@@ -2334,26 +2191,32 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                                                                        NeeIO nee, unsigned long long* ctr) {
     stage_spectra(sp);
     stage_scene<QCAP>(sc, 0);
-    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0, nvx = 0;
     const int nl = sc.n_lights, nf4 = nee_stride(nl);
-    // one path vertex: visibility of each sampled light, then the unoccluded lights' contributions in order
+    // one path vertex: visibility of each sampled light, then the unoccluded lights' contributions in order, then
+    // the throughput of the continued path (NeeIO)
+    const float InvPi = 0.31830988618379067154f;
+    const int nuv4 = (nl + 1) / 2;
     auto vertex = [&](int slot) __attribute__((always_inline)) {
         const float4* r = nee.rec + (size_t)slot * nf4;
         const float4 p4 = r[N_PO];
         const V3 po = v3(p4.x, p4.y, p4.z);
+        const unsigned tag = __float_as_uint(p4.w);
+        const float* uv = reinterpret_cast<const float*>(r + N_UV);
+        const float* wg = uv + 4 * nuv4;
         uint64_t vis = 0;
         ctr_t nv = 0;
         bool defer = false;
         for (int li = 0; li < nl; ++li) {
-            const float4 ray = r[N_RAY + li];
-            if (ray.w < 0) continue;  // light not sampled (cos <= 0)
+            if (wg[li] < 0) continue;  // light not sampled (cos <= 0)
             ++nv;
+            const LightRay lr = light_ray(ldconst(sc.lights, li), po, uv[2 * li], uv[2 * li + 1]);
             bool occ;
             if constexpr (QCAP != 1 && !FB) {
-                occ = scene_occluded_bvh(sc, po, v3(ray.x, ray.y, ray.z), ray.w, snn, snt, defer);
+                occ = scene_occluded_bvh(sc, po, lr.wi, lr.tmax, snn, snt, defer);
                 if (defer) break;
             } else {
-                occ = scene_occluded<QCAP>(sc, po, v3(ray.x, ray.y, ray.z), ray.w, snn, snt, sfb);
+                occ = scene_occluded<QCAP>(sc, po, lr.wi, lr.tmax, snn, snt, sfb);
             }
             if (!occ) vis |= 1ull << li;
         }
@@ -2362,25 +2225,38 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
             return;
         }
         nsh += nv;
-        if (vis) {
-            float lam[8], L[8];
+        nvx += 1;
+        const bool bounced = (tag >> 31) != 0;
+        if (vis || bounced) {
+            float lam[8], beta[8], R[8];
             rload8(io.rec, slot, R_LAM, lam);
-            rload8(io.rec, slot, R_L, L);
-            const float4 xa = r[nf4 - 2], xb = r[nf4 - 1];
-            const float x[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
-            const float* wg = reinterpret_cast<const float*>(r + N_RAY + nl);
-            for (int li = 0; li < nl; ++li) {
-                if (!((vis >> li) & 1)) continue;
-                const DevLight Lt = ldconst(sc.lights, li);
-                const float sc_le = Lt.type <= 1 ? sc.materials[Lt.material].emit : Lt.scale;
-                const float wgt = wg[li];
+            rload8(io.rec, slot, R_BETA, beta);
+            const DevMaterial mt = sc.materials[tag & 0x7fffffffu];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    float Le = sc_le * d65_query(sp, lam[i]);
-                    L[i] += ((x[i] * Le)) * wgt;
+            for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.c0, mt.c1, mt.c2, lam[i]);
+            if (vis) {
+                float L[8], x[8];
+                rload8(io.rec, slot, R_L, L);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) x[i] = beta[i] * (R[i] * InvPi);
+                for (int li = 0; li < nl; ++li) {
+                    if (!((vis >> li) & 1)) continue;
+                    const DevLight Lt = ldconst(sc.lights, li);
+                    const float sc_le = Lt.type <= 1 ? sc.materials[Lt.material].emit : Lt.scale;
+                    const float wgt = wg[li];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        float Le = sc_le * d65_query(sp, lam[i]);
+                        L[i] += ((x[i] * Le)) * wgt;
+                    }
                 }
+                rstore8(io.rec, slot, R_L, L);
             }
-            rstore8(io.rec, slot, R_L, L);
+            if (bounced) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) beta[i] *= R[i];
+                rstore8(io.rec, slot, R_BETA, beta);
+            }
         }
     };
     if constexpr (FB) {
@@ -2400,6 +2276,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
     count_add(ctr, C_SFALLBACK, sfb);
+    count_add(ctr, C_NEEVTX, nvx);
     if constexpr (QCAP != 1 && !FB) simd_flush();
 }
 

@@ -51,19 +51,31 @@ class FrameLoop:
         self.frames_done = 0
 
     def step(self, render):
-        """render(i0, i1, film) accumulates indices [i0, i1) of this rank's pixels; returns i1 - i0."""
+        """render(i0, i1, film) accumulates indices [i0, i1) of this rank's pixels; returns i1 - i0.
+
+        At frame end only `dst` keeps the reduced frame, by swapping buffers (no copy): the reduced film becomes
+        `frame` and the previous frame's buffer, zeroed, the next accumulation film.  The other ranks' films hold
+        only their own pixels after the reduce and are simply zeroed."""
         i0 = self.cursor
         i1 = min(self.spp, i0 + self.per_step)
         render(i0, i1, self.film)
         if i1 >= self.spp:
             reduce_film(self.film, dst=self.dst)
-            self.frame = self.film.clone()
+            if _rank() == self.dst:
+                spare = self.frame
+                self.frame = self.film
+                self.film = spare if spare is not None else self.film.new_zeros(self.film.shape)
             self.film.zero_()
             self.frames_done += 1
             self.cursor = 0
         else:
             self.cursor = i1
         return i1 - i0
+
+
+def _rank():
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_initialized() else 0
 
 
 def reduce_film(film, dst=0):

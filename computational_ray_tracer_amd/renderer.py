@@ -130,6 +130,22 @@ class Renderer:
                                                                   P(tmax, C.c_float), P(occ, C.c_int32)))
         return occ
 
+    def debug_sort(self, which, S, shard_len, keys, slots=None, bits_a=3, bits_b=3):
+        """rt_debug_sort: the ray (which 0) or NEE (which 1) coherence sort on a synthetic sharded queue; returns the
+        output array (8 S int32: queue positions / slots at the sorted positions) and the rewritten shard lengths."""
+        shard_len = np.ascontiguousarray(shard_len, np.int32)
+        keys = np.ascontiguousarray(keys, np.uint32)
+        assert len(shard_len) == capi.QUEUE_SHARDS and len(keys) == capi.QUEUE_SHARDS * S
+        sl = None if slots is None else np.ascontiguousarray(slots, np.int32)
+        out = np.zeros(capi.QUEUE_SHARDS * S, np.int32)
+        olen = np.zeros(capi.QUEUE_SHARDS, np.int32)
+        P = lambda a, t: a.ctypes.data_as(C.POINTER(t))
+        self._chk("rt_debug_sort", self.lib.rt_debug_sort(self.h, int(which), int(S), P(shard_len, C.c_int32),
+                                                          P(keys, C.c_uint32), None if sl is None else P(sl, C.c_int32),
+                                                          int(bits_a), int(bits_b), P(out, C.c_int32),
+                                                          P(olen, C.c_int32)))
+        return out, olen
+
     def samples(self, pixel_ids, indices):
         pixel_ids = np.ascontiguousarray(pixel_ids, np.int32)
         indices = np.ascontiguousarray(indices, np.int32)

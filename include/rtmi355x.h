@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 typedef enum {
     RT_OK = 0,
@@ -38,6 +38,7 @@ typedef enum {
 typedef struct rt_ctx rt_ctx;
 
 #define RT_MAX_DEVICES 16
+#define RT_QUEUE_SHARDS 8   /* shards of the multi-level path queues (rt_debug_sort) */
 /* rt_create ("device list"): n_devices <= 1 renders on `device`; n_devices > 1 renders every pass
  * on devices[0..n_devices) at once — pixel tiles interleaved over the devices (tile t -> device t mod n), the
  * caller's film on devices[0] (rt_render_pass_device) or on the host, owned pixels exchanged with peer copies
@@ -215,6 +216,7 @@ typedef struct {
                                         ambiguous (canonical rule), traced by the reference BFS */
     int64_t shadow_fallback_rays;    /* the same for any-hit (shadow) rays                */
     double ms_sort;                  /* multi-level octrees: coherence sort of bounce rays (HIP events)  */
+    int64_t nee_vertices;            /* mixed scenes: path vertices whose light samples k_path_nee traced */
 } rt_stats;   /* multi-device contexts: every field summed over the devices */
 
 /* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */
@@ -325,6 +327,15 @@ int rt_debug_trace(rt_ctx* ctx, int n, const float* ro, const float* rd, int use
 int rt_debug_occluded(rt_ctx* ctx, int n, const float* ro, const float* rd, const float* tmax, int32_t* occluded);
 /* K1..K3 for n explicit (pixel_id, index) samples (reference integrator). */
 int rt_debug_samples(rt_ctx* ctx, int n, const int32_t* pixel_ids, const int32_t* indices, rt_sample_record* out);
+/* The multi-level coherence sorts alone (rt_sort.hip: stable device LSD radix sorts) on a synthetic queue of
+ * RT_QUEUE_SHARDS shards of stride S (a multiple of 64): shard j holds shard_len[j] <= S items at positions
+ * [j S, j S + shard_len[j]), with keys[pos] (8 S entries) and, for the NEE sort, slots[pos].  which 0: the bounce-ray
+ * sort (key bits 3 + 2 bits_a + 3 bits_b; out[pos'] = the queue position of the sorted item at pos'); which 1: the
+ * NEE-vertex sort (key bits 3 bits_a; out = the slots, sorted in place).  Sorted item k' sits at position
+ * (k' / S2) S + k' % S2, S2 = ceil(ceil(n / 8) / 64) 64; out_len[8] = the rewritten shard lengths.  Not a
+ * reference function (the reference has no sort): exported so tests can check order and stability directly. */
+int rt_debug_sort(rt_ctx* ctx, int which, int S, const int32_t* shard_len, const uint32_t* keys, const int32_t* slots,
+                  int bits_a, int bits_b, int32_t* out, int32_t* out_len);
 
 #ifdef __cplusplus
 }

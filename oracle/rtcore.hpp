@@ -949,14 +949,30 @@ struct Octree {
     }
 
     struct Hit { int tri = -1; TriIsect isect{}; long nodes_tested = 0, tris_tested = 0; };
+    // The BFS queue of Traverse / Occluded: std::queue's FIFO order (Octtree_Model.h:70-75) over one buffer per host
+    // thread, reused from ray to ray.  A std::queue per ray allocates a deque block on every call, and the CPU
+    // baseline's threads then contend in malloc (bench.py cpu_baseline); the visiting order is unchanged.
+    struct Fifo {
+        std::vector<int> v;
+        size_t h = 0;
+        void push(int x) { v.push_back(x); }
+        bool empty() const { return h == v.size(); }
+        int pop() { return v[h++]; }
+    };
+    static Fifo& fifo(int which) {
+        thread_local Fifo f[2];
+        f[which].v.clear();
+        f[which].h = 0;
+        return f[which];
+    }
     // Octtree_Model.h:66-127 Traverse — BFS with a shrinking tMax, first hit in BFS order wins ties
     Hit Traverse(const Ray& ray, bool use_cull) const {
         Hit h;
         float tMax = std::numeric_limits<float>::max();
-        std::queue<int> q;
+        Fifo& q = fifo(0);
         q.push(0);
         while (!q.empty()) {
-            int cur = q.front(); q.pop();
+            int cur = q.pop();
             ++h.nodes_tested;
             if (IntersectP(nodes[cur].bounds, ray, tMax)) {
                 if (nodes[cur].leaf) {
@@ -977,10 +993,10 @@ struct Octree {
     }
     // any-hit with a fixed tMax (path mode shadow rays, build-defined): order-independent answer
     bool Occluded(const Ray& ray, float tMax) const {
-        std::queue<int> q;
+        Fifo& q = fifo(1);
         q.push(0);
         while (!q.empty()) {
-            int cur = q.front(); q.pop();
+            int cur = q.pop();
             if (!IntersectP(nodes[cur].bounds, ray, tMax)) continue;
             if (nodes[cur].leaf) {
                 for (int t : nodes[cur].tris) {

@@ -12,7 +12,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
       v=${item%%+*}; envs=""; [ "$item" != "$v" ] && envs=$(echo ${item#*+} | tr '+' ' ')
       tag=$(echo "${c}_${item}" | tr '/+=' '___')
       env RTMI_LIB=$PWD/computational_ray_tracer_amd/lib/variants/$v.so $envs timeout -k 10 300 \
-        python bench.py --config $c --steps $s --warmup 1 --no-cpu-baseline > gpurun_out/abs_${tag}_$r.log 2>&1
+        python bench.py --config $c --steps $s --warmup 1 --no-cpu-baseline --project-shards 0 > gpurun_out/abs_${tag}_$r.log 2>&1
       rc=$?; [ $rc -ne 0 ] && { echo "$c $item rc=$rc"; tail -3 gpurun_out/abs_${tag}_$r.log; exit $rc; }
       python3 -c "
 import json

@@ -8,7 +8,7 @@ TAG=${TAG:-r02}
 mkdir -p gpurun_out
 for c in ${CONFIGS:-cornell cfg3 cfg4}; do
   D=gpurun_out/cnt_${c}_$TAG
-  B="python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline"
+  B="python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --project-shards 0"
   RTMI_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/kt -o kt --output-format csv -- $B > $D.kt.log 2>&1
   rc=$?; echo "$c kt rc=$rc"; [ $rc -ne 0 ] && exit $rc
   RTMI_LANES=1 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $D/fetch -o pmc --output-format csv -- $B > $D.fetch.log 2>&1

@@ -24,12 +24,13 @@ def test_trace_bytes_with_and_without_the_sort_gather():
 
 
 def test_nee_record_bytes_and_traffic_ratio():
-    st = _stats()
+    st = _stats(nee_vertices=250_000)
     counters = {"k_path_nee": {"dram_bytes_per_launch": 12_000_000, "valu_insts_per_launch": 1e6}}
     rl = bench.kernel_rooflines(st, counters, "k_path_nee", sorted_bounces=True, n_lights=4)
     nee = rl["k_path_nee"]
-    # 32 B per shadow ray + the 128-B record (16 B point, 4 x 16 B rays, 16 B weights, 32 B throughput) per vertex
-    assert nee["algorithmic_bytes_per_launch"] == (32 * 800_000 + 128 * 800_000 // 4) // 10
+    # 32 B per shadow ray + per vertex the 64-B record (16 B point + material, 4 x 8 B light samples, 16 B
+    # weights), the slot's λ, β, L read (96 B) and L, β written (64 B)
+    assert nee["algorithmic_bytes_per_launch"] == (32 * 800_000 + (64 + 96 + 64) * 250_000) // 10
     assert nee["traffic"] == 12_000_000
     assert nee["traffic_over_algorithmic"] == round(12_000_000 / nee["algorithmic_bytes_per_launch"], 2)
     assert 0 < nee["valu"]["frac"] <= 1.0

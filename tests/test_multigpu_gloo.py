@@ -39,8 +39,11 @@ def _worker(rank, world, port, q):
     for _ in range(3):
         loop.step(render)
     assert loop.frames_done == 1
+    # only dst keeps the reduced frame (its film buffer swapped out, no clone); the others keep no frame copy
+    assert (loop.frame is not None) == (rank == 0)
     if rank == 0:
-        q.put((film.numpy().copy(), loop.frame.numpy().copy(), acc.numpy().copy(), pix))
+        assert loop.frame.data_ptr() == acc.data_ptr() and loop.film.data_ptr() != acc.data_ptr()
+        q.put((film.numpy().copy(), loop.frame.numpy().copy(), loop.film.numpy().copy(), pix))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -97,6 +100,7 @@ def _timed_worker(rank, world, port, q):
 
     tm = timed_steps(lambda: loop.step(render), 6, 1, lambda: None, lambda: done["samples"],
                      lambda: done.update(samples=0))
+    assert (loop.frame is not None) == (rank == 0)  # dst-only frame
     if rank == 0:
         q.put((tm, loop.frames_done, loop.frame.numpy().copy(), len(pix)))
     dist.barrier()
