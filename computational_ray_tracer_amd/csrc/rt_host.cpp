@@ -1095,7 +1095,11 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     // Cornell-like single-leaf scenes cost the same per ray: static chunks on a resident grid beat tickets there
     // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
     const bool dyn = c->dsc.qcap != 1;
-    const bool lean = !c->dsc.full;  // simple path kernel: no β / L / pdf streams (+4.5 %)
+    // k_generate stores no β = 1 / L = 0 / pdf streams: depth 0 starts from them in registers and the film recomputes
+    // the pdf (simple path: +4.5 %).  1: the simple path (the host derives each depth's sampler dimension); 2: mixed
+    // scenes, whose slots keep their dimension, prevPdf and TerminateSecondary flag in R_MISC (CFG4: k_generate
+    // writes 96 instead of 192 B per sample)
+    const int lean = c->dsc.full ? 2 : 1;
     // multi-level simple scenes: the NEE shadow rays the BVH alone cannot decide (or, with RTMI_SHADOW_QUEUE=1,
     // all of them) are queued and traced exactly by their own kernel
     const bool shq = c->dsc.qcap != 1 && !c->dsc.full;
@@ -1128,7 +1132,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     const bool records = c->dsc.qcap != 1;
     const size_t rec_fs = records ? 1 : nmax;
     const unsigned rec_ss = records ? (unsigned)kRecF4 : 1u;
-    const int rec_rng8 = !records && lean ? 1 : 0;  // SoA simple path: dense 8-byte PCG states
+    const int rec_rng8 = !records && lean == 1 ? 1 : 0;  // SoA simple path: dense 8-byte PCG states
     int last_film = -1;      // lane of the most recent film launch
     for (int g0 = ib; g0 < ie; g0 += B * lanes) {
         int nIdx[kLanes] = {0}, cur[kLanes] = {0}, nSq[kLanes] = {0}, Sq[kLanes] = {0};
@@ -1143,7 +1147,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             nSq[l] = nS;
             Sq[l] = shard_stride(nS, nsh);  // every queue of this batch: shard j at [j S, j S + len_j)
             SampleIds ids = sample_ids(c, b0);
-            GenOut go{w.rayO, w.rayD, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean ? 1 : 0, 1};
+            GenOut go{w.rayO, w.rayD, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean, 1};
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, s, ST_GEN, e0);
@@ -1175,6 +1179,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 const DevScene dsl = lane_scene(c, w);
                 TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
                 BinIO bio{qv, w.hitPrim, {w.neeSlot + 3 * ncap, w.neeSlot + 4 * ncap}, qc_cur + kQBinLen};
+                if (depth == 0) { bio.rayO = cO; bio.rec = rv; }  // lean depth 0: the misses' L = 0 (BinIO)
                 static_assert(kMatClasses == 2, "bin index lists");
                 if (sort_rays && depth > 0) {  // the device reads the queue length itself: no host round trip
                     SortRaysIO so{w.sQKey, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
@@ -1190,7 +1195,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
                 ev_mark(c, s, ST_TRACE, e0);
                 PathIO pio{};
-                pio.lean = lean ? 1 : 0;
+                pio.lean = lean;
                 pio.rayO = cO; pio.rayD = cD; pio.q = qv;
                 pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
                 pio.nO = w.rayO + 2 * (size_t)nxt * qs; pio.nD = pio.nO + 1;
@@ -1198,7 +1203,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 pio.rec = rv; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;
                 pio.depth = depth; pio.max_depth = c->integ.max_depth;
                 pio.dim = -1;
-                if (lean) {
+                if (lean == 1) {
                     pio.dim = dim_after_camera(smp, cam);
                     for (int d = 0; d < depth; ++d) pio.dim = dim_get2d(smp, dim_get2d(smp, pio.dim));
                 }
@@ -1269,7 +1274,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             const RecView rv{w.rec, rec_fs, rec_ss, rec_rng8};
             if (last_film >= 0 && last_film != l) HIPCHK(c, hipStreamWaitEvent(s, c->ws[last_film].film_done, 0));
             PathFilmIO fio{c->d_work, c->n_work, nIdx[l], rv, w.pdfA, w.pdfB, film};
-            fio.lean = lean ? 1 : 0;
+            fio.lean = lean;
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_path_film(s, 0, c->d_spec, fd, fio, c->d_ctr));
             ev_mark(c, s, ST_FILM, e0);
@@ -2026,6 +2031,8 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         const int src = bvh[st].nodes.empty() ? 0 : st;
         c->bvh_count[st][0] = (int)(bvh[src].nodes.size() / kBvhNodeF4);
         c->bvh_count[st][1] = (int)bvh[src].tid.size();
+    }
+    for (int st = 0; st < 3; ++st) {
         if (bvh[st].nodes.empty()) continue;
         // the kernels stage nodes [0, kBvhTopNodes) in LDS unconditionally: pad with empty nodes
         if (bvh[st].nodes.size() < kBvhNodeF4 * (size_t)kBvhTopNodes)

@@ -220,8 +220,9 @@ struct GenOut {
     float4* rayO; float4* rayD;   // the origin's w = the ray's path slot
     float4* lamA; float4* lamB; float4* pdfA; float4* pdfB;  // reference mode (lamA/lamB) + pdfs
     RecView rec;                                             // path mode: the slot state (λ, sampler, β, L, ...)
-    int lean;  // simple path kernel: no β = 1 / L = 0 / pdf / dimension stores (depth 0, the film kernel and the
-               // host's per-depth dimension derive them)
+    int lean;  // no β = 1 / L = 0 / pdf stores (depth 0 and the film kernel derive them); 1: the simple path, which
+               // stores no dimension either (the host derives each depth's); 2: mixed scenes (dimension, prevPdf = 0
+               // and the TerminateSecondary flag 0 in R_MISC)
     int rsh = 0;  // ray k at rayO[k << rsh] / rayD[k << rsh] (1: the workspace's interleaved (o, d) pairs)
 };
 
@@ -283,6 +284,10 @@ struct BinIO {
     const int* hitPrim;
     int* idx[kMatClasses];
     int* len;
+    // lean depth 0 (GenOut lean): k_generate left L unwritten, so the misses' L = 0 is stored here (no bin sees them);
+    // rayO == nullptr otherwise.  Queue rays are interleaved (o, d) pairs: ray k's origin (w = slot) at rayO[2k].
+    const float4* rayO = nullptr;
+    RecView rec{};
 };
 hipError_t launch_bin_materials(hipStream_t st, int grid, const DevScene& sc, const BinIO& io);
 
@@ -309,7 +314,8 @@ struct PathIO {
     RecView rec;                                                          // slot state (R_LAM ...)
     float4* pdfA; float4* pdfB;                                           // TerminateSecondary writes them
     int depth, max_depth;
-    int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers
+    int lean;   // k_generate ran lean (GenOut::lean): depth 0 starts from β = 1, L = 0 in registers; 2: the pdfs are
+                // not stored either, TerminateSecondary sets R_MISC's z instead (k_path_film recomputes the pdfs)
     int dim;    // >= 0: the sampler dimension every path of this depth starts from (simple path: each bounce takes
                 // two Get2D); -1: per slot in R_MISC
     int* ticket;  // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
@@ -390,7 +396,8 @@ struct PathFilmIO {
     const int* work_pixels; int n_pixels; int n_index;
     RecView rec; const float4* pdfA; const float4* pdfB;
     float4* film;
-    int lean;  // pdf = VisibleWavelengthsPDF(λ) recomputed here (nothing rewrites it on the simple path)
+    int lean;  // pdf = VisibleWavelengthsPDF(λ) recomputed here; 2: and divided as TerminateSecondary did when the
+               // slot's R_MISC z flag is set (mixed scenes: dispersive glass)
 };
 
 struct RecordIO {

@@ -541,8 +541,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
                 *reinterpret_cast<uint4*>(recf(out.rec, s, R_RNG)) =
                     make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
                                (uint32_t)(sm.rng.inc >> 32));
+            if (out.lean != 1)  // (dimension, prevPdf 0, TerminateSecondary flag 0)
+                *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, 0.f);
             if (!out.lean) {
-                *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, 0.f);  // (dimension, prevPdf 0)
                 const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
                 const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 rstore8(out.rec, s, R_BETA, one);
@@ -1479,6 +1480,10 @@ __global__ void __launch_bounds__(kBlock) k_bin_materials(DevScene sc, BinIO io)
                 const int prim = io.hitPrim[j * io.q.S + idx];
                 if (prim >= 0)
                     cls[r] = mat_at(sc, lds_mats, prim < sc.n_tris ? sc.triMaterial[prim] : sc.shapes[prim - sc.n_tris].material).cls;
+                else if (io.rayO) {  // lean depth 0: a camera ray that missed ends with L = 0
+                    const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    rstore8(io.rec, __float_as_int(io.rayO[2 * (j * io.q.S + idx)].w), R_L, z);
+                }
             }
         }
 #pragma unroll
@@ -1962,6 +1967,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     if constexpr (MC != 2) stage_spectra(sp);  // (the mirror / glass bin reads no spectrum table)
     const bool lds_mats = stage_materials(sc);
     const int nee_f4 = nee_stride(sc.n_lights);
+    // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
+    const bool d0 = io.lean && io.depth == 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
     constexpr bool WAVE = QCAP != 1;
     // single leaf: the host gives the queues one shard (rt_host.cpp nsh)
@@ -1975,13 +1982,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         unsigned neeKey = 0;
         float4 nO = make_float4(0, 0, 0, 0), nD = nO;
         int slot = -1;
+        bool storedL = false;
         if (live) {
             slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
             int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
                 rload8(io.rec, slot, R_LAM, lam);
-                rload8(io.rec, slot, R_BETA, beta);
+                if (d0) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) beta[i] = 1.f;
+                } else {
+                    rload8(io.rec, slot, R_BETA, beta);
+                }
                 float4 o4 = io.rayO[2 * k], d4 = io.rayD[2 * k];
                 V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
                 V3 rayd = vnorm(rdw);
@@ -2021,7 +2034,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                 if (MC != 2 && mt.emit > 0) {  // one-sided pure emitter, ends the path
                     if (front) {
                         float L[8];
-                        rload8(io.rec, slot, R_L, L);
+                        rload8_or_zero(io.rec, slot, R_L, L, d0);
                         if (prevPdf == 0) {
 #pragma unroll
                             for (int i = 0; i < 8; ++i) L[i] += beta[i] * (mt.emit * d65_query(sp, lam[i]));
@@ -2038,6 +2051,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                             }
                         }
                         rstore8(io.rec, slot, R_L, L);
+                        storedL = true;
                     }
                 } else if (io.depth < io.max_depth) {
                     float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
@@ -2058,16 +2072,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed);
                         if (MC != 1 && mt.type == 2) {  // smooth dielectric
                             if (mt.eta == 0) {  // dispersive BK7: TerminateSecondary (spectrum.h:302-310)
-                                float pdf[8];
-                                load8(io.pdfA, io.pdfB, slot, pdf);
-                                bool term = true;
+                                if (io.lean == 2) {  // the pdfs are not stored: flag it, k_path_film divides
+                                    reinterpret_cast<float*>(recf(io.rec, slot, R_MISC))[2] = 1.f;
+                                } else {
+                                    float pdf[8];
+                                    load8(io.pdfA, io.pdfB, slot, pdf);
+                                    bool term = true;
 #pragma unroll
-                                for (int i = 1; i < 8; ++i) term = term && pdf[i] == 0;
-                                if (!term) {
+                                    for (int i = 1; i < 8; ++i) term = term && pdf[i] == 0;
+                                    if (!term) {
 #pragma unroll
-                                    for (int i = 1; i < 8; ++i) pdf[i] = 0;
-                                    pdf[0] /= 8;
-                                    store8(io.pdfA, io.pdfB, slot, pdf);
+                                        for (int i = 1; i < 8; ++i) pdf[i] = 0;
+                                        pdf[0] /= 8;
+                                        store8(io.pdfA, io.pdfB, slot, pdf);
+                                    }
                                 }
                             }
                             float eta = mt.eta != 0 ? mt.eta : piecewise_query(sp->bk7_lambda, sp->bk7_value, sp->bk7_n, lam[0]);
@@ -2079,6 +2097,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                             if (u < Fr || !refract_dir(wo, nout, eta, etap, wt)) {
                                 po = vadd(p, vmul(nrm, off));
                                 wi = reflect_dir(rayd, nrm);
+                                if (d0) rstore8(io.rec, slot, R_BETA, beta);  // (lean: β = 1 was never stored)
                             } else {
 #pragma unroll
                                 for (int i = 0; i < 8; ++i) beta[i] /= (etap * etap);
@@ -2144,6 +2163,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                     }
                 }
             }
+        }
+        if (d0 && slot >= 0 && !storedL) {  // (k_path_nee and the film read it; misses: k_bin_materials or here)
+            const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            rstore8(io.rec, slot, R_L, z);
         }
         if constexpr (MC != 2) {
             const int pe = queue_append<WAVE>(nee.len + qj * kQStride, wantNee, lds) + qj * io.q.S;
@@ -2230,7 +2253,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         if (vis || bounced) {
             float lam[8], beta[8], R[8];
             rload8(io.rec, slot, R_LAM, lam);
-            rload8(io.rec, slot, R_BETA, beta);
+            if (io.lean && io.depth == 0) {  // (lean depth 0: β = 1, never stored)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) beta[i] = 1.f;
+            } else {
+                rload8(io.rec, slot, R_BETA, beta);
+            }
             const DevMaterial mt = sc.materials[tag & 0x7fffffffu];
 #pragma unroll
             for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.c0, mt.c1, mt.c2, lam[i]);
@@ -2296,6 +2324,11 @@ __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevF
             if (io.lean) {
 #pragma unroll
                 for (int w = 0; w < 8; ++w) pdf[w] = visible_pdf<WarpTab>(lam[w]);  // the value k_generate would have stored
+                if (io.lean == 2 && recf(io.rec, s, R_MISC)->z != 0.f) {  // TerminateSecondary (spectrum.h:302-310)
+#pragma unroll
+                    for (int w = 1; w < 8; ++w) pdf[w] = 0;
+                    pdf[0] /= 8;
+                }
             } else {
                 load8(io.pdfA, io.pdfB, s, pdf);
             }
