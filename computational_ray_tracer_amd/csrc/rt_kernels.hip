@@ -1090,6 +1090,7 @@ static constexpr int kLeafStep = 8;  // triangles per leaf phase of the BVH walk
 struct Bvh8Ray {
     V3 inv, oi;
 };
+typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void node_keys(const BvhNode8& n, const Bvh8Ray& r, float tcut, unsigned k[8], bool sort) {
     const unsigned w0 = __float_as_uint(n.N0.w);
     const float sx = ldexpf(r.inv.x, (int)(w0 & 255u) - 127), sy = ldexpf(r.inv.y, (int)((w0 >> 8) & 255u) - 127),
@@ -1101,19 +1102,18 @@ __device__ __forceinline__ void node_keys(const BvhNode8& n, const Bvh8Ray& r, f
     const unsigned ny0 = py ? n.QY.x : n.QY.z, ny1 = py ? n.QY.y : n.QY.w, fy0 = py ? n.QY.z : n.QY.x, fy1 = py ? n.QY.w : n.QY.y;
     const unsigned nz0 = pz ? n.QZ.x : n.QZ.z, nz1 = pz ? n.QZ.y : n.QZ.w, fz0 = pz ? n.QZ.z : n.QZ.x, fz1 = pz ? n.QZ.w : n.QZ.y;
     const unsigned valid = n.N1.w;
+    // (near, far) plane pairs of one axis in one packed FMA (v_pk_fma_f32: two IEEE fmas, the same bits)
+    const f2v SX = {sx, sx}, SY = {sy, sy}, SZ = {sz, sz}, BX = {bx, bx}, BY = {by, by}, BZ = {bz, bz};
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
         const int sh = 8 * (s & 3);
         const unsigned nx = s < 4 ? nx0 : nx1, fx = s < 4 ? fx0 : fx1, ny = s < 4 ? ny0 : ny1, fy = s < 4 ? fy0 : fy1;
         const unsigned nz = s < 4 ? nz0 : nz1, fz = s < 4 ? fz0 : fz1;
-        const float tnx = __builtin_fmaf((float)((nx >> sh) & 255u), sx, bx);
-        const float tny = __builtin_fmaf((float)((ny >> sh) & 255u), sy, by);
-        const float tnz = __builtin_fmaf((float)((nz >> sh) & 255u), sz, bz);
-        const float tfx = __builtin_fmaf((float)((fx >> sh) & 255u), sx, bx);
-        const float tfy = __builtin_fmaf((float)((fy >> sh) & 255u), sy, by);
-        const float tfz = __builtin_fmaf((float)((fz >> sh) & 255u), sz, bz);
-        const float tn = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, 0.f));
-        const float tf = fminf(fminf(tfx, tfy), fminf(tfz, tcut)) * 1.00000048f;
+        const f2v tx = __builtin_elementwise_fma((f2v){(float)((nx >> sh) & 255u), (float)((fx >> sh) & 255u)}, SX, BX);
+        const f2v ty = __builtin_elementwise_fma((f2v){(float)((ny >> sh) & 255u), (float)((fy >> sh) & 255u)}, SY, BY);
+        const f2v tz = __builtin_elementwise_fma((f2v){(float)((nz >> sh) & 255u), (float)((fz >> sh) & 255u)}, SZ, BZ);
+        const float tn = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, 0.f));
+        const float tf = fminf(fminf(tx.y, ty.y), fminf(tz.y, tcut)) * 1.00000048f;
         k[s] = (((valid >> s) & 1u) && tn <= tf) ? ((__float_as_uint(tn) & 0x7ffffff8u) | (unsigned)s) : kNoChild;
     }
     if (!sort) return;  // (any-hit walks: any order gives the same answer)
