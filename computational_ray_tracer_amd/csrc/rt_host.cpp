@@ -439,7 +439,7 @@ struct Work {
     int* d_qcount = nullptr;   // queue q's counters at [q * kQRegion + kQLen / kQTraceTicket / ...] (rt_internal.h)
     // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers
     float4 *sO = nullptr, *sD = nullptr;
-    int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;  // sS: the sort permutation (TraceIO perm)
+    int *sVals = nullptr, *sValsAlt = nullptr;
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
     unsigned* sQKey = nullptr;  // the ray queue's sort keys at queue positions (written by the shade kernels)
     void* sTemp = nullptr;      // the sorts' histograms and meta (sort_temp_bytes)
@@ -618,11 +618,11 @@ int ensure_shadow_workspace(rt_ctx* c, Work& w, size_t n) {
 }
 
 void free_sort_workspace(Work& w) {
-    void* ptrs[] = {w.sO, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sQKey, w.sTemp};  // (sD = sO + 1)
+    void* ptrs[] = {w.sO, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sQKey, w.sTemp};  // (sD = sO + 1)
     for (void* p : ptrs)
         if (p) hipFree(p);
     w.sO = w.sD = nullptr;
-    w.sS = w.sVals = w.sValsAlt = nullptr;
+    w.sVals = w.sValsAlt = nullptr;
     w.sKeys = w.sKeysAlt = w.sQKey = nullptr;
     w.sTemp = nullptr;
     w.sCap = 0;
@@ -632,7 +632,7 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
     if (w.sCap >= n) return RT_OK;
     free_sort_workspace(w);
     // the side queue's rays as interleaved (o, d) pairs like the queues' (sD = sO + 1)
-    HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1; HIPCHK(c, dalloc(&w.sS, n));
+    HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1;
     HIPCHK(c, dalloc(&w.sVals, n)); HIPCHK(c, dalloc(&w.sValsAlt, n));
     HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n)); HIPCHK(c, dalloc(&w.sQKey, n));
     HIPCHK(c, hipMalloc(&w.sTemp, sort_temp_bytes()));
@@ -1182,14 +1182,13 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 if (depth == 0) { bio.rayO = cO; bio.rec = rv; }  // lean depth 0: the misses' L = 0 (BinIO)
                 static_assert(kMatClasses == 2, "bin index lists");
                 if (sort_rays && depth > 0) {  // the device reads the queue length itself: no host round trip
-                    SortRaysIO so{w.sQKey, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
+                    SortRaysIO so{w.sQKey, cO, w.sO, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
                                   c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l]};
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, so));
                     ev_mark(c, s, ST_SORT, e0);
-                    tio.perm = w.sS;  // the trace kernel gathers the sorted rays into the side queue
-                    tio.so = w.sO;
-                    cO = w.sO; cD = w.sD;
+                    cO = w.sO; cD = w.sD;  // the last sort pass gathered the rays into the sorted side queue
+                    tio.rayO = cO; tio.rayD = cD;
                 }
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
@@ -2424,6 +2423,7 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
     const size_t cap = (size_t)kShards * S;
     unsigned *dkey = nullptr, *k0 = nullptr, *k1 = nullptr;
     int *dslot = nullptr, *dlen = nullptr, *dout = nullptr, *v0 = nullptr, *v1 = nullptr;
+    float4 *rin = nullptr, *rout = nullptr;  // rays: the queue position rides in the origin's w
     void* temp = nullptr;
     if (dalloc(&dkey, cap) || dalloc(&dslot, cap) || dalloc(&dlen, (size_t)kShards * kQStride) || dalloc(&dout, cap) ||
         dalloc(&k0, cap) || dalloc(&k1, cap) || dalloc(&v0, cap) || dalloc(&v1, cap) ||
@@ -2438,10 +2438,31 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
         if (e == hipSuccess) e = hipMemcpy(dslot, hs.data(), cap * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(dlen, hlen.data(), hlen.size() * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemset(dout, 0xff, cap * 4);
+        if (e == hipSuccess && which == 0) {
+            if (dalloc(&rin, 2 * cap) || dalloc(&rout, 2 * cap)) e = hipErrorOutOfMemory;
+            std::vector<float4> hr(2 * cap, make_float4(0.f, 0.f, 0.f, 0.f));
+            for (size_t i = 0; i < cap; ++i) {
+                std::memcpy(&hr[2 * i].w, &i, 4);
+                hr[2 * i + 1].x = (float)i;  // (the direction travels too)
+            }
+            if (e == hipSuccess) e = hipMemcpy(rin, hr.data(), hr.size() * 16, hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemset(rout, 0xff, 2 * cap * 16);
+        }
         if (e == hipSuccess) {
             if (which == 0) {
-                SortRaysIO so{dkey, dout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S};
+                SortRaysIO so{dkey, rin, rout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S};
                 e = launch_sort_rays(c->stream, so);
+                if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+                if (e == hipSuccess) {  // out[pos'] = the origin's w (the queue position), -1 where nothing landed;
+                    std::vector<float4> hr(2 * cap);  // a direction that did not travel with its origin is an error
+                    e = hipMemcpy(hr.data(), rout, hr.size() * 16, hipMemcpyDeviceToHost);
+                    std::vector<int> ho(cap);
+                    for (size_t i = 0; i < cap && e == hipSuccess; ++i) {
+                        std::memcpy(&ho[i], &hr[2 * i].w, 4);
+                        if (ho[i] != -1 && hr[2 * i + 1].x != (float)ho[i]) ho[i] = -2;
+                    }
+                    if (e == hipSuccess) e = hipMemcpy(dout, ho.data(), cap * 4, hipMemcpyHostToDevice);
+                }
             } else {
                 SortNeeIO so{dslot, dlen, S, dkey, k0, k1, v0, v1, temp, bits_a};
                 e = launch_sort_nee(c->stream, so);
@@ -2454,6 +2475,7 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
         else
             for (int j = 0; j < kShards; ++j) out_len[j] = hlen[(size_t)j * kQStride];
     }
+    hipFree(rin); hipFree(rout);
     hipFree(dkey); hipFree(dslot); hipFree(dlen); hipFree(dout);
     hipFree(k0); hipFree(k1); hipFree(v0); hipFree(v1); hipFree(temp);
     if (!rc) rc = mark_done(c, c->stream);

@@ -270,10 +270,6 @@ struct TraceIO {
     int* hitPrim;
     int* ticket = nullptr;    // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
     int rsh = 0;              // ray k at rayO[k << rsh] (1: the workspace's interleaved (o, d) pairs; 0: caller arrays)
-    // sorted bounce (multi-level scenes, tickets only): position p traces the queue's ray perm[p] (rt_sort.hip) and
-    // stores it to so[2p], so[2p + 1] — the sorted side queue the shade kernel reads; nullptr: no sort
-    const int* perm = nullptr;
-    float4* so = nullptr;
 };
 
 // Material binning of a mixed multi-level scene's bounce (k_bin_materials, after the trace): every hit's queue
@@ -418,8 +414,9 @@ hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, 
 struct SortRaysIO {
     const unsigned* qkey;                                 // ray keys at the queue positions (ray_sort_key, written
                                                           // by the shade kernel that appended the rays)
-    int* perm;                                            // out: sorted position -> queue position (the trace
-                                                          // kernel gathers the rays: TraceIO perm)
+    const float4* ray_in;                                 // the queue's rays (interleaved (o, d) pairs)
+    float4* ray_out;                                      // out: the sorted side queue (same layout, sorted order
+                                                          // in the rewritten shards)
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp;
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin

@@ -1424,18 +1424,15 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
             }
         }
     } else {
-        // Multi-level scenes, sorted bounces: position p's ray is the queue's ray perm[p] (rt_sort.hip), gathered
-        // here into the sorted side queue `so` (coalesced stores) on its way to the traversal
+        // Multi-level scenes: per-wave tickets (sorted bounces read the sorted side queue the last sort pass gathered
+        // the rays into, rt_sort.hip)
         WaveTickets tk(io.ticket, io.q);
         int j, base;
         while (tk.next(j, base)) {
             const int idx = base + lane_id();
             if (idx < tk.len) {
                 const int p = j * io.q.S + idx;
-                const int src = io.perm ? io.perm[p] : p;
-                const float4 o4 = io.rayO[src << io.rsh], d4 = io.rayD[src << io.rsh];
-                if (io.so) { io.so[2 * p] = o4; io.so[2 * p + 1] = d4; }
-                trace_one(p, o4, d4);
+                trace_one(p, io.rayO[p << io.rsh], io.rayD[p << io.rsh]);
             }
         }
     }

@@ -14,9 +14,9 @@
 //                 the same digit with nbits ballots (lane order), the sub-tile's waves are prefixed per digit through
 //                 LDS, and a running count per digit (one digit per thread) carries the order across sub-tiles; the
 //                 tile is then staged in LDS in digit order and stored in runs of consecutive addresses.  The
-//                 first pass reads the keys at the queue positions; the last one writes the queue positions (rays:
-//                 the trace kernel gathers them, TraceIO perm) or the NEE slots (in place) in the sorted queue's
-//                 sharded layout, the sorted order split evenly over the shards.
+//                 first pass reads the keys at the queue positions; the last one gathers the rays themselves into the
+//                 sorted side queue (the trace kernel then reads its rays in order) or writes the NEE slots (in place),
+//                 in the sorted queue's sharded layout, the sorted order split evenly over the shards.
 // Stability matters: within a key, rays keep their slot order, so the shade kernel's per-slot state reads stay
 // close (an unstable atomic counting sort with the same keys measured CFG3 463 -> 375 Msamples/s in round 2).
 #include <algorithm>
@@ -69,7 +69,7 @@ __device__ __forceinline__ int rs_pos(const int* meta, int S, int k) {
 }
 
 enum { SRC_ARRAY = 0, SRC_RAYQ = 1, SRC_NEEQ = 2 };       // where a pass reads (key, value)
-enum { DST_ARRAY = 0, DST_PERM = 1, DST_NEEQ = 2 };       // where it writes them
+enum { DST_ARRAY = 0, DST_RAYS = 1, DST_NEEQ = 2 };       // where it writes them
 
 struct RsPass {
     const int* meta;
@@ -81,11 +81,12 @@ struct RsPass {
     int* hist;                   // kRsBins x kRsGrid (digit-major): counts, then (k_rs_offsets) each block's
                                  // exclusive start within its digit
     int* tot;                    // kRsBins digit totals (k_rs_offsets)
-    // destinations: DST_ARRAY keys_out / vals_out[k']; DST_PERM the values (queue positions) in the sorted queue's
-    // sharded layout (perm: the trace kernel gathers the rays); DST_NEEQ the NEE queue's slots in place; both rewrite
-    // the shard lengths `len`
+    // destinations: DST_ARRAY keys_out / vals_out[k']; DST_RAYS the rays at the values (queue positions), gathered
+    // from ray_in into the sorted side queue ray_out in its sharded layout; DST_NEEQ the NEE queue's slots in place;
+    // both rewrite the shard lengths `len`.  Rays are interleaved (o, d) pairs: ray k at ray_in[2k], ray_in[2k + 1].
     unsigned* keys_out; int* vals_out;
     int* nslot;
+    const float4* ray_in; float4* ray_out;
     int* len;
 };
 
@@ -268,15 +269,41 @@ __global__ void __launch_bounds__(1 << RB) k_rs_scatter(RsPass p) {
             }
         lds_barrier();
         const int tn = min(kRsTile, b1 - t0);
-        for (int l = tid; l < tn; l += kRsThreads) {  // in digit order: consecutive threads, consecutive addresses
-            const unsigned kk = skey[l];
-            const unsigned dg = (kk >> p.shift) & mask;
-            const int d = rstart[dg] + (l - dstart[dg]);
-            if constexpr (DST == DST_ARRAY) {
-                p.keys_out[d] = kk;
-                p.vals_out[d] = sval[l];
-            } else {
-                p.nslot[(d / S2) * p.S + d % S2] = sval[l];
+        if constexpr (DST == DST_RAYS) {
+            // the rays of the tile's items: all the scattered 32-B reads in flight at once, then the stores in digit
+            // order (consecutive threads, consecutive 32-B slots of the sorted queue)
+            float4 ro[kRsIpt], rd[kRsIpt];
+            int q[kRsIpt];
+#pragma unroll
+            for (int j = 0; j < kRsIpt; ++j) {
+                const int l = tid + j * kRsThreads;
+                q[j] = -1;
+                if (l < tn) {
+                    const unsigned dg = (skey[l] >> p.shift) & mask;
+                    const int d = rstart[dg] + (l - dstart[dg]);
+                    const int v = sval[l];
+                    ro[j] = p.ray_in[2 * v];
+                    rd[j] = p.ray_in[2 * v + 1];
+                    q[j] = (d / S2) * p.S + d % S2;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kRsIpt; ++j)
+                if (q[j] >= 0) {
+                    p.ray_out[2 * q[j]] = ro[j];
+                    p.ray_out[2 * q[j] + 1] = rd[j];
+                }
+        } else {
+            for (int l = tid; l < tn; l += kRsThreads) {  // in digit order: consecutive threads, consecutive addresses
+                const unsigned kk = skey[l];
+                const unsigned dg = (kk >> p.shift) & mask;
+                const int d = rstart[dg] + (l - dstart[dg]);
+                if constexpr (DST == DST_ARRAY) {
+                    p.keys_out[d] = kk;
+                    p.vals_out[d] = sval[l];
+                } else {
+                    p.nslot[(d / S2) * p.S + d % S2] = sval[l];
+                }
             }
         }
         lds_barrier();  // (skey / sval / dstart / rstart are rewritten by the next tile)
@@ -326,10 +353,11 @@ hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io) {
     p.meta = p.tot + kRsBinsMax;
     p.S = io.S;
     p.qkey = io.qkey;
-    p.nslot = io.perm;
+    p.ray_in = io.ray_in;
+    p.ray_out = io.ray_out;
     p.len = io.len;
     const int bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
-    return rs_sort<SRC_RAYQ, DST_PERM, RT_RS_RAY_BITS>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
+    return rs_sort<SRC_RAYQ, DST_RAYS, RT_RS_RAY_BITS>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io) {

@@ -2,11 +2,11 @@
 # r04 ab1 on one box: the GPU suite on the default build (all: compact 36-B BVH tiles + any-hit walks on the closest-hit
 # BVH + coalesced radix scatter + 64-B NEE records), then interleaved bench A/Bs of
 #   base  round-3 final build (ed6d035e)
-#   rsc   compact tiles + shared BVH + the LDS-staged (coalesced) radix scatter (+ variant pruning, rt_debug_sort)
 #   all   rsc + the 64-B NEE records + lean mixed-scene camera samples
-#   pk    all + the slab test in packed FMAs (the default build)
+#   pk    all + the slab test in packed FMAs
+#   gat   pk + the last ray-sort pass gathers the rays (the trace reads the sorted queue in order; the default build)
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04ab1_t.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -n 3 gpurun_out/r04ab1_t.log; [ $rc -ne 0 ] && exit $rc
 export RTMI_AB_COMPAT=1
-SETS="cfg4:base,rsc,all,pk,all+RTMI_BVH_ANY=2/4 cfg3:base,rsc,all,pk" ROUNDS=2 bash scripts/gpu_ab_sets.sh
+SETS="cfg4:base,all,pk,gat,gat+RTMI_BVH_ANY=2/4 cfg3:base,all,pk,gat cornell:base,gat" ROUNDS=2 bash scripts/gpu_ab_sets.sh
