@@ -181,6 +181,8 @@ __global__ void __launch_bounds__(1 << RB) k_rs_scatter(RsPass p) {
     __shared__ int wsum[NW];
     const int n = p.meta[0], c = rs_chunk<kRsTile>(n);
     const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
+    if (b0 >= b1 && blockIdx.x != 0) return;  // (no items: a deep bounce's few rays leave most blocks idle; block 0
+                                              // always rewrites the shard lengths)
     const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
     const unsigned mask = (1u << p.nbits) - 1u;
     {  // the digits' starts: exclusive scan of the digit totals (Hillis-Steele over the kRsBins digits, in wpre[0])
