@@ -161,24 +161,27 @@ def single_lane_pass(cfg, world, rank, spp_per_step, steps):
     return st, dt
 
 
-def effective_cpus():
+def effective_cpus(cgroup_root="/sys/fs/cgroup", affinity=None):
     """CPUs this process may actually use: the affinity mask, capped by the cgroup CPU quota (cgroup v2 cpu.max or v1
     cfs_quota_us / cfs_period_us).  os.cpu_count() reports the whole machine (256 on the GPU boxes) although a
     one-GPU box's container gets a share of it."""
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        aff = os.cpu_count() or 1
+    aff = affinity
+    if aff is None:
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            aff = os.cpu_count() or 1
     quota, src = None, "none"
+    root = Path(cgroup_root)
     try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        q, per = (root / "cpu.max").read_text().split()[:2]
         src = f"cgroup v2 cpu.max = {q} {per}"
         if q != "max":
             quota = float(q) / float(per)
     except (OSError, ValueError):
         try:
-            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
-            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            q = int((root / "cpu" / "cpu.cfs_quota_us").read_text())
+            per = int((root / "cpu" / "cpu.cfs_period_us").read_text())
             src = f"cgroup v1 cfs_quota_us = {q}, cfs_period_us = {per}"
             if q > 0:
                 quota = q / per

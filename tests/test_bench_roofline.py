@@ -42,3 +42,19 @@ def test_no_counters_means_no_traffic_fields():
     rl = bench.kernel_rooflines(_stats(), None, "k_path_shadow")
     for v in rl.values():
         assert v.get("traffic") is None and "valu" not in v and "traffic_over_algorithmic" not in v
+
+
+def test_effective_cpus_reads_the_cgroup_quota(tmp_path):
+    """The CPU baseline runs on the CPUs the process may use: the affinity mask capped by the cgroup quota."""
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")  # cgroup v2: 16 CPUs of quota
+    eff, info = bench.effective_cpus(tmp_path, affinity=256)
+    assert eff == 16 and info["cgroup_quota_cpus"] == 16.0 and info["affinity_cpus"] == 256
+    (tmp_path / "cpu.max").write_text("max 100000\n")  # no quota: the affinity mask
+    assert bench.effective_cpus(tmp_path, affinity=64)[0] == 64
+    (tmp_path / "cpu.max").unlink()
+    (tmp_path / "cpu").mkdir()
+    (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("250000\n")  # cgroup v1: 2.5 CPUs -> 2
+    (tmp_path / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert bench.effective_cpus(tmp_path, affinity=8)[0] == 2
+    (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")  # v1 unlimited
+    assert bench.effective_cpus(tmp_path, affinity=8)[0] == 8
