@@ -454,7 +454,13 @@ __device__ __forceinline__ void stage_warp_tables() {
 // RayTracerTestApp.h:305-323: StartPixelSample → SampleVisible(Get1D) → filter.Sample(GetPixel2D) →
 // pixel + .5 + p → PerspectiveCamera::generateRay (Cameras.h:273-297) → Ray::Transform (Shapes.h:37-41).
 // 4 waves/SIMD (158 -> 128 VGPRs, 112 B/lane spill): +3 % on the Cornell box
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
+// PDF: the pdf streams are stored (reference mode; not lean): the lean instantiation holds no pdf[8] registers
+// (103 VGPRs, no spill, against 128 + 28 B spill)
+#ifndef RT_GEN_LEAN_WAVES
+#define RT_GEN_LEAN_WAVES 4
+#endif
+template <bool PDF>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PDF ? 4 : RT_GEN_LEAN_WAVES))) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
                                                      DevFilm film, GenOut out) {
     stage_warp_tables();
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nS; s += gridDim.x * blockDim.x) {
@@ -470,7 +476,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
             float up = u + float(i) / 8;
             if (up > 1) up -= 1;
             lam[i] = sample_visible_wavelength<WarpTab>(up);
-            pdf[i] = out.lean ? 0.f : visible_pdf<WarpTab>(lam[i]);
+            pdf[i] = PDF ? visible_pdf<WarpTab>(lam[i]) : 0.f;
         }
         float u0, u1;
         sm.get_pixel2d(smp, u0, u1);  // Sampler::GetPixel2D (RayTracerTestApp.h:316)
@@ -532,7 +538,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
         // the origin's w carries the path slot (= s for camera rays) through every queue and sort
         out.rayO[s << out.rsh] = make_float4(wo[0], wo[1], wo[2], __int_as_float(s));
         out.rayD[s << out.rsh] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
-        if (!out.lean) store8(out.pdfA, out.pdfB, s, pdf);
+        if (PDF) store8(out.pdfA, out.pdfB, s, pdf);
         if (out.rec.p) {  // path mode: the slot's state
             rstore8(out.rec, s, R_LAM, lam);
             if (out.rec.rng8)
@@ -2434,7 +2440,10 @@ static int resident_grid(F kern, int gb, int grid) {
 
 hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& ids, const DevCamera& cam,
                            const DevSampler& smp, const DevFilm& film, const GenOut& out) {
-    hipLaunchKernelGGL(k_generate, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
+    if (out.lean)
+        hipLaunchKernelGGL(k_generate<false>, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
+    else
+        hipLaunchKernelGGL(k_generate<true>, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
     return hipGetLastError();
 }
 
