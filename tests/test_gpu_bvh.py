@@ -130,3 +130,23 @@ def test_forced_fallback_paths_film_bitexact(oracle_lib, monkeypatch, kind):
     st = g.stats()
     assert st["fallback_rays"] > 0.1 * st["rays"], st
     assert st["shadow_fallback_rays"] > 0.1 * st["shadow_rays"], st
+
+
+@pytest.mark.parametrize("any_bvh", ["shared", "2/4"])
+def test_any_hit_bvh_choice_film_bitexact(oracle_lib, monkeypatch, any_bvh):
+    """The shadow rays walk set 0's closest-hit BVH (the default: one working set) or a BVH of their own
+    (RTMI_BVH_ANY="cost/leaf", round 3's layout): either way the CFG3 and CFG4 films are the oracle's bit for bit, and
+    the exported any-hit BVH is the host build of the same choice."""
+    if any_bvh != "shared":
+        monkeypatch.setenv("RTMI_BVH_ANY", any_bvh)
+    for cfg in (scene.cfg3_blob(res=(40, 24), spp_side=2, max_depth=4),
+                scene.cfg4_mixed(res=(40, 24), spp=(2, 2), frequency=16)):
+        g = Renderer(cfg)
+        a, b = g.bvh(2), build_bvh_host(cfg.model, 2)
+        for k in ("nodes", "tiles", "consts"):
+            assert np.array_equal(bits(a[k]), bits(b[k])), k
+        same = np.array_equal(bits(a["nodes"]), bits(g.bvh(0)["nodes"]))
+        assert same == (any_bvh == "shared")
+        fg = g.render_pass(0, 4)
+        fo = oracle_lib.OracleScene(cfg).render(0, 4)
+        assert np.array_equal(bits(fg), bits(fo))
