@@ -772,7 +772,10 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 // closest-hit waves compact the passing (ray, cluster) pairs (culling every cluster: -2 %).
                 const float4* cl = sc.clusters[set];
                 const int ncl = sc.n_clusters[set];
-                constexpr bool kCompact = !ANYHIT && KZ < 0;  // (shadow rays compacted too: Cornell -7 %)
+#ifndef RT_AB_COMPACT_SHADOW
+#define RT_AB_COMPACT_SHADOW 0
+#endif
+                constexpr bool kCompact = (!ANYHIT || RT_AB_COMPACT_SHADOW) && KZ < 0;  // (shadow rays compacted too: Cornell -7 %, r01)
                 constexpr bool kCull = ANYHIT || KZ >= 0 || kCompact;
                 if (kCull && ncl * kClusterTris >= r.y && ncl <= 32) {
                     const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
