@@ -61,11 +61,13 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=Fa
     (the Cornell scene is 1.8 KB, the CFG3 BVH 1 MB + 4.7 MB of triangles), never an HBM rate.  `traffic` is the
     PMC-measured DRAM bytes per launch and `valu` the SQ_INSTS_VALU per launch over the same single-lane launch time,
     both from profiles/counters_<config>.json when it was measured on the loaded library build."""
-    # Multi-level scenes sort their bounce rays (DESIGN.md §6b); since round 4 the sort's last pass gathers the rays
-    # into the sorted side queue, so the trace kernel reads its rays in queue order either way: the §8(d) 40 B per ray
-    # (round 3 added 36 B per bounce ray for the gather the trace kernel then did)
+    # Multi-level scenes sort their bounce rays (DESIGN.md §6b): the trace kernel reads each bounce ray through the
+    # sort's permutation (4 B index) and writes it to the sorted side queue (32 B) on its way to the traversal —
+    # the sort's data movement, fused into the trace: 36 B per bounce ray on top of the §8(d) 40 B.  (Gathering the
+    # rays in the sort's last pass instead measured CFG3 -7 %, r04: the random reads are exposed there.)
+    gather = 36 * max(0, st["rays"] - st["samples"]) if sorted_bounces else 0
     ks = {
-        "k_trace_closest": (st["ms_trace"], st["launches_trace"], 40 * st["rays"],
+        "k_trace_closest": (st["ms_trace"], st["launches_trace"], 40 * st["rays"] + gather,
                             32 * st["nodes_tested"] + 40 * st["tris_tested"]),
         "k_path_shade": (st["ms_shade"], st["launches_shade"], 312 * st["rays"] + 32 * st["shadow_rays"],
                          32 * st["shadow_nodes_tested"] + 40 * st["shadow_tris_tested"]),

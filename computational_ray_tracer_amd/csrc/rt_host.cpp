@@ -439,7 +439,7 @@ struct Work {
     int* d_qcount = nullptr;   // queue q's counters at [q * kQRegion + kQLen / kQTraceTicket / ...] (rt_internal.h)
     // coherence sort of path queues (multi-level octrees): side queue, radix-sort buffers
     float4 *sO = nullptr, *sD = nullptr;
-    int *sVals = nullptr, *sValsAlt = nullptr;
+    int *sS = nullptr, *sVals = nullptr, *sValsAlt = nullptr;  // sS: the sort permutation (TraceIO perm)
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
     unsigned* sQKey = nullptr;  // the ray queue's sort keys at queue positions (written by the shade kernels)
     void* sTemp = nullptr;      // the sorts' histograms and meta (sort_temp_bytes)
@@ -503,13 +503,14 @@ struct rt_ctx {
     float bvh_node_cost = 3.f; // SAH node cost relative to a triangle test (RTMI_BVH_CI; 1-4 within 1 %)
     int bvh_max_leaf = kBvhMaxLeaf;  // triangles per BVH leaf at most (RTMI_BVH_LEAF)
     int bvh_count[3][2] = {};  // per BVH (set 0, set 1, any-hit): nodes, tiles (rt_bvh_export)
-    // the any-hit walks' BVH: 0 = the closest-hit BVH of set 0 itself (one node + tile working set for both queries,
-    // round 4); RTMI_BVH_ANY="cost/leaf" builds a separate one (round 3: 2/4, which halved the shadow rays' triangle
-    // tests while the closest-hit leaves held 8 triangles)
-    float bvh_any_cost = 0.f;
+    // the any-hit walks' BVH: its own (SAH node cost 2, leaves <= 4), or with RTMI_BVH_ANY="0/4" the closest-hit BVH
+    // of set 0 itself (one working set for both queries).  r04 A/B: the shared BVH made CFG4's NEE stage 7.7 % slower
+    // (30.0 vs 27.9 ms per step): the shadow rays' better tree outweighs the smaller working set
+    float bvh_any_cost = 2.f;
     int bvh_any_leaf = 4;
     int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
     int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
+    int emit_filter = 1;       // RTMI_EMIT_FILTER=0: the last depth of a mixed scene traces every ray (A/B)
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
@@ -618,11 +619,11 @@ int ensure_shadow_workspace(rt_ctx* c, Work& w, size_t n) {
 }
 
 void free_sort_workspace(Work& w) {
-    void* ptrs[] = {w.sO, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sQKey, w.sTemp};  // (sD = sO + 1)
+    void* ptrs[] = {w.sO, w.sS, w.sVals, w.sValsAlt, w.sKeys, w.sKeysAlt, w.sQKey, w.sTemp};  // (sD = sO + 1)
     for (void* p : ptrs)
         if (p) hipFree(p);
     w.sO = w.sD = nullptr;
-    w.sVals = w.sValsAlt = nullptr;
+    w.sS = w.sVals = w.sValsAlt = nullptr;
     w.sKeys = w.sKeysAlt = w.sQKey = nullptr;
     w.sTemp = nullptr;
     w.sCap = 0;
@@ -632,7 +633,7 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
     if (w.sCap >= n) return RT_OK;
     free_sort_workspace(w);
     // the side queue's rays as interleaved (o, d) pairs like the queues' (sD = sO + 1)
-    HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1;
+    HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1; HIPCHK(c, dalloc(&w.sS, n));
     HIPCHK(c, dalloc(&w.sVals, n)); HIPCHK(c, dalloc(&w.sValsAlt, n));
     HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n)); HIPCHK(c, dalloc(&w.sQKey, n));
     HIPCHK(c, hipMalloc(&w.sTemp, sort_temp_bytes()));
@@ -751,7 +752,7 @@ hipEvent_t ev_start(rt_ctx* c, hipStream_t st) {
     hipEventRecord(a, st);
     return a;
 }
-enum { ST_GEN = 0, ST_TRACE, ST_SHADE, ST_SHADOW, ST_FILM, ST_SORT };
+enum { ST_GEN = 0, ST_TRACE, ST_SHADE, ST_SHADOW, ST_FILM, ST_SORT, ST_FILTER };
 
 void harvest(rt_ctx* c) {
     for (auto& e : c->pending) {
@@ -764,6 +765,7 @@ void harvest(rt_ctx* c) {
             case ST_SHADE: c->stats.ms_shade += ms; c->stats.launches_shade += 1; break;
             case ST_SHADOW: c->stats.ms_shadow += ms; break;
             case ST_SORT: c->stats.ms_sort += ms; break;
+            case ST_FILTER: c->stats.ms_trace += ms; break;  // (the last depth's emitter filter: no trace launch)
             default: c->stats.ms_film += ms; break;
         }
         c->pool.push_back(e.a);
@@ -1174,21 +1176,36 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 // multi-level octrees: bounce rays sorted by (octant, direction cell, origin Morton code) before
                 // the trace.  The queue length is read back so only live rays are sorted (sorting the capacity with
                 // padded keys instead, without the host read: -0.6 %); the other lane keeps the GPU busy meanwhile.
-                const QueueView qv = depth == 0 ? QueueView{nullptr, Sq[l], nSq[l], nsh}
-                                                : QueueView{qc_cur + kQLen, Sq[l], 0, nsh};
+                QueueView qv = depth == 0 ? QueueView{nullptr, Sq[l], nSq[l], nsh}
+                                          : QueueView{qc_cur + kQLen, Sq[l], 0, nsh};
                 const DevScene dsl = lane_scene(c, w);
+                // the last depth of a mixed scene: only emitter hits still add to L, so the rays that hit no emissive
+                // surface are dropped first (k_emitter_filter, EmitIO) into the free next queue, whose rays the trace
+                // and shade kernels then take (the shade appends nothing at this depth); no coherence sort
+                const bool efilter = c->emit_filter && c->dsc.full && depth == c->integ.max_depth && depth > 0 &&
+                                     c->dsc.n_emit_tris >= 0;
+                if (efilter) {
+                    const EmitIO eio{qv, cO, w.rayO + 2 * (size_t)nxt * qs, qc_nxt + kQLen};
+                    e0 = ev_start(c, s);
+                    HIPCHK(c, launch_emitter_filter(s, grid, dsl, eio));
+                    ev_mark(c, s, ST_FILTER, e0);
+                    cO = eio.nO;
+                    cD = cO + 1;
+                    qv = QueueView{qc_nxt + kQLen, Sq[l], 0, nsh};
+                }
                 TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
                 BinIO bio{qv, w.hitPrim, {w.neeSlot + 3 * ncap, w.neeSlot + 4 * ncap}, qc_cur + kQBinLen};
                 if (depth == 0) { bio.rayO = cO; bio.rec = rv; }  // lean depth 0: the misses' L = 0 (BinIO)
                 static_assert(kMatClasses == 2, "bin index lists");
-                if (sort_rays && depth > 0) {  // the device reads the queue length itself: no host round trip
-                    SortRaysIO so{w.sQKey, cO, w.sO, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
+                if (sort_rays && depth > 0 && !efilter) {  // the device reads the queue length itself: no host read
+                    SortRaysIO so{w.sQKey, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
                                   c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l]};
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, so));
                     ev_mark(c, s, ST_SORT, e0);
-                    cO = w.sO; cD = w.sD;  // the last sort pass gathered the rays into the sorted side queue
-                    tio.rayO = cO; tio.rayD = cD;
+                    tio.perm = w.sS;  // the trace kernel gathers the sorted rays into the side queue
+                    tio.so = w.sO;
+                    cO = w.sO; cD = w.sD;
                 }
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
@@ -1565,6 +1582,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     }
     if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
+    if (const char* e = std::getenv("RTMI_EMIT_FILTER")) c->emit_filter = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) {
         int db = 3, ob = 4, om = -1;
         const int got = std::sscanf(e, "%d/%d/%d", &db, &ob, &om);
@@ -2078,6 +2096,20 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     }
     d.n_lights = s->n_lights;
     if (s->n_lights >= 1) d.light0 = lights[0];
+    // the emissive surfaces, for the last depth's emitter filter (EmitIO): non-degenerate triangles and shapes whose
+    // material emits; more than kMaxEmitTris emissive triangles turn the filter off
+    std::vector<int> etris, eshapes;
+    for (int t = 0; t < nt; ++t)
+        if (!degen[t] && mats[tm[t]].emit > 0) etris.push_back(t);
+    for (int i = 0; i < s->n_shapes; ++i)
+        if (mats[shapes[i].material].emit > 0) eshapes.push_back(i);
+    void *pet = nullptr, *pes = nullptr;
+    if ((rc = up(etris.data(), etris.size() * 4, &pet)) || (rc = up(eshapes.data(), eshapes.size() * 4, &pes)))
+        return rc;
+    d.emit_tris = (const int*)pet;
+    d.n_emit_tris = (int)etris.size() <= kMaxEmitTris ? (int)etris.size() : -1;
+    d.emit_shapes = (const int*)pes;
+    d.n_emit_shapes = (int)eshapes.size();
     c->have_scene = true;
     return RT_OK;
 }
@@ -2324,12 +2356,11 @@ static int impl_rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes
     int leaf = kBvhMaxLeaf;
     if (const char* e = std::getenv("RTMI_BVH_CI")) cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_BVH_LEAF")) leaf = std::max(1, std::min(15, std::atoi(e)));
-    if (set == kBvhAny) {  // rt_create's default (set 0's closest-hit BVH) / RTMI_BVH_ANY for the any-hit BVH
-        if (const char* e = std::getenv("RTMI_BVH_ANY")) {
-            float ac = 0.f;
-            int al = 4;
-            if (std::sscanf(e, "%f/%d", &ac, &al) == 2 && ac > 0) { cost = ac; leaf = std::max(1, std::min(15, al)); }
-        }
+    if (set == kBvhAny) {  // rt_create's default (cost 2, leaves <= 4) / RTMI_BVH_ANY ("0/..": set 0's closest-hit BVH)
+        float ac = 2.f;
+        int al = 4;
+        if (const char* e = std::getenv("RTMI_BVH_ANY")) std::sscanf(e, "%f/%d", &ac, &al);
+        if (ac > 0) { cost = ac; leaf = std::max(1, std::min(15, al)); }
     }
     SceneWorld sw;
     scene_world(s, sw);
@@ -2423,7 +2454,6 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
     const size_t cap = (size_t)kShards * S;
     unsigned *dkey = nullptr, *k0 = nullptr, *k1 = nullptr;
     int *dslot = nullptr, *dlen = nullptr, *dout = nullptr, *v0 = nullptr, *v1 = nullptr;
-    float4 *rin = nullptr, *rout = nullptr;  // rays: the queue position rides in the origin's w
     void* temp = nullptr;
     if (dalloc(&dkey, cap) || dalloc(&dslot, cap) || dalloc(&dlen, (size_t)kShards * kQStride) || dalloc(&dout, cap) ||
         dalloc(&k0, cap) || dalloc(&k1, cap) || dalloc(&v0, cap) || dalloc(&v1, cap) ||
@@ -2438,31 +2468,10 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
         if (e == hipSuccess) e = hipMemcpy(dslot, hs.data(), cap * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(dlen, hlen.data(), hlen.size() * 4, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemset(dout, 0xff, cap * 4);
-        if (e == hipSuccess && which == 0) {
-            if (dalloc(&rin, 2 * cap) || dalloc(&rout, 2 * cap)) e = hipErrorOutOfMemory;
-            std::vector<float4> hr(2 * cap, make_float4(0.f, 0.f, 0.f, 0.f));
-            for (size_t i = 0; i < cap; ++i) {
-                std::memcpy(&hr[2 * i].w, &i, 4);
-                hr[2 * i + 1].x = (float)i;  // (the direction travels too)
-            }
-            if (e == hipSuccess) e = hipMemcpy(rin, hr.data(), hr.size() * 16, hipMemcpyHostToDevice);
-            if (e == hipSuccess) e = hipMemset(rout, 0xff, 2 * cap * 16);
-        }
         if (e == hipSuccess) {
             if (which == 0) {
-                SortRaysIO so{dkey, rin, rout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S};
+                SortRaysIO so{dkey, dout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S};
                 e = launch_sort_rays(c->stream, so);
-                if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-                if (e == hipSuccess) {  // out[pos'] = the origin's w (the queue position), -1 where nothing landed;
-                    std::vector<float4> hr(2 * cap);  // a direction that did not travel with its origin is an error
-                    e = hipMemcpy(hr.data(), rout, hr.size() * 16, hipMemcpyDeviceToHost);
-                    std::vector<int> ho(cap);
-                    for (size_t i = 0; i < cap && e == hipSuccess; ++i) {
-                        std::memcpy(&ho[i], &hr[2 * i].w, 4);
-                        if (ho[i] != -1 && hr[2 * i + 1].x != (float)ho[i]) ho[i] = -2;
-                    }
-                    if (e == hipSuccess) e = hipMemcpy(dout, ho.data(), cap * 4, hipMemcpyHostToDevice);
-                }
             } else {
                 SortNeeIO so{dslot, dlen, S, dkey, k0, k1, v0, v1, temp, bits_a};
                 e = launch_sort_nee(c->stream, so);
@@ -2475,7 +2484,6 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
         else
             for (int j = 0; j < kShards; ++j) out_len[j] = hlen[(size_t)j * kQStride];
     }
-    hipFree(rin); hipFree(rout);
     hipFree(dkey); hipFree(dslot); hipFree(dlen); hipFree(dout);
     hipFree(k0); hipFree(k1); hipFree(v0); hipFree(v1); hipFree(temp);
     if (!rc) rc = mark_done(c, c->stream);

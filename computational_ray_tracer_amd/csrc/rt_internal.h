@@ -146,7 +146,14 @@ struct DevScene {
                                     // padding covers the slab test's rounding only for origins inside 8 M)
     unsigned amb_mask;              // test knob (RTMI_FORCE_AMB=k): with amb_force set, rays whose direction-bit hash
     int amb_force;                  // has its low k bits zero are declared ambiguous (exercises every fallback path)
+    // the emissive surfaces (material emit > 0): non-degenerate triangle ids and shape indices, for the last depth's
+    // emitter filter (k_emitter_filter); n_emit_tris < 0: too many emissive triangles, no filter
+    const int* emit_tris;
+    int n_emit_tris;
+    const int* emit_shapes;
+    int n_emit_shapes;
 };
+static const int kMaxEmitTris = 64;  // emitter filter only with at most this many emissive triangles
 
 // device counter slots (u64).  Every wave of a persistent kernel adds its totals at the end, all at about the same
 // time: one counter word per slot serialised those atomics (a fixed ~0.15 ms tail per trace launch), so each slot
@@ -270,6 +277,10 @@ struct TraceIO {
     int* hitPrim;
     int* ticket = nullptr;    // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
     int rsh = 0;              // ray k at rayO[k << rsh] (1: the workspace's interleaved (o, d) pairs; 0: caller arrays)
+    // sorted bounce (multi-level scenes, tickets only): position p traces the queue's ray perm[p] (rt_sort.hip) and
+    // stores it to so[2p], so[2p + 1] — the sorted side queue the shade kernel reads; nullptr: no sort
+    const int* perm = nullptr;
+    float4* so = nullptr;
 };
 
 // Material binning of a mixed multi-level scene's bounce (k_bin_materials, after the trace): every hit's queue
@@ -286,6 +297,18 @@ struct BinIO {
     RecView rec{};
 };
 hipError_t launch_bin_materials(hipStream_t st, int grid, const DevScene& sc, const BinIO& io);
+
+// The last depth of a mixed scene (depth == max_depth > 0): only hits on an emitter still add to L, so the rays that
+// hit no emissive surface at all — each emitter tested alone with tMax = FLT_MAX, a test the closest-hit traversal's
+// own test of that surface can only pass if this one does (both are monotone in tMax) — are dropped before the trace
+// (k_emitter_filter).  The others are appended, shard by shard, to the output queue (interleaved (o, d) pairs).
+struct EmitIO {
+    QueueView q;              // the depth's queue
+    const float4* rayO;       // its rays: ray k at rayO[2k], rayO[2k + 1]
+    float4* nO;               // the filtered queue (same shard stride), lengths at nCount + j kQStride (zeroed)
+    int* nCount;
+};
+hipError_t launch_emitter_filter(hipStream_t st, int grid, const DevScene& sc, const EmitIO& io);
 
 struct ShadeRefIO {
     const int* work_pixels; int n_pixels; int n_index;
@@ -414,9 +437,8 @@ hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, 
 struct SortRaysIO {
     const unsigned* qkey;                                 // ray keys at the queue positions (ray_sort_key, written
                                                           // by the shade kernel that appended the rays)
-    const float4* ray_in;                                 // the queue's rays (interleaved (o, d) pairs)
-    float4* ray_out;                                      // out: the sorted side queue (same layout, sorted order
-                                                          // in the rewritten shards)
+    int* perm;                                            // out: sorted position -> queue position (the trace
+                                                          // kernel gathers the rays: TraceIO perm)
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp;
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin

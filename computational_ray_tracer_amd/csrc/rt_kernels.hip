@@ -772,10 +772,8 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 // closest-hit waves compact the passing (ray, cluster) pairs (culling every cluster: -2 %).
                 const float4* cl = sc.clusters[set];
                 const int ncl = sc.n_clusters[set];
-#ifndef RT_AB_COMPACT_SHADOW
-#define RT_AB_COMPACT_SHADOW 0
-#endif
-                constexpr bool kCompact = (!ANYHIT || RT_AB_COMPACT_SHADOW) && KZ < 0;  // (shadow rays compacted too: Cornell -7 %, r01)
+                // (shadow rays compacted too: Cornell -7 % in r01, -6.5 % in r04)
+                constexpr bool kCompact = !ANYHIT && KZ < 0;
                 constexpr bool kCull = ANYHIT || KZ >= 0 || kCompact;
                 if (kCull && ncl * kClusterTris >= r.y && ncl <= 32) {
                     const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
@@ -1433,15 +1431,18 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
             }
         }
     } else {
-        // Multi-level scenes: per-wave tickets (sorted bounces read the sorted side queue the last sort pass gathered
-        // the rays into, rt_sort.hip)
+        // Multi-level scenes, sorted bounces: position p's ray is the queue's ray perm[p] (rt_sort.hip), gathered
+        // here into the sorted side queue `so` (coalesced stores) on its way to the traversal
         WaveTickets tk(io.ticket, io.q);
         int j, base;
         while (tk.next(j, base)) {
             const int idx = base + lane_id();
             if (idx < tk.len) {
                 const int p = j * io.q.S + idx;
-                trace_one(p, io.rayO[p << io.rsh], io.rayD[p << io.rsh]);
+                const int src = io.perm ? io.perm[p] : p;
+                const float4 o4 = io.rayO[src << io.rsh], d4 = io.rayD[src << io.rsh];
+                if (io.so) { io.so[2 * p] = o4; io.so[2 * p + 1] = d4; }
+                trace_one(p, o4, d4);
             }
         }
     }
@@ -1517,6 +1518,47 @@ __global__ void __launch_bounds__(kBlock) k_bin_materials(DevScene sc, BinIO io)
                     io.idx[c][j * io.q.S + base[c] + wc[c][r][w] + __popcll(m & lt)] = j * io.q.S + c0 + r * kBlock + (int)threadIdx.x;
             }
         __syncthreads();  // (wc / base are rewritten by the block's next chunk)
+    }
+}
+
+// The last depth's emitter filter (EmitIO, rt_internal.h): a ray is kept when some emissive triangle passes the
+// watertight test (Shapes.h:1101-1260) or some emissive shape its intersection test, each with tMax = FLT_MAX.  The
+// closest-hit traversal can only return an emitter whose own test passed with a smaller tMax, and both tests are
+// monotone in tMax, so a dropped ray's closest hit is never an emitter: the shade kernel would have added nothing.
+__global__ void __launch_bounds__(kBlock) k_emitter_filter(DevScene sc, EmitIO io) {
+    __shared__ int lds[kBlock / 64 + 1];
+    QueueItems<false> items(nullptr, io.q);
+    int qj, qidx;
+    bool live;
+    while (items.next(qj, qidx, live)) {
+        const int k = qj * io.q.S + qidx;
+        float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = o4;
+        bool keep = false;
+        if (live) {
+            o4 = io.rayO[2 * k];
+            d4 = io.rayO[2 * k + 1];
+            const V3 o = v3(o4.x, o4.y, o4.z), d = v3(d4.x, d4.y, d4.z);
+            const TriRay R = make_triray<-1>(o, d);
+            for (int e = 0; e < sc.n_emit_tris && !keep; ++e) {
+                const int t = sc.emit_tris[e];
+                const float4 P0 = sc.triWorld[3 * t], P1 = sc.triWorld[3 * t + 1], P2 = sc.triWorld[3 * t + 2];
+                float b0, b1, b2, tt;
+                keep = tri_intersect<-1>(R, 3.402823466e+38f, make_float4(P0.x, P0.y, P0.z, P1.x),
+                                         make_float4(P1.y, P1.z, P2.x, P2.y), make_float4(P2.z, 0.f, 0.f, 0.f), b0, b1,
+                                         b2, tt);
+            }
+            for (int e = 0; e < sc.n_emit_shapes && !keep; ++e) {
+                const DevShape sh = ldconst(sc.shapes, sc.emit_shapes[e]);
+                V3 ph;
+                float th;
+                keep = shape_isect(sh, o, d, 3.402823466e+38f, ph, th);
+            }
+        }
+        const int p = block_append(io.nCount + qj * kQStride, keep, lds) + qj * io.q.S;
+        if (keep) {
+            io.nO[2 * p] = o4;
+            io.nO[2 * p + 1] = d4;
+        }
     }
 }
 
@@ -2439,6 +2481,13 @@ static int resident_grid(F kern, int gb, int grid) {
         if (res > 0 && gb > res) gb = res;
     }
     return gb;
+}
+
+hipError_t launch_emitter_filter(hipStream_t st, int grid, const DevScene& sc, const EmitIO& io) {
+    if (sc.n_emit_tris < 0 || sc.n_emit_tris > kMaxEmitTris) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_emitter_filter, dim3(grid_for(io.q.n ? io.q.n : grid * kBlock, grid)), dim3(kBlock), 0, st,
+                       sc, io);
+    return hipGetLastError();
 }
 
 hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& ids, const DevCamera& cam,

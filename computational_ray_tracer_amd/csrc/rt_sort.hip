@@ -14,9 +14,9 @@
 //                 the same digit with nbits ballots (lane order), the sub-tile's waves are prefixed per digit through
 //                 LDS, and a running count per digit (one digit per thread) carries the order across sub-tiles; the
 //                 tile is then staged in LDS in digit order and stored in runs of consecutive addresses.  The
-//                 first pass reads the keys at the queue positions; the last one gathers the rays themselves into the
-//                 sorted side queue (the trace kernel then reads its rays in order) or writes the NEE slots (in place),
-//                 in the sorted queue's sharded layout, the sorted order split evenly over the shards.
+//                 first pass reads the keys at the queue positions; the last one writes the queue positions (rays:
+//                 the trace kernel gathers them, TraceIO perm) or the NEE slots (in place) in the sorted queue's
+//                 sharded layout, the sorted order split evenly over the shards.
 // Stability matters: within a key, rays keep their slot order, so the shade kernel's per-slot state reads stay
 // close (an unstable atomic counting sort with the same keys measured CFG3 463 -> 375 Msamples/s in round 2).
 #include <algorithm>
@@ -36,7 +36,10 @@ namespace {
 #define RT_RS_NEE_BITS 8
 #endif
 constexpr int kRsGrid = 1024;  // blocks of the histogram / scatter kernels (4 per CU)
-constexpr int kRsIpt = 8;      // items per thread of a scatter tile (tiles of kRsIpt x 2^RB items)
+#ifndef RT_AB_RS_OLD
+#define RT_AB_RS_OLD 0
+#endif
+constexpr int kRsIpt = RT_AB_RS_OLD ? 1 : 8;  // items per thread of a scatter tile (tiles of kRsIpt x 2^RB items)
 constexpr int kRsBinsMax = 512;
 
 // meta: [0] n, [1 .. kShards + 1] the exclusive prefix of the shard lengths
@@ -69,7 +72,7 @@ __device__ __forceinline__ int rs_pos(const int* meta, int S, int k) {
 }
 
 enum { SRC_ARRAY = 0, SRC_RAYQ = 1, SRC_NEEQ = 2 };       // where a pass reads (key, value)
-enum { DST_ARRAY = 0, DST_RAYS = 1, DST_NEEQ = 2 };       // where it writes them
+enum { DST_ARRAY = 0, DST_PERM = 1, DST_NEEQ = 2 };       // where it writes them
 
 struct RsPass {
     const int* meta;
@@ -81,12 +84,11 @@ struct RsPass {
     int* hist;                   // kRsBins x kRsGrid (digit-major): counts, then (k_rs_offsets) each block's
                                  // exclusive start within its digit
     int* tot;                    // kRsBins digit totals (k_rs_offsets)
-    // destinations: DST_ARRAY keys_out / vals_out[k']; DST_RAYS the rays at the values (queue positions), gathered
-    // from ray_in into the sorted side queue ray_out in its sharded layout; DST_NEEQ the NEE queue's slots in place;
-    // both rewrite the shard lengths `len`.  Rays are interleaved (o, d) pairs: ray k at ray_in[2k], ray_in[2k + 1].
+    // destinations: DST_ARRAY keys_out / vals_out[k']; DST_PERM the values (queue positions) in the sorted queue's
+    // sharded layout (perm: the trace kernel gathers the rays); DST_NEEQ the NEE queue's slots in place; both rewrite
+    // the shard lengths `len`
     unsigned* keys_out; int* vals_out;
     int* nslot;
-    const float4* ray_in; float4* ray_out;
     int* len;
 };
 
@@ -271,44 +273,96 @@ __global__ void __launch_bounds__(1 << RB) k_rs_scatter(RsPass p) {
             }
         lds_barrier();
         const int tn = min(kRsTile, b1 - t0);
-        if constexpr (DST == DST_RAYS) {
-            // the rays of the tile's items: all the scattered 32-B reads in flight at once, then the stores in digit
-            // order (consecutive threads, consecutive 32-B slots of the sorted queue)
-            float4 ro[kRsIpt], rd[kRsIpt];
-            int q[kRsIpt];
-#pragma unroll
-            for (int j = 0; j < kRsIpt; ++j) {
-                const int l = tid + j * kRsThreads;
-                q[j] = -1;
-                if (l < tn) {
-                    const unsigned dg = (skey[l] >> p.shift) & mask;
-                    const int d = rstart[dg] + (l - dstart[dg]);
-                    const int v = sval[l];
-                    ro[j] = p.ray_in[2 * v];
-                    rd[j] = p.ray_in[2 * v + 1];
-                    q[j] = (d / S2) * p.S + d % S2;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < kRsIpt; ++j)
-                if (q[j] >= 0) {
-                    p.ray_out[2 * q[j]] = ro[j];
-                    p.ray_out[2 * q[j] + 1] = rd[j];
-                }
-        } else {
-            for (int l = tid; l < tn; l += kRsThreads) {  // in digit order: consecutive threads, consecutive addresses
-                const unsigned kk = skey[l];
-                const unsigned dg = (kk >> p.shift) & mask;
-                const int d = rstart[dg] + (l - dstart[dg]);
-                if constexpr (DST == DST_ARRAY) {
-                    p.keys_out[d] = kk;
-                    p.vals_out[d] = sval[l];
-                } else {
-                    p.nslot[(d / S2) * p.S + d % S2] = sval[l];
-                }
+        for (int l = tid; l < tn; l += kRsThreads) {  // in digit order: consecutive threads, consecutive addresses
+            const unsigned kk = skey[l];
+            const unsigned dg = (kk >> p.shift) & mask;
+            const int d = rstart[dg] + (l - dstart[dg]);
+            if constexpr (DST == DST_ARRAY) {
+                p.keys_out[d] = kk;
+                p.vals_out[d] = sval[l];
+            } else {
+                p.nslot[(d / S2) * p.S + d % S2] = sval[l];
             }
         }
         lds_barrier();  // (skey / sval / dstart / rstart are rewritten by the next tile)
+    }
+}
+
+// (A/B: round 3's scatter, tiles of one item per thread, scattered stores; RT_AB_RS_OLD=1)
+template <int SRC, int DST, int RB>
+__global__ void __launch_bounds__(1 << RB) k_rs_scatter_r3(RsPass p) {
+    constexpr int kRsBins = 1 << RB, kRsThreads = kRsBins, kRsTile = kRsThreads;
+    constexpr int NW = kRsThreads / 64;
+    __shared__ int wcnt[NW][kRsBins];
+    __shared__ int wpre[NW][kRsBins];
+    const int n = p.meta[0], c = rs_chunk<kRsTile>(n);
+    const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
+    const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
+    const unsigned mask = (1u << p.nbits) - 1u;
+    {  // the digits' starts: exclusive scan of the digit totals (Hillis-Steele over the kRsBins digits, in wpre[0])
+        int* sc = wpre[0];
+        sc[tid] = p.tot[tid];
+        __syncthreads();
+        for (int off = 1; off < kRsBins; off <<= 1) {
+            const int y = tid >= off ? sc[tid - off] : 0;
+            __syncthreads();
+            sc[tid] += y;
+            __syncthreads();
+        }
+    }
+    // this thread's digit (tid): next output index
+    int run = wpre[0][tid] - p.tot[tid] + p.hist[tid * kRsGrid + blockIdx.x];
+    __syncthreads();
+    const int S2 = shard_stride(n, kShards);      // the sorted queue: item k' at shard k' / S2
+    if (DST != DST_ARRAY && blockIdx.x == 0 && tid < kShards) {
+        const int cc = n - tid * S2;
+        p.len[tid * kQStride] = cc < 0 ? 0 : (cc > S2 ? S2 : cc);
+    }
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // software-pipelined over the tiles: tile t + 1's (key, value) are loaded before tile t's ranking, whose
+    // barriers wait for LDS only (lds_barrier)
+    unsigned key_n = 0;
+    int val_n = 0;
+    if (b0 + tid < b1) rs_load<SRC>(p, b0 + tid, key_n, val_n);
+    for (int t0 = b0; t0 < b1; t0 += kRsTile) {  // (block-uniform trip count)
+        const int k = t0 + tid;
+        const bool valid = k < b1;
+        const unsigned key = key_n;
+        const int val = val_n;
+        if (k + kRsTile < b1) rs_load<SRC>(p, k + kRsTile, key_n, val_n);
+        const unsigned dg = (key >> p.shift) & mask;
+        // lanes of this wave with the same digit: AND over the digit's bits of (ballot of the bit, or its complement)
+        uint64_t m = __ballot(valid);
+        for (int bit = 0; bit < p.nbits; ++bit) {
+            const uint64_t bb = __ballot((dg >> bit) & 1u);
+            m &= ((dg >> bit) & 1u) ? bb : ~bb;
+        }
+        const int rank = __popcll(m & lt);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) wcnt[i][tid] = 0;
+        lds_barrier();
+        if (valid && rank == 0) wcnt[w][dg] = __popcll(m);  // the digit's lowest lane reports the wave's count
+        lds_barrier();
+        {  // digit tid: prefix over the tile's waves, then carry the running count
+            int r = run;
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                wpre[i][tid] = r;
+                r += wcnt[i][tid];
+            }
+            run = r;
+        }
+        lds_barrier();
+        if (valid) {
+            const int dst = wpre[w][dg] + rank;
+            if constexpr (DST == DST_ARRAY) {
+                p.keys_out[dst] = key;
+                p.vals_out[dst] = val;
+            } else {
+                p.nslot[(dst / S2) * p.S + dst % S2] = val;
+            }
+        }
+        // (wcnt / wpre are rewritten only after the next tile's first barrier)
     }
 }
 
@@ -316,7 +370,11 @@ template <int SRC, int DST, int RB>
 void rs_launch(hipStream_t st, const RsPass& p) {
     hipLaunchKernelGGL((k_rs_hist<SRC, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
     hipLaunchKernelGGL(k_rs_offsets, dim3(1 << RB), dim3(kRsGrid), 0, st, p.hist, p.tot);
+#if RT_AB_RS_OLD
+    hipLaunchKernelGGL((k_rs_scatter_r3<SRC, DST, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
+#else
     hipLaunchKernelGGL((k_rs_scatter<SRC, DST, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
+#endif
 }
 
 // the passes of a `bits`-bit key, <= RB bits each (split evenly), ping-ponging between the two arrays
@@ -355,11 +413,10 @@ hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io) {
     p.meta = p.tot + kRsBinsMax;
     p.S = io.S;
     p.qkey = io.qkey;
-    p.ray_in = io.ray_in;
-    p.ray_out = io.ray_out;
+    p.nslot = io.perm;
     p.len = io.len;
     const int bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
-    return rs_sort<SRC_RAYQ, DST_RAYS, RT_RS_RAY_BITS>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
+    return rs_sort<SRC_RAYQ, DST_PERM, RT_RS_RAY_BITS>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io) {

@@ -132,12 +132,12 @@ def test_forced_fallback_paths_film_bitexact(oracle_lib, monkeypatch, kind):
     assert st["shadow_fallback_rays"] > 0.1 * st["shadow_rays"], st
 
 
-@pytest.mark.parametrize("any_bvh", ["shared", "2/4"])
+@pytest.mark.parametrize("any_bvh", ["0/4", "default"])
 def test_any_hit_bvh_choice_film_bitexact(oracle_lib, monkeypatch, any_bvh):
-    """The shadow rays walk set 0's closest-hit BVH (the default: one working set) or a BVH of their own
-    (RTMI_BVH_ANY="cost/leaf", round 3's layout): either way the CFG3 and CFG4 films are the oracle's bit for bit, and
-    the exported any-hit BVH is the host build of the same choice."""
-    if any_bvh != "shared":
+    """The shadow rays walk a BVH of their own (the default: SAH node cost 2, leaves <= 4) or set 0's closest-hit
+    BVH (RTMI_BVH_ANY="0/4": one working set for both queries): either way the CFG3 and CFG4 films are the oracle's bit
+    for bit, and the exported any-hit BVH is the host build of the same choice."""
+    if any_bvh != "default":
         monkeypatch.setenv("RTMI_BVH_ANY", any_bvh)
     for cfg in (scene.cfg3_blob(res=(40, 24), spp_side=2, max_depth=4),
                 scene.cfg4_mixed(res=(40, 24), spp=(2, 2), frequency=16)):
@@ -146,7 +146,7 @@ def test_any_hit_bvh_choice_film_bitexact(oracle_lib, monkeypatch, any_bvh):
         for k in ("nodes", "tiles", "consts"):
             assert np.array_equal(bits(a[k]), bits(b[k])), k
         same = np.array_equal(bits(a["nodes"]), bits(g.bvh(0)["nodes"]))
-        assert same == (any_bvh == "shared")
+        assert same == (any_bvh == "0/4")
         fg = g.render_pass(0, 4)
         fo = oracle_lib.OracleScene(cfg).render(0, 4)
         assert np.array_equal(bits(fg), bits(fo))
