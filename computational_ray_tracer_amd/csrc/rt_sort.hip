@@ -36,10 +36,10 @@ namespace {
 #define RT_RS_NEE_BITS 8
 #endif
 constexpr int kRsGrid = 1024;  // blocks of the histogram / scatter kernels (4 per CU)
-#ifndef RT_AB_RS_OLD
-#define RT_AB_RS_OLD 0
-#endif
-constexpr int kRsIpt = RT_AB_RS_OLD ? 1 : 8;  // items per thread of a scatter tile (tiles of kRsIpt x 2^RB items)
+// items per thread of a scatter tile (tiles of kRsIpt x 2^RB items); r04 A/B against round 3's tiles of one item per
+// thread with scattered stores: the same time (CFG3 1.93 vs 2.03 ms, CFG4 5.11 vs 5.08 ms of sort per step), fewer
+// bytes written
+constexpr int kRsIpt = 8;
 constexpr int kRsBinsMax = 512;
 
 // meta: [0] n, [1 .. kShards + 1] the exclusive prefix of the shard lengths
@@ -288,93 +288,11 @@ __global__ void __launch_bounds__(1 << RB) k_rs_scatter(RsPass p) {
     }
 }
 
-// (A/B: round 3's scatter, tiles of one item per thread, scattered stores; RT_AB_RS_OLD=1)
-template <int SRC, int DST, int RB>
-__global__ void __launch_bounds__(1 << RB) k_rs_scatter_r3(RsPass p) {
-    constexpr int kRsBins = 1 << RB, kRsThreads = kRsBins, kRsTile = kRsThreads;
-    constexpr int NW = kRsThreads / 64;
-    __shared__ int wcnt[NW][kRsBins];
-    __shared__ int wpre[NW][kRsBins];
-    const int n = p.meta[0], c = rs_chunk<kRsTile>(n);
-    const int b0 = (int)blockIdx.x * c, b1 = min(b0 + c, n);
-    const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
-    const unsigned mask = (1u << p.nbits) - 1u;
-    {  // the digits' starts: exclusive scan of the digit totals (Hillis-Steele over the kRsBins digits, in wpre[0])
-        int* sc = wpre[0];
-        sc[tid] = p.tot[tid];
-        __syncthreads();
-        for (int off = 1; off < kRsBins; off <<= 1) {
-            const int y = tid >= off ? sc[tid - off] : 0;
-            __syncthreads();
-            sc[tid] += y;
-            __syncthreads();
-        }
-    }
-    // this thread's digit (tid): next output index
-    int run = wpre[0][tid] - p.tot[tid] + p.hist[tid * kRsGrid + blockIdx.x];
-    __syncthreads();
-    const int S2 = shard_stride(n, kShards);      // the sorted queue: item k' at shard k' / S2
-    if (DST != DST_ARRAY && blockIdx.x == 0 && tid < kShards) {
-        const int cc = n - tid * S2;
-        p.len[tid * kQStride] = cc < 0 ? 0 : (cc > S2 ? S2 : cc);
-    }
-    const uint64_t lt = (1ull << lane) - 1ull;
-    // software-pipelined over the tiles: tile t + 1's (key, value) are loaded before tile t's ranking, whose
-    // barriers wait for LDS only (lds_barrier)
-    unsigned key_n = 0;
-    int val_n = 0;
-    if (b0 + tid < b1) rs_load<SRC>(p, b0 + tid, key_n, val_n);
-    for (int t0 = b0; t0 < b1; t0 += kRsTile) {  // (block-uniform trip count)
-        const int k = t0 + tid;
-        const bool valid = k < b1;
-        const unsigned key = key_n;
-        const int val = val_n;
-        if (k + kRsTile < b1) rs_load<SRC>(p, k + kRsTile, key_n, val_n);
-        const unsigned dg = (key >> p.shift) & mask;
-        // lanes of this wave with the same digit: AND over the digit's bits of (ballot of the bit, or its complement)
-        uint64_t m = __ballot(valid);
-        for (int bit = 0; bit < p.nbits; ++bit) {
-            const uint64_t bb = __ballot((dg >> bit) & 1u);
-            m &= ((dg >> bit) & 1u) ? bb : ~bb;
-        }
-        const int rank = __popcll(m & lt);
-#pragma unroll
-        for (int i = 0; i < NW; ++i) wcnt[i][tid] = 0;
-        lds_barrier();
-        if (valid && rank == 0) wcnt[w][dg] = __popcll(m);  // the digit's lowest lane reports the wave's count
-        lds_barrier();
-        {  // digit tid: prefix over the tile's waves, then carry the running count
-            int r = run;
-#pragma unroll
-            for (int i = 0; i < NW; ++i) {
-                wpre[i][tid] = r;
-                r += wcnt[i][tid];
-            }
-            run = r;
-        }
-        lds_barrier();
-        if (valid) {
-            const int dst = wpre[w][dg] + rank;
-            if constexpr (DST == DST_ARRAY) {
-                p.keys_out[dst] = key;
-                p.vals_out[dst] = val;
-            } else {
-                p.nslot[(dst / S2) * p.S + dst % S2] = val;
-            }
-        }
-        // (wcnt / wpre are rewritten only after the next tile's first barrier)
-    }
-}
-
 template <int SRC, int DST, int RB>
 void rs_launch(hipStream_t st, const RsPass& p) {
     hipLaunchKernelGGL((k_rs_hist<SRC, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
     hipLaunchKernelGGL(k_rs_offsets, dim3(1 << RB), dim3(kRsGrid), 0, st, p.hist, p.tot);
-#if RT_AB_RS_OLD
-    hipLaunchKernelGGL((k_rs_scatter_r3<SRC, DST, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
-#else
     hipLaunchKernelGGL((k_rs_scatter<SRC, DST, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
-#endif
 }
 
 // the passes of a `bits`-bit key, <= RB bits each (split evenly), ping-ponging between the two arrays
