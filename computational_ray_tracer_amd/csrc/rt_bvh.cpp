@@ -5,8 +5,9 @@
 // and every box is rounded outwards (conservative: a triangle the watertight test hits at t lies in boxes the ray
 // enters before t).
 //
-// Build: binned SAH (16 bins per axis, leaves of <= kMaxLeaf triangles) into a binary tree, collapsed to 8-wide
-// nodes by repeatedly opening the largest-area internal child.
+// Build: binned SAH (64 bins per axis, leaves of <= kMaxLeaf triangles) into a binary tree, collapsed to 8-wide
+// nodes by an SAH-optimal dynamic program over the binary tree (round 4; round 3 opened the largest-area internal
+// child until there were 8: CFG3 9,314 -> 5,918 wide nodes, node visits per bounce ray 4.69 -> 4.54).
 //
 // Node (one 128-B cache line, 8 float4; the kernels read the first five):
 //   N0 = (origin.xyz, bits: ex | ey << 8 | ez << 16 | imask << 24)   origin = the node's padded box corner,
@@ -26,6 +27,7 @@
 // tiles' 48-B format (p0.xyz, p1.x) (p1.yz, p2.xy) (p2.z, bits(id), 0, 0) remains the exported, logical view
 // (bvh_tiles_logical): CFG3's closest-hit tiles shrink from 4.7 MB to 3.5 MB + 0.4 MB of ids.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -151,25 +153,62 @@ struct Collapse {
     BvhData& out;
     int depth_max = 0;
 
-    // the up-to-8 binary nodes that become the children of the 8-wide node for binary node n2 (opening the
-    // largest-area internal child until there are 8)
+    // Which binary nodes become the children of each 8-wide node: an SAH-optimal collapse (dynamic programming over
+    // the binary tree, Ylitie et al. 2017).  C1[n] = the cost of binary node n as one child of a wide node (a leaf:
+    // area x triangles; an internal node: a wide node of its own, area x wide_cost + its best spread D[n][8]);
+    // D[n][k] = the least cost of n's two subtrees spread over at most k child slots (each subtree either one child,
+    // C1, or opened again); Ck(n, k) = min(C1[n], D[n][k]).  Costs are areas: the SAH's hit probabilities.
+    double wide_cost = 3.0;  // a wide node's visit relative to one triangle test (2-6: the same CFG3 / CFG4 trees)
+    std::vector<double> C1;
+    std::vector<std::array<double, 9>> D;
+    std::vector<std::array<int, 9>> Dsplit;  // D[n][k]'s slots for the left subtree
+    double Ck(int n, int k) const { return k <= 1 || B.nodes[n].left < 0 ? C1[n] : std::min(C1[n], D[n][k]); }
+    void plan(int root) {
+        const size_t nn = B.nodes.size();
+        C1.assign(nn, 0.0);
+        D.assign(nn, {});
+        Dsplit.assign(nn, {});
+        // children have larger indices than their parent (pre-order build): a reverse sweep is post-order
+        for (size_t i = nn; i-- > 0;) {
+            const Node2& x = B.nodes[i];
+            const double a = x.box.area();
+            if (x.left < 0) {
+                C1[i] = a * x.count;
+                continue;
+            }
+            for (int k = 2; k <= 8; ++k) {
+                double best = std::numeric_limits<double>::infinity();
+                int bs = 1;
+                for (int kl = 1; kl < k; ++kl) {
+                    const double c = Ck(x.left, kl) + Ck(x.right, k - kl);
+                    if (c < best) { best = c; bs = kl; }
+                }
+                D[i][k] = best;
+                Dsplit[i][k] = bs;
+            }
+            C1[i] = a * wide_cost + D[i][8];
+        }
+        (void)root;
+    }
+    void expand(int n, int k, std::vector<int>& ch) const {
+        if (k <= 1 || B.nodes[n].left < 0 || C1[n] <= D[n][k]) {
+            ch.push_back(n);
+            return;
+        }
+        const int kl = Dsplit[n][k];
+        expand(B.nodes[n].left, kl, ch);
+        expand(B.nodes[n].right, k - kl, ch);
+    }
+    // the up-to-8 binary nodes that become the children of the 8-wide node for binary node n2
     std::vector<int> children8(int n2) const {
         std::vector<int> ch;
         if (B.nodes[n2].left < 0) {
             ch.push_back(n2);  // a leaf root
             return ch;
         }
-        ch = {B.nodes[n2].left, B.nodes[n2].right};
-        while (ch.size() < 8) {
-            int pick = -1;
-            double pa = -1;
-            for (size_t k = 0; k < ch.size(); ++k)
-                if (B.nodes[ch[k]].left >= 0 && B.nodes[ch[k]].box.area() > pa) { pa = B.nodes[ch[k]].box.area(); pick = (int)k; }
-            if (pick < 0) break;
-            const int o = ch[pick];
-            ch[pick] = B.nodes[o].left;
-            ch.push_back(B.nodes[o].right);
-        }
+        const int kl = Dsplit[n2][8];
+        expand(B.nodes[n2].left, kl, ch);
+        expand(B.nodes[n2].right, 8 - kl, ch);
         return ch;
     }
     int reserve(int n) {
@@ -325,6 +364,7 @@ void build_bvh8(const float* tri9, const int* ids, int n, float pad, float node_
     B.nodes.reserve(2 * (size_t)n);
     B.build(0, n);
     Collapse C{B, tri9, ids, (double)pad, out};
+    C.plan(0);
     out.nodes.reserve((size_t)kBvhNodeF4 * (n / 4 + 1));
     out.tiles.reserve(9 * (size_t)n);
     out.tid.reserve((size_t)n);

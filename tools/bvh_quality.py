@@ -52,6 +52,8 @@ def main():
            "shadow_nodes": round(ss["anyhit_nodes"] / r, 3), "shadow_boxes": round(ss["anyhit_boxes"] / r, 3),
            "shadow_tris": round(ss["anyhit_tris"] / r, 3),
            "mismatch": sb["closest_mismatch"] + ss["anyhit_mismatch"],
+           "closest_ambiguous": sb["closest_ambiguous"], "shadow_ambiguous": ss["anyhit_ambiguous"],
+           "stack_overflows": sb["stack_overflows"] + ss["stack_overflows"], "max_stack": max(sb["max_stack"], ss["max_stack"]),
            "env": {k: v for k, v in os.environ.items() if k.startswith("RTMI_BVH")}}
     print(json.dumps(out))
 
