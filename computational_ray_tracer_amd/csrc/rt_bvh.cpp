@@ -158,7 +158,7 @@ struct Collapse {
     // area x triangles; an internal node: a wide node of its own, area x wide_cost + its best spread D[n][8]);
     // D[n][k] = the least cost of n's two subtrees spread over at most k child slots (each subtree either one child,
     // C1, or opened again); Ck(n, k) = min(C1[n], D[n][k]).  Costs are areas: the SAH's hit probabilities.
-    double wide_cost = 3.0;  // a wide node's visit relative to one triangle test (2-6: the same CFG3 / CFG4 trees)
+    double wide_cost = 3.0;  // a wide node's visit relative to one triangle test (1-12: the same CFG3 / CFG4 trees)
     std::vector<double> C1;
     std::vector<std::array<double, 9>> D;
     std::vector<std::array<int, 9>> Dsplit;  // D[n][k]'s slots for the left subtree

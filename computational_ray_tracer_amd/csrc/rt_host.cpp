@@ -511,7 +511,6 @@ struct rt_ctx {
     int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
     int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
     int emit_filter = 1;       // RTMI_EMIT_FILTER=0: the last depth of a mixed scene traces every ray (A/B)
-    int force_full = 0;        // RTMI_FULL_PATH=1: simple scenes on the general path kernels too (deferred, sorted NEE)
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
@@ -1045,7 +1044,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     if (ie == ib || c->n_work == 0) return RT_OK;
     bool path = c->integ.kind == RT_INTEGRATOR_PATH || c->integ.kind == RT_INTEGRATOR_PATH_MIS;
     c->dsc.mis = c->integ.kind == RT_INTEGRATOR_PATH_MIS;
-    c->dsc.full = c->scene_full || c->dsc.mis || c->force_full;
+    c->dsc.full = c->scene_full || c->dsc.mis;
     // 16 Mi samples per path batch (8 Mi: Cornell 1874 -> 1827, CFG3 503 -> 484, CFG4 298 -> 284 Msamples/s)
     const size_t target = c->batch_samples ? c->batch_samples : (size_t)16 << 20;
     int B = (int)std::max<size_t>(1, target / (size_t)c->n_work);
@@ -1584,7 +1583,6 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
     if (const char* e = std::getenv("RTMI_EMIT_FILTER")) c->emit_filter = std::atoi(e);
-    if (const char* e = std::getenv("RTMI_FULL_PATH")) c->force_full = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) {
         int db = 3, ob = 4, om = -1;
         const int got = std::sscanf(e, "%d/%d/%d", &db, &ob, &om);

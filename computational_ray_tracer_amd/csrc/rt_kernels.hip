@@ -453,19 +453,13 @@ __device__ __forceinline__ void stage_warp_tables() {
 // ===================================================================================== K1 generate
 // RayTracerTestApp.h:305-323: StartPixelSample → SampleVisible(Get1D) → filter.Sample(GetPixel2D) →
 // pixel + .5 + p → PerspectiveCamera::generateRay (Cameras.h:273-297) → Ray::Transform (Shapes.h:37-41).
-// 4 waves/SIMD (158 -> 128 VGPRs, 112 B/lane spill): +3 % on the Cornell box
-// PDF: the pdf streams are stored (reference mode; not lean): the lean instantiation holds no pdf[8] registers
-// (103 VGPRs, no spill, against 128 + 28 B spill)
-#ifndef RT_GEN_LEAN_WAVES
-#define RT_GEN_LEAN_WAVES 4
-#endif
-#ifndef RT_AB_GEN_OLD
-#define RT_AB_GEN_OLD 0
-#endif
-template <int PDF>  // (A/B: 2 = round 3's single kernel, the pdf streams by the runtime flag)
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PDF ? 4 : RT_GEN_LEAN_WAVES))) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
+// 4 waves/SIMD (158 -> 128 VGPRs, 112 B/lane spill): +3 % on the Cornell box.  The pdf streams are stored only in
+// the reference mode (not lean); a lean instantiation without the pdf[8] registers (103 VGPRs, no spill) measured
+// Cornell -0.9 % (round 4, two interleaved rounds), so one kernel serves both.
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
                                                      DevFilm film, GenOut out) {
     stage_warp_tables();
+    const bool with_pdf = !out.lean;
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nS; s += gridDim.x * blockDim.x) {
         int pixel, index, x, y;
         sample_of(ids, s, pixel, index);
@@ -479,7 +473,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PDF
             float up = u + float(i) / 8;
             if (up > 1) up -= 1;
             lam[i] = sample_visible_wavelength<WarpTab>(up);
-            pdf[i] = (PDF == 1 || (PDF == 2 && !out.lean)) ? visible_pdf<WarpTab>(lam[i]) : 0.f;
+            pdf[i] = with_pdf ? visible_pdf<WarpTab>(lam[i]) : 0.f;
         }
         float u0, u1;
         sm.get_pixel2d(smp, u0, u1);  // Sampler::GetPixel2D (RayTracerTestApp.h:316)
@@ -541,7 +535,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PDF
         // the origin's w carries the path slot (= s for camera rays) through every queue and sort
         out.rayO[s << out.rsh] = make_float4(wo[0], wo[1], wo[2], __int_as_float(s));
         out.rayD[s << out.rsh] = make_float4(wd[0] * inv, wd[1] * inv, wd[2] * inv, 0.f);
-        if (PDF == 1 || (PDF == 2 && !out.lean)) store8(out.pdfA, out.pdfB, s, pdf);
+        if (with_pdf) store8(out.pdfA, out.pdfB, s, pdf);
         if (out.rec.p) {  // path mode: the slot's state
             rstore8(out.rec, s, R_LAM, lam);
             if (out.rec.rng8)
@@ -2495,14 +2489,7 @@ hipError_t launch_emitter_filter(hipStream_t st, int grid, const DevScene& sc, c
 
 hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& ids, const DevCamera& cam,
                            const DevSampler& smp, const DevFilm& film, const GenOut& out) {
-#if RT_AB_GEN_OLD
-    hipLaunchKernelGGL(k_generate<2>, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
-#else
-    if (out.lean)
-        hipLaunchKernelGGL(k_generate<0>, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
-    else
-        hipLaunchKernelGGL(k_generate<1>, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
-#endif
+    hipLaunchKernelGGL(k_generate, dim3(grid_for(nS, grid)), dim3(kBlock), 0, st, nS, ids, cam, smp, film, out);
     return hipGetLastError();
 }
 
