@@ -52,31 +52,6 @@ def parse():
     return p.parse_args()
 
 
-def pixel_roofline(st, counters, film_pixels):
-    """k_path_pixel (single-leaf simple-path scenes: the Cornell box): the whole path of a pixel's samples in one
-    thread, path state in registers.  Its only per-launch HBM stream is the film (16 B read + 16 B written per pixel);
-    everything else — the 36 staged triangles, the spectra, the warp tables — is LDS.  The bound is VALU issue:
-    `achieved` = SQ_INSTS_VALU per launch (profiles/counters_<config>.json, tools/counters.py, only when measured on
-    the loaded library build; else null) over the live HIP-event launch time, against one wave64 VALU instruction
-    per SIMD every 2 cycles.  The film stream is reported beside it as an HBM rate."""
-    launches = max(1, st["launches_shade"])
-    avg_s = st["ms_shade"] / launches * 1e-3
-    kc = (counters or {}).get("k_path_pixel", {})
-    film_b = 32 * film_pixels
-    r = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s", "frac": None,
-         "traffic": kc.get("dram_bytes_per_launch"), "kernel": "k_path_pixel", "launches": launches,
-         "avg_launch_ms": round(avg_s * 1e3, 4), "total_ms": round(st["ms_shade"], 3),
-         "hbm": {"algorithmic_bytes_per_launch": film_b, "achieved": round(film_b / avg_s / 1e9, 1) if avg_s else None,
-                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": round(film_b / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s else None},
-         "scene_bytes_per_launch_lds_served": int((32 * (st["nodes_tested"] + st["shadow_nodes_tested"]) +
-                                                   40 * (st["tris_tested"] + st["shadow_tris_tested"])) / launches)}
-    if kc.get("valu_insts_per_launch") and avg_s:
-        g = kc["valu_insts_per_launch"] / avg_s / 1e9
-        r.update(achieved=round(g, 1), frac=round(g / VALU_PEAK_GINST, 4), insts_per_launch=int(kc["valu_insts_per_launch"]))
-    return r
-
-
 def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=False, n_lights=1):
     """Per-kernel HBM and VALU rooflines from HIP-event launch times (the single-lane pass: one launch at a time).
 
@@ -120,7 +95,7 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=Fa
         ks["k_path_shade"] = (st["ms_shade"], st["launches_shade"], 312 * st["rays"], 0)
     res = {}
     for name, (ms, launches, stream_b, scene_b) in ks.items():
-        if ms <= 0:
+        if ms <= 0:  # (a stage that did not run)
             continue
         launches = max(1, launches)
         avg_s = ms / launches * 1e-3
@@ -371,31 +346,21 @@ def main():
     roofline, st1 = {}, None
     if rank == 0:
         st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
-        pixel_path = st1["ms_trace"] == 0 and st1["ms_shade"] > 0  # k_path_pixel ran (single leaf, simple path)
-        if pixel_path:
-            # this rank's pixels: the pass added spp_per_step * world indices per step to each
-            px = st1["samples"] // max(1, a.spp_per_step * world * a.steps)
-            rl = {"k_path_pixel": pixel_roofline(st1, counters, px)}
-        else:
-            rl = kernel_rooflines(st1, counters, "k_path_nee" if a.config in ("cfg4", "cfg5") else "k_path_shadow",
-                                  sorted_bounces=st1["ms_sort"] > 0,
-                                  n_lights=len(cfg.model.lights))
+        rl = kernel_rooflines(st1, counters, "k_path_nee" if a.config in ("cfg4", "cfg5") else "k_path_shadow",
+                              sorted_bounces=st1["ms_sort"] > 0,
+                              n_lights=len(cfg.model.lights))
         dom = max(rl, key=lambda k: rl[k]["total_ms"])
         roofline = dict(rl[dom])
         roofline["basis"] = (f"single-lane pass (RTMI_LANES=1, {a.steps} steps, {dt1 / a.steps * 1e3:.3f} ms/step): "
                              f"{roofline['launches'] / a.steps:g} launches per step x {roofline['avg_launch_ms']} ms")
         roofline["ms_per_step_single_lane"] = round(dt1 / a.steps * 1e3, 3)
-        roofline["limiter"] = ("VALU issue (box + watertight triangle tests, sampling, spectra) with the path in "
-                               "registers; see DESIGN.md §4" if pixel_path else
-                               "VALU issue and memory latency (box + watertight triangle tests); see DESIGN.md §4")
+        roofline["limiter"] = "VALU issue and memory latency (box + watertight triangle tests); see DESIGN.md §4"
         roofline["other_kernels"] = {k: v for k, v in rl.items() if k != dom}
         roofline["counters"] = cstat
     # Two batches run concurrently on two streams in the timed region (DESIGN.md §4 lanes); the node-level figure
     # divides every kernel's §8(d) stream bytes (generate 96 B/sample, trace 40 B/ray, shade 312 B/bounce + 32 B per
     # shadow ray, film 128 B/sample) by the wall time of the timed region.
     node_b = 96 * st["samples"] + (40 + 312) * st["rays"] + 32 * st["shadow_rays"] + 128 * st["samples"]
-    if st["ms_trace"] == 0 and st["ms_shade"] > 0:  # k_path_pixel: the film is the only stream (32 B per pixel, launch)
-        node_b = 32 * (W * H // world) * st["launches_shade"]
     node_a = node_b / dt / 1e9
     roofline["node"] = {"achieved": round(node_a, 1), "frac": round(node_a / HBM_PEAK_GBS, 4),
                         "bytes_per_step": int(node_b / a.steps), "lanes": int(os.environ.get("RTMI_LANES", "2")),

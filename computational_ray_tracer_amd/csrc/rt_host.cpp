@@ -520,7 +520,6 @@ struct rt_ctx {
     // per axis (6 / 7 bits: 353 / 356; CFG5 334 -> 355 at 7)
     int sort_nee = 1, sort_nee_bits = 8;  // (r03, device radix sort: 8 bits = 3 passes, CFG4 +1.5 % over 9 bits = 4 passes)
     hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
-    int pixel_path = 1;  // single-leaf simple-path scenes: k_path_pixel (0: the wavefront kernels; RTMI_PIXEL_PATH)
     size_t batch_samples = 0;  // samples in flight per batch (0: 16 Mi; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
@@ -1083,17 +1082,6 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
         return RT_OK;
     }
 
-    // ---- single-leaf simple-path scenes (the Cornell box): one k_path_pixel launch per batch of sample indices on the
-    // caller's stream, each thread one pixel's samples in index order (the film adds stay in order without lanes)
-    if (c->dsc.qcap == 1 && !c->dsc.full && c->pixel_path) {
-        for (int b0 = ib; b0 < ie; b0 += B) {
-            const PixelIO pio{c->d_work, c->n_work, b0, std::min(B, ie - b0), c->integ.max_depth, film};
-            hipEvent_t e0 = ev_start(c, st);
-            HIPCHK(c, launch_path_pixel(st, c->dsc, c->d_spec, cam, smp, fd, pio, c->d_ctr));
-            ev_mark(c, st, ST_SHADE, e0);
-        }
-        return RT_OK;
-    }
     // ---- path mode: up to c->lanes batches in flight, batch k on lane k mod lanes (lane 0 = the caller's stream).
     // Within a lane everything is stream-ordered; across lanes only the film kernels are chained (batch k's film
     // after batch k-1's), so every pixel still adds its sample indices in increasing order.
@@ -1595,7 +1583,6 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
     if (const char* e = std::getenv("RTMI_EMIT_FILTER")) c->emit_filter = std::atoi(e);
-    if (const char* e = std::getenv("RTMI_PIXEL_PATH")) c->pixel_path = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) {
         int db = 3, ob = 4, om = -1;
         const int got = std::sscanf(e, "%d/%d/%d", &db, &ob, &om);

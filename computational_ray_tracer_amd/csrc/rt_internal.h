@@ -419,14 +419,6 @@ struct PathFilmIO {
                // slot's R_MISC z flag is set (mixed scenes: dispersive glass)
 };
 
-// k_path_pixel (single-leaf simple-path scenes): pixel j of the work list adds its samples [index_begin,
-// index_begin + n_index) to film[work_pixels[j]], each path traced to the end in registers
-struct PixelIO {
-    const int* work_pixels; int n_pixels; int index_begin; int n_index;
-    int max_depth;
-    float4* film;
-};
-
 struct RecordIO {
     int n;
     const float4* rayO; const float4* rayD; const float4* lamA; const float4* lamB; const float4* pdfA;
@@ -478,8 +470,6 @@ hipError_t launch_path_shade(hipStream_t st, int grid, int qcap, const DevScene&
                              const DevSampler& smp, const DevFilm& film, const SampleIds& ids, const PathIO& io,
                              unsigned long long* ctr, const ShadowQueueIO& shq = ShadowQueueIO{},
                              const NeeIO& nee = NeeIO{}, int matclass = 0);
-hipError_t launch_path_pixel(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevCamera& cam,
-                             const DevSampler& smp, const DevFilm& film, const PixelIO& io, unsigned long long* ctr);
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr);
 hipError_t launch_path_nee_fallback(hipStream_t st, int grid, int qcap, const DevScene& sc, const DevSpectra* sp,

@@ -453,8 +453,7 @@ __device__ __forceinline__ void stage_warp_tables() {
 // ===================================================================================== K1 generate
 // RayTracerTestApp.h:305-323: StartPixelSample → SampleVisible(Get1D) → filter.Sample(GetPixel2D) →
 // pixel + .5 + p → PerspectiveCamera::generateRay (Cameras.h:273-297) → Ray::Transform (Shapes.h:37-41).
-// One camera sample of pixel (x, y): the sampler started at `index`, the 8 hero wavelengths and the world ray (w = 0)
-// — shared by k_generate and k_path_pixel.
+// One camera sample of pixel (x, y): the sampler started at `index`, the 8 hero wavelengths and the world ray (w = 0).
 __device__ __forceinline__ void camera_sample(const DevCamera& cam, const DevSampler& smp, const DevFilm& film, int x,
                                               int y, int index, Smp& sm, float lam[8], float4& ro, float4& rd) {
     sm.start(smp, x, y, index, 0);
@@ -2402,169 +2401,6 @@ __global__ void __launch_bounds__(kBlock) k_path_film(const DevSpectra* sp, DevF
     count_add(ctr, C_SAMPLES, ns);
 }
 
-// Single-leaf simple-path scenes (the Cornell box): a pixel's whole sample loop in one thread — the reference's
-// evaluate_pixel loop (RayTracerTestApp.h:300-330) — with the path state in registers instead of slot records and
-// ray queues in HBM.  Per sample: camera_sample (as k_generate), then per depth the closest-hit walk of the staged
-// leaf (as k_trace_closest<1>), the shading of k_path_shade<1> (emitter Le at depth 0, NEE with the shadow ray traced
-// inline after the bounce is drawn, the cosine bounce) and, when the path ends, the sensor conversion and the film
-// add of k_path_film — the same arithmetic in the same order, so the film is bit-identical to the wavefront
-// kernels'.  A thread adds its pixel's indices [index_begin, index_begin + n_index) in order, as k_path_film does.
-// The lanes of a wave stay in step per sample (a finished path's lane idles until the wave's longest path ends).
-#ifndef RT_PIXEL_WAVES
-#define RT_PIXEL_WAVES 4
-#endif
-#ifndef RT_PIXEL_TRI_LDS
-#define RT_PIXEL_TRI_LDS 0  // the shading inputs staged in LDS (g_tri1): 41 KB per block, above the 4-block budget
-#endif
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_PIXEL_WAVES))) k_path_pixel(
-    DevScene sc, const DevSpectra* sp, DevCamera cam, DevSampler smp, DevFilm film, PixelIO io, unsigned long long* ctr) {
-    const float InvPi = 0.31830988618379067154f;
-    stage_warp_tables();
-    stage_spectra(sp);
-    stage_scene<1>(sc, 0);
-    const bool lds_tris = RT_PIXEL_TRI_LDS ? stage_tris1(sc) : false;
-    // per-thread counts fit 32 bits (a thread's samples x depths x clusters): 10 VGPRs fewer than ctr_t
-    unsigned nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0, snn = 0, snt = 0, nsh = 0, sfb = 0, ns = 0;
-    const int nd = io.max_depth > 0 ? io.max_depth : 1;  // depths traced (rt_host.cpp: the last one never is)
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < io.n_pixels; j += gridDim.x * blockDim.x) {
-        const int pixel = io.work_pixels[j];
-        int x, y;
-        pixel_xy(film, pixel, x, y);
-        float4 f = io.film[pixel];
-        for (int i = 0; i < io.n_index; ++i) {
-            Smp sm;
-            float lam[8];
-            float4 o4, d4;
-            camera_sample(cam, smp, film, x, y, io.index_begin + i, sm, lam, o4, d4);
-            float beta[8], L[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) { beta[w] = 1.f; L[w] = 0.f; }
-            for (int depth = 0; depth < nd; ++depth) {
-                // --- closest hit (k_trace_closest trace_one)
-                float b0 = 0, b1 = 0, b2 = 0, t = 0;
-                ctr_t cnn = 0, cnt = 0, cfb = 0;
-                int prim = traverse_any<1, false>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
-                                                  b0, b1, b2, t, cnn, cnt, cfb);
-                nn += (unsigned)cnn; nt += (unsigned)cnt; nfb += (unsigned)cfb;
-                if (sc.n_shapes) {
-                    float tm = prim >= 0 ? t : 3.402823466e+38f;
-                    for (int si = 0; si < sc.n_shapes; ++si) {
-                        DevShape sh = ldconst(sc.shapes, si);
-                        V3 ph;
-                        float th;
-                        if (shape_isect(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
-                            prim = sc.n_tris + si; b0 = ph.x; b1 = ph.y; b2 = ph.z; t = th; tm = th;
-                        }
-                    }
-                }
-                nh += prim >= 0;
-                nr += 1;
-                if (prim < 0) break;
-                // --- shading (k_path_shade<1>)
-                float4 P0, P1, P2, mt;
-                if (lds_tris) {
-                    P0 = g_tri1[4 * prim]; P1 = g_tri1[4 * prim + 1]; P2 = g_tri1[4 * prim + 2]; mt = g_tri1[4 * prim + 3];
-                } else {
-                    P0 = sc.triWorld[3 * prim]; P1 = sc.triWorld[3 * prim + 1]; P2 = sc.triWorld[3 * prim + 2];
-                    const DevMaterial dm = sc.materials[sc.triMaterial[prim]];
-                    mt = make_float4(dm.c0, dm.c1, dm.c2, dm.emit);
-                }
-                V3 p0 = v3(P0.x, P0.y, P0.z), p1 = v3(P1.x, P1.y, P1.z), p2 = v3(P2.x, P2.y, P2.z);
-                V3 ng = vnorm(vcross(vsub(p0, p2), vsub(p1, p2)));  // Shapes.h:1073
-                V3 rayd = vnorm(v3(d4.x, d4.y, d4.z));
-                if (mt.w > 0) {
-                    if (depth == 0 && vdot(ng, rayd) < 0) {
-#pragma unroll
-                        for (int w = 0; w < 8; ++w) L[w] += beta[w] * (mt.w * d65_query(sp, lam[w]));
-                    }
-                    break;
-                }
-                if (depth >= io.max_depth) break;
-                V3 nrm = ng;
-                if (vdot(nrm, rayd) > 0) nrm = v3(-nrm.x, -nrm.y, -nrm.z);
-                V3 p = vadd(vadd(vmul(p0, b0), vmul(p1, b1)), vmul(p2, b2));
-                float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
-                V3 po = vadd(p, vmul(nrm, off));
-                float R[8];
-#pragma unroll
-                for (int w = 0; w < 8; ++w) R[w] = sigmoid_eval(mt.x, mt.y, mt.z, lam[w]);
-                bool wantShadow = false, wantNext = false;
-                V3 sd = v3(0, 0, 0);
-                float stmax = 0.f, Ld[8];
-                float u0, u1;
-                sm.get2d(smp, u0, u1);
-                if (sc.n_lights > 0) {
-                    const DevLight& Lq = sc.light0;
-                    V3 pl = vadd(vadd(v3(Lq.p[0], Lq.p[1], Lq.p[2]), vmul(v3(Lq.e1[0], Lq.e1[1], Lq.e1[2]), u0)),
-                                 vmul(v3(Lq.e2[0], Lq.e2[1], Lq.e2[2]), u1));
-                    V3 wv = vsub(pl, po);
-                    float dist2 = vdot(wv, wv);
-                    float dist = sqrtf(dist2);
-                    V3 wi = vmul(wv, 1.0f / dist);
-                    float cs = vdot(nrm, wi);
-                    float cl = -vdot(v3(Lq.n[0], Lq.n[1], Lq.n[2]), wi);
-                    if (cs > 0 && cl > 0) {
-                        float le = sc.materials[Lq.material].emit;
-                        float G = (cs * cl) / dist2;
-                        float wgt = G * Lq.area;
-#pragma unroll
-                        for (int w = 0; w < 8; ++w) Ld[w] = ((beta[w] * (R[w] * InvPi)) * (le * d65_query(sp, lam[w]))) * wgt;
-                        wantShadow = true;
-                        sd = wi;
-                        stmax = dist * 0.999f;
-                    }
-                }
-                if (depth + 1 < io.max_depth) {
-                    sm.get2d(smp, u0, u1);
-                    V3 wi;
-                    float z;
-                    if (cosine_bounce(u0, u1, nrm, wi, z)) {
-#pragma unroll
-                        for (int w = 0; w < 8; ++w) beta[w] *= R[w];
-                        wantNext = true;
-                        o4 = make_float4(po.x, po.y, po.z, 0.f);
-                        d4 = make_float4(wi.x, wi.y, wi.z, 0.f);
-                    }
-                }
-                if (wantShadow) {  // after the bounce, as in k_path_shade
-                    float c0, c1, c2, ct;
-                    ctr_t cnn = 0, cnt = 0, cfb = 0;
-                    const int hit = traverse_any<1, true>(sc, 0, po, sd, stmax, c0, c1, c2, ct, cnn, cnt, cfb);
-                    snn += (unsigned)cnn; snt += (unsigned)cnt; sfb += (unsigned)cfb;
-                    ++nsh;
-                    if (hit < 0) {
-#pragma unroll
-                        for (int w = 0; w < 8; ++w) L[w] += Ld[w];
-                    }
-                }
-                if (!wantNext) break;
-            }
-            // --- sensor and film (k_path_film, lean: the pdf recomputed)
-            float pdf[8], rgb[3];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) pdf[w] = visible_pdf<WarpTab>(lam[w]);
-            to_sensor_rgb_spk(sp, L, lam, pdf, film.imaging_ratio, rgb);
-            const float fw = 1.0f;
-            f.x += fw * gclamp(rgb[0], 0.0f, 1.0f);
-            f.y += fw * gclamp(rgb[1], 0.0f, 1.0f);
-            f.z += fw * gclamp(rgb[2], 0.0f, 1.0f);
-            f.w += fw;
-            ++ns;
-        }
-        io.film[pixel] = f;
-    }
-    count_add(ctr, C_NODES, nn);
-    count_add(ctr, C_TRIS, nt);
-    count_add(ctr, C_HITS, nh);
-    count_add(ctr, C_RAYS, nr);
-    count_add(ctr, C_FALLBACK, nfb);
-    count_add(ctr, C_SNODES, snn);
-    count_add(ctr, C_STRIS, snt);
-    count_add(ctr, C_SHADOW, nsh);
-    count_add(ctr, C_SFALLBACK, sfb);
-    count_add(ctr, C_SAMPLES, ns);
-}
-
 // a20 resolve (RayTracerTestApp.h:437-451): rgbsum/weightsum → XYZFromSensorRGB → RGBFromXYZ → clamp → u8
 // pbrt ColorEncoding::sRGB LinearToSRGB8 (color.h:537-557): EvaluatePolynomial is a Horner chain of FMAs
 __device__ __forceinline__ unsigned char linear_to_srgb8(float v) {
@@ -2801,12 +2637,6 @@ hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, 
 hipError_t launch_path_film(hipStream_t st, int grid, const DevSpectra* sp, const DevFilm& film, const PathFilmIO& io,
                             unsigned long long* ctr) {
     hipLaunchKernelGGL(k_path_film, dim3(resident_grid(k_path_film, grid_for(io.n_pixels, grid), grid)), dim3(kBlock), 0, st, sp, film, io, ctr);
-    return hipGetLastError();
-}
-
-hipError_t launch_path_pixel(hipStream_t st, const DevScene& sc, const DevSpectra* sp, const DevCamera& cam,
-                             const DevSampler& smp, const DevFilm& film, const PixelIO& io, unsigned long long* ctr) {
-    hipLaunchKernelGGL(k_path_pixel, dim3(grid_for(io.n_pixels, 0)), dim3(kBlock), 0, st, sc, sp, cam, smp, film, io, ctr);
     return hipGetLastError();
 }
 

@@ -116,30 +116,21 @@ def test_resolve_matches_oracle(pair_small):
     assert np.array_equal(g.resolve(f, srgb=True), o.resolve(f, srgb=True))   # pbrt sRGB encoding (color.h:537-557)
 
 
-@pytest.mark.parametrize("pixel_path", ["1", "0"])
-def test_cornell_path_film_bitexact(oracle_lib, monkeypatch, pixel_path):
-    """The Cornell box through k_path_pixel (a pixel's samples in one thread, the path in registers: the default for
-    single-leaf simple-path scenes) and through the wavefront kernels (RTMI_PIXEL_PATH=0): tolerance 0."""
-    monkeypatch.setenv("RTMI_PIXEL_PATH", pixel_path)
+def test_cornell_path_film_bitexact(oracle_lib):
     cfg = scene.cfg_cornell(res=(64, 64), spp_side=4)
     g = Renderer(cfg)
     fg = g.render_pass(0, 16)
     fo = oracle_lib.OracleScene(cfg).render(0, 16)
     bad = np.any(bits(fg) != bits(fo), axis=1)
     assert bad.sum() == 0, f"{bad.sum()} pixels differ; max |diff| {np.abs(fg - fo).max()}"
-    st = g.stats()
-    assert st["samples"] == 64 * 64 * 16 and st["rays"] > st["samples"] and st["shadow_rays"] > 0
 
 
-@pytest.mark.parametrize("lanes,scene_kind,pixel_path", [(2, "cornell", "0"), (1, "cornell", "0"), (2, "cornell", "1"),
-                                                        (2, "mesh", "1")])
-def test_concurrent_batches_film_bitexact(oracle_lib, monkeypatch, lanes, scene_kind, pixel_path):
-    """Several batches per pass (RTMI_BATCH_SAMPLES) alternating between the two lane streams (wavefront kernels) or
-    in sequence (k_path_pixel), including an odd batch count and a ragged last batch: the film chain must keep every
-    pixel's index order (tolerance 0)."""
+@pytest.mark.parametrize("lanes,scene_kind", [(2, "cornell"), (1, "cornell"), (2, "mesh")])
+def test_concurrent_batches_film_bitexact(oracle_lib, monkeypatch, lanes, scene_kind):
+    """Several batches per pass (RTMI_BATCH_SAMPLES) alternating between the two lane streams, including an odd
+    batch count and a ragged last batch: the film chain must keep every pixel's index order (tolerance 0)."""
     monkeypatch.setenv("RTMI_BATCH_SAMPLES", str(48 * 40 * 2))   # 2 indices per batch
     monkeypatch.setenv("RTMI_LANES", str(lanes))
-    monkeypatch.setenv("RTMI_PIXEL_PATH", pixel_path)
     if scene_kind == "cornell":
         cfg = scene.cfg_cornell(res=(48, 40), spp_side=3)
     else:

@@ -17,7 +17,7 @@ import glob
 import json
 from pathlib import Path
 
-KERNELS = ("k_path_pixel", "k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_shade_full_c1", "k_path_shade_full_c2",
+KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_shade_full_c1", "k_path_shade_full_c2",
            "k_bin_materials", "k_path_nee", "k_path_nee_fb", "k_path_shadow", "k_generate", "k_path_film",
            "k_ref_shade_film", "k_rs_hist", "k_rs_scatter", "k_rs_offsets", "k_rs_prep")
 # the mixed-scene shade of one bounce with material bins: the binning pass and one kernel per material class, all
