@@ -139,8 +139,8 @@ struct DevScene {
     // kBvhNodeF4 float4 per node) and its leaf-ordered triangle tiles (9 floats each, packed) with their triangle
     // ids; rays it finds ambiguous fall back to the octree BFS
     const float4* bvh[3];           // [0], [1]: closest-hit BVH of tile set 0 / 1; [kBvhAny]: the any-hit walks' BVH
-    const float* btiles[3];         // (by default the same arrays as [0]: one working set for both queries;
-    const int* btid[3];             // RTMI_BVH_ANY="cost/leaf" builds a separate one, set 0)
+    const float* btiles[3];         // ([kBvhAny]: its own build, SAH node cost 2; RTMI_BVH_ANY="0/4" aliases set 0's
+    const int* btid[3];             // arrays, "cost/leaf" builds it with other parameters)
     float wabs;                     // canonical-rule window W(t) = t 2^-16 + wabs
     float oguard;                   // rays whose origin has a coordinate beyond +-oguard are ambiguous (the box
                                     // padding covers the slab test's rounding only for origins inside 8 M)
