@@ -244,28 +244,34 @@ def cpu_baseline(cfg, seconds):
     oracle.use_native()
     o = oracle.OracleScene(cfg)
     W, H = cfg.film.res
+    spp = cfg.sampler.spp()
     eff, cpuinfo = effective_cpus()
 
     def run(threads, budget):
-        rows = max(1, min(H, threads))
+        # a band of full rows at sample index 0, grown to the whole frame, then more sample indices of the frame
+        rows, nidx = max(1, min(H, threads)), 1
         while True:
             y0 = H // 2 - rows // 2
             pix = np.arange(y0 * W, (y0 + rows) * W, dtype=np.int32)
             t0 = time.perf_counter()
-            o.render(0, 1, nthreads=threads, pixel_ids=pix)
+            o.render(0, nidx, nthreads=threads, pixel_ids=pix)
             dt = time.perf_counter() - t0
-            if dt > budget * 0.5 or rows >= H:
-                return len(pix) / dt / 1e6, len(pix), dt
-            rows = min(H, int(rows * max(2.0, budget / max(dt, 1e-3))))
+            if dt > budget * 0.5 or nidx >= spp:
+                return len(pix) * nidx / dt / 1e6, len(pix) * nidx, dt, nidx
+            grow = max(2.0, budget / max(dt, 1e-3))
+            if rows < H:
+                rows = min(H, int(rows * grow))
+            else:
+                nidx = min(spp, int(np.ceil(nidx * grow)))
 
     points = sorted({1, min(8, eff), eff, min(2 * eff, 512)})
     share = {t: (0.5 if t == eff else 0.15) for t in points}
     sweep, main = [], None
     for t in points:
-        v, n, dt = run(t, seconds * share[t])
+        v, n, dt, k = run(t, seconds * share[t])
         sweep.append({"threads": t, "msamples_s": round(v, 4), "samples": n, "seconds": round(dt, 2)})
         if t == eff:
-            main = (v, n, dt)
+            main = (v, n, dt, k)
     v1 = sweep[0]["msamples_s"]
     model = "unknown"
     try:
@@ -275,14 +281,14 @@ def cpu_baseline(cfg, seconds):
                 break
     except OSError:
         pass
-    v, n, dt = main
+    v, n, dt, k = main
     return {"value": round(v, 4), "unit": "Msamples/s", "cores": eff, "kind": "port",
             "effective_cpus": eff, **cpuinfo, "thread_sweep": sweep,
             "speedup_at_cores": round(v / v1, 2) if v1 else None,
             "single_thread": v1, "cpu_model": model,
             "build": "g++ -O3 -march=native -ffp-contract=off (built on this host)",
             "sample": f"oracle C++ restatement (same octree BFS, watertight test, path integrator): {n} samples = "
-                      f"{n // W} full rows of the {W}x{H} frame x sample index 0 on {eff} threads "
+                      f"{n // W // k} full rows of the {W}x{H} frame x sample indices 0..{k - 1} on {eff} threads "
                       f"(affinity capped by the cgroup quota), {dt:.1f} s"}
 
 
