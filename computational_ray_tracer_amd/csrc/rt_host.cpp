@@ -1194,7 +1194,6 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     qv = QueueView{qc_nxt + kQLen, Sq[l], 0, nsh};
                 }
                 TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
-                tio.prim_w = c->dsc.full ? 0 : 1;  // simple path: the id in hitB.w for k_path_shade (TraceIO)
                 BinIO bio{qv, w.hitPrim, {w.neeSlot + 3 * ncap, w.neeSlot + 4 * ncap}, qc_cur + kQBinLen};
                 if (depth == 0) { bio.rayO = cO; bio.rec = rv; }  // lean depth 0: the misses' L = 0 (BinIO)
                 static_assert(kMatClasses == 2, "bin index lists");
@@ -1214,7 +1213,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 PathIO pio{};
                 pio.lean = lean;
                 pio.rayO = cO; pio.rayD = cD; pio.q = qv;
-                pio.hitB = w.hitB; pio.hitPrim = w.hitPrim; pio.prim_w = tio.prim_w;
+                pio.hitB = w.hitB; pio.hitPrim = w.hitPrim;
                 pio.nO = w.rayO + 2 * (size_t)nxt * qs; pio.nD = pio.nO + 1;
                 pio.nCount = qc_nxt + kQLen;
                 pio.rec = rv; pio.pdfA = w.pdfA; pio.pdfB = w.pdfB;

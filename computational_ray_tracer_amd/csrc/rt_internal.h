@@ -281,9 +281,6 @@ struct TraceIO {
     // stores it to so[2p], so[2p + 1] — the sorted side queue the shade kernel reads; nullptr: no sort
     const int* perm = nullptr;
     float4* so = nullptr;
-    // 1 (simple-path bounces): the hit's primitive id rides in hitB.w (int bits) instead of t, which k_path_shade
-    // never reads, and hitPrim is not written: one 16-B store per ray and one 16-B load per shaded ray
-    int prim_w = 0;
 };
 
 // Material binning of a mixed multi-level scene's bounce (k_bin_materials, after the trace): every hit's queue
@@ -343,7 +340,6 @@ struct PathIO {
     int* ticket;  // per-shard chunk tickets (zeroed before the launch) or nullptr: static chunks
     RayKeyIO nkey;  // multi-level scenes: the coherence-sort key of every appended ray (rt_sort.hip)
     const int* bin_idx = nullptr;  // material-binned shade: item i of q is queue position bin_idx[i] (BinIO)
-    int prim_w = 0;                // the trace stored the primitive id in hitB.w (TraceIO prim_w)
 };
 
 // Shadow queue (multi-level octrees): the shade kernel appends NEE shadow rays {o, tMax}, {d, slot} and their

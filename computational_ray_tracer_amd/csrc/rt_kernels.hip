@@ -1400,8 +1400,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                 }
             }
         }
-        io.hitB[p] = make_float4(b0, b1, b2, io.prim_w ? __int_as_float(prim) : t);
-        if (!io.prim_w) io.hitPrim[p] = prim;
+        io.hitB[p] = make_float4(b0, b1, b2, t);
+        io.hitPrim[p] = prim;
         nh += prim >= 0;
         nr += 1;
     };
@@ -1726,8 +1726,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         int slot = -1;
         if (live) {
             slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
-            const float4 hb = io.hitB[k];
-            const int prim = io.prim_w ? __float_as_int(hb.w) : io.hitPrim[k];
+            const int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
                 rload8(io.rec, slot, R_LAM, lam);
@@ -1762,6 +1761,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                 } else if (io.depth < io.max_depth) {
                     V3 nrm = ng;
                     if (vdot(nrm, rayd) > 0) nrm = v3(-nrm.x, -nrm.y, -nrm.z);
+                    const float4 hb = io.hitB[k];
                     V3 p = vadd(vadd(vmul(p0, hb.x), vmul(p1, hb.y)), vmul(p2, hb.z));
                     float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
                     V3 po = vadd(p, vmul(nrm, off));

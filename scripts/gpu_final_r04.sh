@@ -4,6 +4,7 @@
 #   b: >= 8-step bench lines of every BASELINE config (the default line with the CPU baseline; CFG4 / CFG5 lines with
 #      the 8-shard tile-efficiency projection)
 #   c: where the Cornell kernels wait (SQ wait / LDS / SMEM counters, gpu_pmc_cornell.sh)
+#   ab: a, then b with a's counters installed
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
 TAG=${TAG:-r04a}
 case "${PART:-a}" in
@@ -22,6 +23,11 @@ b)
   ;;
 c)
   CFG=cornell TAG=$TAG bash scripts/gpu_pmc_cornell.sh || exit 1
+  ;;
+ab)  # a, the new counters installed into this copy's profiles/ (the bench reads them), then b
+  PART=a TAG=$TAG bash scripts/gpu_final_r04.sh || exit 1
+  for c in ${CONFIGS:-cornell cfg3 cfg4 cfg5}; do cp gpurun_out/cnt_${c}_$TAG.counters.json profiles/counters_$c.json || exit 1; done
+  PART=b TAG=$TAG bash scripts/gpu_final_r04.sh || exit 1
   ;;
 esac
 exit 0
