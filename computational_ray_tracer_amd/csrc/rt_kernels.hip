@@ -1462,11 +1462,11 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
 }
 
 // Material bins of a mixed multi-level scene's bounce (BinIO): every hit's queue position is appended to the index
-// list of its material class, shard by shard, in queue order within a chunk; misses go to no bin (the full path integrator has no miss work).  A pass
-// over the hit ids of its own (in the trace kernel the appends cost registers the traversal needs).  A block takes
-// chunks of kBinItems x 256 consecutive positions of one shard: it counts each class (wave ballots, LDS), makes ONE
-// atomic per class and chunk (per-wave appends on the 16 shard counters saturated them: 313 us per launch), then
-// writes the positions at their ranks.
+// list of its material class, shard by shard, in queue order within a chunk; misses go to no bin (no miss work; at
+// lean depth 0 their L = 0 is stored here).  A pass over the hit ids of its own (in the trace kernel the appends cost
+// registers the traversal needs).  A block takes chunks of kBinItems x 256 consecutive positions of one shard: it
+// counts each class (wave ballots, LDS), makes ONE atomic per class and chunk (per-wave appends on the per-shard
+// class counters saturated them: 313 us per launch), then writes the positions at their ranks.
 static constexpr int kBinItems = 8;
 __global__ void __launch_bounds__(kBlock) k_bin_materials(DevScene sc, BinIO io) {
     constexpr int NW = kBlock / 64, CH = kBinItems * kBlock;
