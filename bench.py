@@ -104,6 +104,8 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=Fa
         res[name] = {"bound": "hbm", "achieved": round(a, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(a / HBM_PEAK_GBS, 4),
                      "traffic": kc.get("dram_bytes_per_launch"),
+                     # FETCH_SIZE not doubled (the guide validates the x2 only for wide coalesced reads)
+                     "traffic_raw": kc.get("dram_bytes_per_launch_raw"),
                      "kernel": name, "launches": launches, "avg_launch_ms": round(avg_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": int(stream_b / launches),
                      # §8(d) scene terms over the EXECUTED box / triangle tests: served by LDS / L1 / L2 (the
@@ -112,6 +114,10 @@ def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=Fa
                      "total_ms": round(ms, 3)}
         if kc.get("dram_bytes_per_launch") and stream_b:
             res[name]["traffic_over_algorithmic"] = round(kc["dram_bytes_per_launch"] / (stream_b / launches), 2)
+            if kc.get("dram_bytes_per_launch_raw"):  # [FETCH_SIZE x1, x2] + WRITE_SIZE over the algorithmic bytes
+                res[name]["traffic_over_algorithmic_range"] = [
+                    round(kc["dram_bytes_per_launch_raw"] / (stream_b / launches), 2),
+                    res[name]["traffic_over_algorithmic"]]
         if kc.get("valu_insts_per_launch"):
             g = kc["valu_insts_per_launch"] / avg_s / 1e9
             res[name]["valu"] = {"achieved": round(g, 1), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
@@ -200,8 +206,9 @@ def project_shards(r, cfg, n, spp_per_step, steps, warmup, stream):
     dispatch this replaces): rank k of an n-GPU run renders shard k of rt_set_shard(32, n, k) — every n-th 32x32
     tile — for spp_per_step * n sample indices per step (weak scaling: the same samples per GPU as the 1-GPU step).
     Each shard is rendered here alone, for the same number of steps; a step of the n-GPU run lasts as long as its
-    slowest shard, so the efficiency is mean / max of the per-shard step times (the once-per-frame film reduce is
-    not included: 33 MB per frame at 1080p over xGMI)."""
+    slowest shard, so the efficiency is mean / max of the per-shard step times; `efficiency_with_reduce` also charges
+    the once-per-frame film reduce (33 MB at 1080p: a measured on-device copy plus the modelled xGMI transfer,
+    frame_reduce_cost) to the steps of the frame."""
     W, H = cfg.film.res
     film = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda")
     per, spp = spp_per_step * n, cfg.sampler.spp()
@@ -228,10 +235,40 @@ def project_shards(r, cfg, n, spp_per_step, steps, warmup, stream):
         dt = (time.perf_counter() - t0) / steps
         rows.append({"shard": k, "ms_per_step": round(dt * 1e3, 3), "samples_per_step": int(r.stats()["samples"] / steps)})
     ms = [x["ms_per_step"] for x in rows]
-    return {"n": n, "efficiency": round(sum(ms) / len(ms) / max(ms), 4), "max_ms": max(ms),
+    eff = sum(ms) / len(ms) / max(ms)
+    red = frame_reduce_cost(film, n, per, spp)
+    step_red = max(ms) + red["per_step_ms"]
+    return {"n": n, "efficiency": round(eff, 4), "max_ms": max(ms),
             "mean_ms": round(sum(ms) / len(ms), 3), "shards": rows,
+            "efficiency_with_reduce": round(sum(ms) / len(ms) / step_red, 4), "frame_reduce": red,
             "basis": f"each shard of rt_set_shard(32, {n}, k) alone on this GPU, {per} indices per step "
-                     f"({steps} steps after {max(1, warmup)} warmup): mean / max step time"}
+                     f"({steps} steps after {max(1, warmup)} warmup): mean / max step time; with_reduce adds the "
+                     f"once-per-frame film reduce (frame_reduce) spread over the frame's steps to the slowest step"}
+
+
+def frame_reduce_cost(film, n, per, spp, link_gbs=153.0, reps=20):
+    """The once-per-frame film reduce of an n-GPU run (distributed.FrameLoop: torch.distributed.reduce(SUM) onto rank
+    0), costed per step.  Measured here: a device-to-device copy of the whole film on this GPU (the copy every rank's
+    film makes on its way through RCCL's buffers; 33 MB at 1080p).  Modelled: the xGMI transfer of a ring reduce,
+    2 (n - 1) / n film sizes over one link at link_gbs (MI355X_MICROARCH: 7 links x ~153 GB/s per GPU; RCCL's ring
+    reduce moves that much per link).  The frame is spp indices, a step renders per = spp_per_step x n of them."""
+    dst = torch.empty_like(film)
+    for _ in range(2):
+        dst.copy_(film)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(film)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_ms = e0.elapsed_time(e1) / reps
+    nbytes = film.numel() * film.element_size()
+    xgmi_ms = 2 * (n - 1) / n * nbytes / (link_gbs * 1e9) * 1e3
+    steps_per_frame = max(1.0, spp / per)
+    per_frame = copy_ms + xgmi_ms
+    return {"film_bytes": nbytes, "d2d_copy_ms_measured": round(copy_ms, 4), "xgmi_ring_reduce_ms_model": round(xgmi_ms, 4),
+            "per_frame_ms": round(per_frame, 4), "steps_per_frame": round(steps_per_frame, 3),
+            "per_step_ms": round(per_frame / steps_per_frame, 4)}
 
 
 def cpu_baseline(cfg, seconds):
@@ -352,8 +389,11 @@ def main():
     roofline, st1 = {}, None
     if rank == 0:
         st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
+        # multi-level scenes sort their bounce rays unless RTMI_SORT=0 (decided by the configuration, not by whether
+        # the sort's stage events recorded time)
+        sorted_b = a.config != "cornell" and os.environ.get("RTMI_SORT", "1") not in ("0", "")
         rl = kernel_rooflines(st1, counters, "k_path_nee" if a.config in ("cfg4", "cfg5") else "k_path_shadow",
-                              sorted_bounces=st1["ms_sort"] > 0,
+                              sorted_bounces=sorted_b,
                               n_lights=len(cfg.model.lights))
         dom = max(rl, key=lambda k: rl[k]["total_ms"])
         roofline = dict(rl[dom])
@@ -394,6 +434,7 @@ def main():
     if world == 1 and a.project_shards > 1:
         pj = project_shards(r, cfg, a.project_shards, a.spp_per_step, a.steps, a.warmup, stream)
         out[f"projected_tile_efficiency_{a.project_shards}"] = pj["efficiency"]
+        out[f"projected_tile_efficiency_{a.project_shards}_with_reduce"] = pj["efficiency_with_reduce"]
         out["shard_projection"] = pj
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds)

@@ -42,12 +42,19 @@ class FrameLoop:
     completed frame is kept in `frame` on `dst`, and `film` is zeroed so the next frame starts from nothing.
     Reducing only at frame end keeps the collective off the per-step path and never re-adds a rank's
     earlier contributions (an in-place reduce per step would count the root's already-reduced pixels again).
+
+    Aliasing: by default `frame` is one of two buffers that alternate with `film` on dst (no 33 MB copy per frame,
+    bench.py), so the tensor `frame` refers to is zeroed and re-used as the accumulation film when the NEXT frame
+    starts, and overwritten when the frame after it completes.  A caller that keeps completed frames beyond one
+    frame period (saving or displaying them asynchronously) passes keep_frames=True: every completed frame is then
+    a fresh tensor the loop never touches again (one device copy per frame).  Ranks other than dst keep no frame.
     """
 
-    def __init__(self, spp, per_step, film, dst=0):
+    def __init__(self, spp, per_step, film, dst=0, keep_frames=False):
         self.spp, self.per_step, self.film, self.dst = int(spp), int(per_step), film, dst
+        self.keep_frames = bool(keep_frames)
         self.cursor = 0
-        self.frame = None      # last completed (reduced) frame, on dst
+        self.frame = None      # last completed (reduced) frame, on dst (see "Aliasing")
         self.frames_done = 0
 
     def step(self, render):
@@ -62,9 +69,12 @@ class FrameLoop:
         if i1 >= self.spp:
             reduce_film(self.film, dst=self.dst)
             if _rank() == self.dst:
-                spare = self.frame
-                self.frame = self.film
-                self.film = spare if spare is not None else self.film.new_zeros(self.film.shape)
+                if self.keep_frames:
+                    self.frame = self.film.clone()
+                else:
+                    spare = self.frame
+                    self.frame = self.film
+                    self.film = spare if spare is not None else self.film.new_zeros(self.film.shape)
             self.film.zero_()
             self.frames_done += 1
             self.cursor = 0

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-4 evidence of one build, in GPU calls of their own (PART=a / b / c); stops at the first failure.
+# Round evidence of one build, in GPU calls of their own (PART=a / b / c); stops at the first failure.
 #   a: smoke, the -m gpu suite, single-lane kernel traces + PMC counters of Cornell / CFG3 / CFG4 / CFG5
 #   b: >= 8-step bench lines of every BASELINE config (the default line with the CPU baseline; CFG4 / CFG5 lines with
 #      the 8-shard tile-efficiency projection)
-#   c: where the Cornell kernels wait (SQ wait / LDS / SMEM counters, gpu_pmc_cornell.sh)
+#   c: where the Cornell kernels wait (SQ wait / LDS / SMEM counters, gpu_pmc_wait.sh)
 #   ab: a, then b with a's counters installed
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
-TAG=${TAG:-r04a}
+TAG=${TAG:-r05a}
 case "${PART:-a}" in
 a)
   timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/smoke_$TAG.log 2>&1
@@ -22,12 +22,12 @@ b)
   TAG=$TAG STEPS=8 CONFIGS="${CONFIGS:-cornell cfg3 cfg4 cfg5}" bash scripts/gpu_bench_cfgs.sh || exit 1
   ;;
 c)
-  CFG=cornell TAG=$TAG bash scripts/gpu_pmc_cornell.sh || exit 1
+  CFG=cornell TAG=$TAG bash scripts/gpu_pmc_wait.sh || exit 1
   ;;
 ab)  # a, the new counters installed into this copy's profiles/ (the bench reads them), then b
-  PART=a TAG=$TAG bash scripts/gpu_final_r04.sh || exit 1
+  PART=a TAG=$TAG bash scripts/gpu_final.sh || exit 1
   for c in ${CONFIGS:-cornell cfg3 cfg4 cfg5}; do cp gpurun_out/cnt_${c}_$TAG.counters.json profiles/counters_$c.json || exit 1; done
-  PART=b TAG=$TAG bash scripts/gpu_final_r04.sh || exit 1
+  PART=b TAG=$TAG bash scripts/gpu_final.sh || exit 1
   ;;
 esac
 exit 0

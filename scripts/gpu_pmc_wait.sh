@@ -1,6 +1,6 @@
 #!/bin/bash
 # Where the Cornell (configs[1]) kernels wait: single-lane PMC passes of one bench step, each pass its own run.
-#   CFG=cornell TAG=r04a bash scripts/gpu_pmc_cornell.sh  -> gpurun_out/pmcw_<cfg>_<tag>.txt
+#   CFG=cornell TAG=r05a bash scripts/gpu_pmc_wait.sh  -> gpurun_out/pmcw_<cfg>_<tag>.txt
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
 CFG=${CFG:-cornell}; TAG=${TAG:-r04}
 B="python3 bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline --project-shards 0"

@@ -4,10 +4,13 @@ the sorted queue's sharded layout and the rewritten shard lengths.
 
 The film tests reach the sort only through its effect on traversal coherence (the results are per ray), so a
 tile-boundary slip that lost or duplicated a few rays could hide there.  The sizes here cover every code path of the
-three kernels: empty and one-item queues, the tile edges (512 items for the 9-bit ray digits, 256 for the 8-bit NEE
-digits), queues large enough that each of the 1024 blocks walks several tiles (> 524288 rays, > 262144 vertices:
-the cross-tile running count and the pipelined next-tile loads), very unbalanced shard lengths, heavy key
-duplication (stability), and the NEE sort in place.
+three kernels: empty and one-item queues, the sub-tile edges (512 items for the 9-bit ray digits, 256 for the 8-bit
+NEE digits), very unbalanced shard lengths, heavy key duplication (stability), and the NEE sort in place.  A scatter
+tile is kRsIpt x 2^RB items (4096 for the ray digits, 2048 for the NEE digits) and rs_chunk rounds ceil(n / 1024) up
+to a whole tile, so a block walks more than one tile only above 1024 x 4096 = 4.19 M rays or 1024 x 2048 = 2.10 M
+vertices: test_ray_sort_multi_tile / test_nee_sort_multi_tile cover that loop (the running per-digit count carried
+across tiles and the LDS staging arrays reused behind the tile's trailing barrier) with unbalanced shards and
+duplicated keys; 1080p bounces reach it (16 Mi-sample batches).
 """
 import numpy as np
 import pytest
@@ -92,3 +95,19 @@ def test_sort_key_widths(ctx):
     _run(ctx, 0, S, lens, 1 << 30, seed=1, bits_a=2, bits_b=2)
     _run(ctx, 0, S, lens, 1 << 30, seed=2, bits_a=4, bits_b=4)
     _run(ctx, 1, S, lens, 1 << 30, seed=3, bits_a=7)
+
+
+@pytest.mark.parametrize("key_range", [1, 16, 1 << 18])
+def test_ray_sort_multi_tile(ctx, key_range):
+    S = 600000  # (a multiple of 64) 4.5 M rays: blocks walk two tiles of 4096
+    lens = [S, S, S // 2, 1, S, S, S - 1, S]
+    assert sum(lens) > 1024 * 4096
+    _run(ctx, 0, S, lens, key_range, seed=7 + key_range)
+
+
+@pytest.mark.parametrize("key_range", [1, 16, 1 << 24])
+def test_nee_sort_multi_tile(ctx, key_range):
+    S = 360000  # 2.28 M vertices: blocks walk two tiles of 2048
+    lens = [S, S, S, 0, S, S // 3, S, S]
+    assert sum(lens) > 1024 * 2048
+    _run(ctx, 1, S, lens, key_range, seed=11 + key_range, bits_a=8)

@@ -161,3 +161,67 @@ def test_gloo_hung_peer_fails_instead_of_hanging():
             p.join(timeout=30)
     assert what != "no error"
     assert waited < 60, waited
+
+
+def _worker_frames8(rank, world, port, q):
+    """bench.py's frame geometry at N = 8: a 256-index frame, 16 indices per GPU per step (per_step = 16 N = 128), so
+    the frame loop must reduce exactly once every spp / (spp_per_step N) = 2 steps, and never in between."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from computational_ray_tracer_amd import distributed as D
+    calls = []
+    real = D.reduce_film
+
+    def counting(film, dst=0):
+        calls.append(len(steps_done))
+        return real(film, dst=dst)
+
+    D.reduce_film = counting  # FrameLoop.step calls the module's reduce_film
+    res, spp, per_gpu = (64, 32), 256, 16
+    pix = torch.from_numpy(shard_pixels(res, 16, world, rank).astype(np.int64))
+    film = torch.zeros((res[0] * res[1], 4), dtype=torch.float32)
+    loop = FrameLoop(spp, per_gpu * world, film, dst=0, keep_frames=(rank == 0))
+    steps_done, frames = [], []
+
+    def render(i0, i1, f):  # every owned pixel gains one unit per sample index of the step
+        f[pix] += float(i1 - i0)
+
+    for s in range(7):
+        loop.step(render)
+        steps_done.append(s)
+        if rank == 0 and loop.frame is not None and len(frames) < loop.frames_done:
+            frames.append(loop.frame)
+    D.reduce_film = real
+    q.put((rank, calls, loop.frames_done, loop.cursor,
+           [f.numpy().copy() for f in frames] if rank == 0 else None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_eight_ranks_reduce_once_per_frame():
+    """N = 8 (gloo): one reduce per completed 256-index frame — at steps 2, 4, 6 of 7 — on every rank, each reduced
+    frame holds every pixel exactly once x 256 indices, and with keep_frames the completed frames stay untouched."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_frames8, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, calls, done, cursor, frames = q.get(timeout=300)
+        got[r] = (calls, done, cursor, frames)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    steps_per_frame = 256 // (16 * world)
+    assert steps_per_frame == 2
+    for r in range(world):
+        calls, done, cursor, _ = got[r]
+        assert calls == [1, 3, 5], (r, calls)  # 0-based step index at which the frame completed
+        assert done == 3 and cursor == 128  # the 7th step started frame 4
+    frames = got[0][3]
+    assert len(frames) == 3
+    for f in frames:
+        assert np.all(f == 256.0)

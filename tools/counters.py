@@ -6,7 +6,10 @@ usage: tools/counters.py --config cfg3 --tag r02c --dir gpurun_out/cnt_cfg3_r02c
 The directory holds the single-lane (RTMI_LANES=1) rocprofv3 runs of `bench.py --config <config>` written by
 scripts/gpu_counters.sh: kt/ (kernel trace stats), fetch/ (FETCH_SIZE), write/ (WRITE_SIZE), sq/ (SQ_INSTS_VALU and
 the stall mix), each pass in a run of its own.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the
-bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.  Both count
+bytes of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.  The guide
+validates the doubling only for wide coalesced streaming reads, and these kernels also gather (sorted rays, slot
+records, BVH lines), so every kernel also carries the undoubled figure (`dram_bytes_per_launch_raw`): the truth lies
+between the two.  Both count
 L2 misses to the fabric (Infinity-Cache hits included), so they bound HBM bytes from above.  SQ_INSTS_VALU counts
 wave-level VALU instructions (one per wave64 instruction issued).
 """
@@ -17,7 +20,7 @@ import glob
 import json
 from pathlib import Path
 
-KERNELS = ("k_trace_closest", "k_path_shade", "k_path_shade_full", "k_path_shade_full_c1", "k_path_shade_full_c2",
+KERNELS = ("k_trace_closest", "k_trace_fallback", "k_path_shade", "k_path_shade_full", "k_path_shade_full_c1", "k_path_shade_full_c2",
            "k_bin_materials", "k_path_nee", "k_path_nee_fb", "k_path_shadow", "k_generate", "k_path_film",
            "k_ref_shade_film", "k_rs_hist", "k_rs_scatter", "k_rs_offsets", "k_rs_prep")
 # the mixed-scene shade of one bounce with material bins: the binning pass and one kernel per material class, all
@@ -70,7 +73,9 @@ def main():
     out = {"tag": a.tag, "config": a.config, "lanes": 1,
            "lib_sha16": hashlib.sha256(Path(a.lib).read_bytes()).hexdigest()[:16],
            "units": "per launch (mean over the run's dispatches); bytes; wave-level instructions",
-           "correction": "FETCH_SIZE x2 (gfx950 half-count of 16 B/lane reads), KiB -> bytes x1024",
+           "correction": "dram_bytes_per_launch: FETCH_SIZE x2 (gfx950 half-count of 16 B/lane reads) + WRITE_SIZE; "
+                         "dram_bytes_per_launch_raw: FETCH_SIZE x1 + WRITE_SIZE (the doubling is validated for wide "
+                         "coalesced reads only); KiB -> bytes x1024",
            "kernels": {}}
     for k in KERNELS:
         e = {}
@@ -78,7 +83,7 @@ def main():
             f = sum(fetch[k]) / len(fetch[k])
             w = sum(write[k]) / len(write[k])
             e.update(dispatches=len(fetch[k]), fetch_kib_raw=round(f, 1), write_kib=round(w, 1),
-                     dram_bytes_per_launch=int((2 * f + w) * 1024))
+                     dram_bytes_per_launch=int((2 * f + w) * 1024), dram_bytes_per_launch_raw=int((f + w) * 1024))
         for c, v in sq.items():
             if k in v:
                 e[c.lower() + "_per_launch"] = round(sum(v[k]) / len(v[k]), 1)
@@ -93,7 +98,7 @@ def main():
     ks = out["kernels"]
     if all(k in ks for k in SHADE_BINNED) and "k_path_shade_full" not in ks:
         e = {"parts": list(SHADE_BINNED)}
-        for f in ("dram_bytes_per_launch", "valu_insts_per_launch", "rocprof_avg_ns"):
+        for f in ("dram_bytes_per_launch", "dram_bytes_per_launch_raw", "valu_insts_per_launch", "rocprof_avg_ns"):
             if all(f in ks[k] for k in SHADE_BINNED):
                 e[f] = sum(ks[k][f] for k in SHADE_BINNED)
         if "dram_bytes_per_launch" in e and "rocprof_avg_ns" in e:
