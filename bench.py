@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--config", choices=["cornell", "cfg3", "cfg4", "cfg5"], default="cornell",
                    help="cornell = BASELINE configs[1] (the metric's workload); cfg3..cfg5 = configs[2..4]")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-single-lane", action="store_true",
+                   help="profiling runs only: skip the single-lane pass (no per-kernel roofline in the line)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     p.add_argument("--project-shards", type=int, default=8,
                    help="N=1 only: render each of the N pixel-tile shards of an N-GPU run on this GPU alone and project "
@@ -387,7 +389,7 @@ def main():
     else:
         cstat = {"status": "none: traffic / valu omitted", "loaded_lib_sha16": loaded}
     roofline, st1 = {}, None
-    if rank == 0:
+    if rank == 0 and not a.no_single_lane:
         st1, dt1 = single_lane_pass(cfg, world, rank, a.spp_per_step, a.steps)
         # multi-level scenes sort their bounce rays unless RTMI_SORT=0 (decided by the configuration, not by whether
         # the sort's stage events recorded time)
@@ -426,7 +428,7 @@ def main():
         # event spans include the other lane's kernels and are not per-stage times
         "stage_ms": ({k: round(st1[k] / a.steps, 3) for k in ("ms_generate", "ms_sort", "ms_trace", "ms_shade",
                                                                "ms_shadow", "ms_film")} | {
-            "basis": "single-lane pass, ms per step (sum <= roofline.ms_per_step_single_lane)"} if rank == 0 else None),
+            "basis": "single-lane pass, ms per step (sum <= roofline.ms_per_step_single_lane)"} if st1 else None),
         "counters": {k: st[k] for k in ("samples", "rays", "shadow_rays", "nodes_tested", "tris_tested",
                                         "shadow_nodes_tested", "shadow_tris_tested", "hits", "fallback_rays",
                                         "shadow_fallback_rays")},

@@ -455,6 +455,10 @@ struct Work {
     // concurrently and index the ring by their own global thread id
     int* ring = nullptr;
     size_t ring_cap = 0;   // ints
+    // multi-level scenes in path mode: the queue positions of the rays the trace kernel's BVH walk could not decide
+    // (TraceIO fb_pos; k_trace_fallback traces them with the reference BFS)
+    int* tfb = nullptr;
+    size_t tfb_cap = 0;    // ints
     hipStream_t stream = nullptr;  // lanes >= 1: own stream (lane 0 runs on the caller's stream)
     hipEvent_t film_done = nullptr;
 };
@@ -553,6 +557,19 @@ struct rt_ctx {
 };
 
 namespace {
+
+// RTMI_BVH_ANY = "cost/leaf" (both fields required; anything else keeps the defaults): the any-hit BVH's SAH node cost
+// and largest leaf, cost 0 = the closest-hit BVH of set 0 itself.  One parser for rt_create and rt_debug_bvh_build, so
+// the exported and the uploaded any-hit BVHs come from the same parameters.
+void parse_bvh_any(float& cost, int& leaf) {
+    const char* e = std::getenv("RTMI_BVH_ANY");
+    float ac;
+    int al;
+    if (e && std::sscanf(e, "%f/%d", &ac, &al) == 2) {
+        cost = ac;
+        leaf = std::max(1, std::min(15, al));
+    }
+}
 
 void set_error(rt_ctx* c, const std::string& msg) {
     if (c) c->err = msg;
@@ -656,6 +673,9 @@ void free_ring(Work& w) {
     if (w.ring) hipFree(w.ring);
     w.ring = nullptr;
     w.ring_cap = 0;
+    if (w.tfb) hipFree(w.tfb);
+    w.tfb = nullptr;
+    w.tfb_cap = 0;
 }
 void free_workspace(rt_ctx* c) {
     for (Work& w : c->ws) {
@@ -673,6 +693,16 @@ int ensure_ring(rt_ctx* c, Work& w) {
         HIPCHK(c, dalloc(&w.ring, need));
         w.ring_cap = need;
     }
+    return RT_OK;
+}
+// this lane's trace-fallback list (multi-level octrees, path mode): one entry per queue position at most
+int ensure_trace_fallback(rt_ctx* c, Work& w, size_t n) {
+    if (w.tfb_cap >= n) return RT_OK;
+    if (w.tfb) hipFree(w.tfb);
+    w.tfb = nullptr;
+    w.tfb_cap = 0;
+    HIPCHK(c, dalloc(&w.tfb, n));
+    w.tfb_cap = n;
     return RT_OK;
 }
 // the scene as a lane's kernels see it: its own overflow ring
@@ -1093,6 +1123,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     for (int l = 0; l < lanes; ++l) {
         if ((rc = ensure_workspace(c, c->ws[l], ncap, true))) return rc;
         if (sort_rays && (rc = ensure_sort_workspace(c, c->ws[l], ncap))) return rc;
+        if (c->dsc.qcap != 1 && (rc = ensure_trace_fallback(c, c->ws[l], ncap))) return rc;
     }
     // Cornell-like single-leaf scenes cost the same per ray: static chunks on a resident grid beat tickets there
     // (A/B 1229 vs 1106-1158 Msamples/s); multi-level octrees vary per ray by 100x: tickets (CFG3 71 -> 96)
@@ -1194,6 +1225,10 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     qv = QueueView{qc_nxt + kQLen, Sq[l], 0, nsh};
                 }
                 TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
+                if (c->dsc.qcap != 1) {  // ambiguous rays listed for k_trace_fallback (the trace holds no BFS)
+                    tio.fb_pos = w.tfb;
+                    tio.fb_len = qc_cur + kQTraceFallback;
+                }
                 BinIO bio{qv, w.hitPrim, {w.neeSlot + 3 * ncap, w.neeSlot + 4 * ncap}, qc_cur + kQBinLen};
                 if (depth == 0) { bio.rayO = cO; bio.rec = rv; }  // lean depth 0: the misses' L = 0 (BinIO)
                 static_assert(kMatClasses == 2, "bin index lists");
@@ -1209,6 +1244,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 }
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
+                if (tio.fb_pos) HIPCHK(c, launch_trace_fallback(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
                 ev_mark(c, s, ST_TRACE, e0);
                 PathIO pio{};
                 pio.lean = lean;
@@ -1572,14 +1608,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_SORT")) c->sort_rays = std::atoi(e);
     if (const char* e = std::getenv("RTMI_BVH_CI")) c->bvh_node_cost = (float)std::atof(e);
     if (const char* e = std::getenv("RTMI_BVH_LEAF")) c->bvh_max_leaf = std::max(1, std::min(15, std::atoi(e)));
-    if (const char* e = std::getenv("RTMI_BVH_ANY")) {
-        float ac = 2.f;
-        int al = 4;
-        if (std::sscanf(e, "%f/%d", &ac, &al) == 2) {
-            c->bvh_any_cost = ac;
-            c->bvh_any_leaf = std::max(1, std::min(15, al));
-        }
-    }
+    parse_bvh_any(c->bvh_any_cost, c->bvh_any_leaf);
     if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
     if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
     if (const char* e = std::getenv("RTMI_EMIT_FILTER")) c->emit_filter = std::atoi(e);
@@ -2359,8 +2388,8 @@ static int impl_rt_debug_bvh_build(const rt_scene_desc* s, int set, int* n_nodes
     if (set == kBvhAny) {  // rt_create's default (cost 2, leaves <= 4) / RTMI_BVH_ANY ("0/..": set 0's closest-hit BVH)
         float ac = 2.f;
         int al = 4;
-        if (const char* e = std::getenv("RTMI_BVH_ANY")) std::sscanf(e, "%f/%d", &ac, &al);
-        if (ac > 0) { cost = ac; leaf = std::max(1, std::min(15, al)); }
+        parse_bvh_any(ac, al);
+        if (ac > 0) { cost = ac; leaf = al; }
     }
     SceneWorld sw;
     scene_world(s, sw);

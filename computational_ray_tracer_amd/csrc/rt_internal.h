@@ -249,7 +249,9 @@ enum { kQLen = 0, kQTraceTicket = 1 * kShards * kQStride, kQShadeTicket = 2 * kS
        kQNeeFallback = 5 * kShards * kQStride,
        // material bins of a mixed multi-level scene's bounce (TraceIO bin_*): class c's shard lengths at
        // kQBinLen + c kShards kQStride, the chunk tickets of its shade kernel at kQBinTicket + c kShards kQStride
-       kQBinLen = 6 * kShards * kQStride, kQBinTicket = 8 * kShards * kQStride, kQRegion = 10 * kShards * kQStride };
+       kQBinLen = 6 * kShards * kQStride, kQBinTicket = 8 * kShards * kQStride,
+       kQTraceFallback = 10 * kShards * kQStride,  // the trace kernel's ambiguous-ray list length (TraceIO fb_len)
+       kQRegion = 11 * kShards * kQStride };
 static const int kMatClasses = 2;  // material bins: 0 Lambert or emitter (NEE), 1 mirror or dielectric
 // Shard stride of a queue of ns shards for n items (a multiple of 64, so wave chunks stay line-aligned); capacity
 // ns * S.  Single-leaf scenes (static chunks, one block append per 256 rays) keep one shard: sharding their queues
@@ -281,6 +283,11 @@ struct TraceIO {
     // stores it to so[2p], so[2p + 1] — the sorted side queue the shade kernel reads; nullptr: no sort
     const int* perm = nullptr;
     float4* so = nullptr;
+    // multi-level scenes in path mode: the trace kernel walks the BVH alone and lists the queue positions of the rays
+    // the canonical rule cannot decide here; k_trace_fallback then runs the exact BFS for them (so the
+    // trace kernel holds no BFS registers).  nullptr: the BFS runs inline (reference mode, debug entry points).
+    int* fb_pos = nullptr;
+    int* fb_len = nullptr;
 };
 
 // Material binning of a mixed multi-level scene's bounce (k_bin_materials, after the trace): every hit's queue
@@ -431,6 +438,9 @@ hipError_t launch_generate(hipStream_t st, int grid, int nS, const SampleIds& id
                            const DevSampler& smp, const DevFilm& film, const GenOut& out);
 hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
                                 unsigned long long* ctr);
+// the rays k_trace_closest listed in io.fb_pos (multi-level scenes; a small grid, the list's length read on the device)
+hipError_t launch_trace_fallback(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
+                                 unsigned long long* ctr);
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
                            int* out, unsigned long long* ctr);
 // Coherence sorts (rt_sort.hip): stable device radix sorts with no host read.  temp = sort_temp_bytes() bytes.

@@ -26,7 +26,10 @@ static constexpr int kBlock = kBlockThreads;
 static constexpr int kLeafChunk = 32;  // triangles per leaf phase of the while-while traversal (16: -5 %, 64: +-0)
 static constexpr int kLdsQ = 32;       // LDS-resident BFS group FIFO entries per lane (2 B each: 16 KB per block)
 static constexpr int kTriUnroll = 4;   // triangles per scalar-cache batch in single-leaf traversal
-static constexpr int kBvhStack = 16;   // BVH traversal stack entries per lane (child word, entry distance): 32 KB
+#ifndef RT_BVH_STACK
+#define RT_BVH_STACK 16
+#endif
+static constexpr int kBvhStack = RT_BVH_STACK;  // BVH traversal stack entries per lane (child word, entry distance): 32 KB
 // One per block, shared by every multi-level traversal call site: the BVH stacks, and — for the rare rays the BVH
 // hands to the reference BFS, after the wave's BVH loop has finished — that BFS's LDS-resident group FIFO.
 __shared__ uint2 g_bstk[kBvhStack * kBlock];
@@ -1047,6 +1050,111 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     return best;
 }
 
+// The reference BFS (Octtree_Model.h:66-127) for ONE closest-hit ray, run by a whole wave (every lane holds the same
+// ray; all 64 lanes active).  Used for the rays the BVH's canonical rule leaves ambiguous: a lane's own
+// BFS of such a ray tests ~300-600 boxes and ~500-1700 triangles one after the other (CPU counts over 11.6 M rays), a
+// single-lane chain of dependent loads of about a millisecond on the GPU, and it holds 147 VGPRs.  Here the lanes split
+// the work while the decisions stay exactly the node-by-node BFS's:
+//   - a popped group's 8 child boxes are loaded and tested by lanes 0-7 against the tMax of that moment, then visited in
+//     child order; a child whose box passed is re-tested when a leaf has shrunk tMax meanwhile (the BFS tests child k
+//     after the leaves of children < k), so each box test sees the BFS's tMax;
+//   - a leaf's triangles are tested 64 at a time against the tMax at the start of the batch, and the ones that pass
+//     are tested again, in leaf order, with the running tMax — the BFS's own test sequence, since a triangle (or box)
+//     that fails with some tMax fails with every smaller one (both tests are monotone in tMax; the canonical rule
+//     rests on the same property), so the skipped tests are exactly failing ones;
+//   - the FIFO of child groups lives in the wave's part of the BVH-stack LDS (its BVH walks are over): kCoopQ entries.
+// Returns false if the FIFO would overflow (the caller then lists the ray for k_trace_fallback's per-thread BFS).
+static constexpr int kCoopQ = kBvhStack * 128;  // ints: the wave's 64 columns of g_bstk (2 ints per uint2 entry)
+static_assert((kCoopQ & (kCoopQ - 1)) == 0, "the cooperative BFS FIFO is a power-of-two ring");
+__device__ __forceinline__ bool bfs_closest_coop(const DevScene& sc, int set, V3 o, V3 d, int& rprim, float& rb0,
+                                                 float& rb1, float& rb2, float& rt, ctr_t& nn, ctr_t& nt) {
+    const int ln = lane_id();
+    int* qb = reinterpret_cast<int*>(g_bstk) + 2 * (threadIdx.x & ~63);  // row r of the wave: qb[r * 2 kBlock + 0..127]
+    auto Q = [&](int e) -> int& { e &= kCoopQ - 1; return qb[(e >> 7) * (2 * kBlock) + (e & 127)]; };
+    const V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
+    const TriRay R = make_triray<-1>(o, d);
+    const int2* __restrict__ lr = sc.leafRange[set];
+    const float4* __restrict__ tiles = sc.tiles[set];
+    float tMax = 3.402823466e+38f;
+    int best = -1;
+    int head = 0, tail = 0;
+    ctr_t cn = 0, ct = 0;
+    auto leaf = [&](int lf, int lc) {
+        for (int base = 0; base < lc; base += 64) {
+            const int k = base + ln;
+            bool c = false;
+            if (k < lc) {
+                const float4* tp = tiles + 3 * (lf + k);
+                float b0, b1, b2, t;
+                c = tri_intersect<-1>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax;
+            }
+            uint64_t m = __ballot(c);
+            while (m) {  // the candidates in leaf order, with the running tMax (uniform: every lane the same test)
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const float4* tp = tiles + 3 * (lf + base + l);
+                const float4 A = tp[0], B = tp[1], Cc = tp[2];
+                float b0, b1, b2, t;
+                if (tri_intersect<-1>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                    best = __float_as_int(Cc.y);
+                    tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+                }
+            }
+        }
+        ct += lc;
+    };
+    bool ok = true;
+    {  // the root: a group of one
+        const float4 a = sc.nodeA[0], b = sc.nodeB[0];
+        ++cn;
+        if (box_entry(a, b, o, inv) <= tMax) {
+            const int ch = __float_as_int(a.w);
+            if (ch >= 0) {
+                if (ln == 0) Q(tail) = ch;
+                ++tail;
+            } else {
+                const int2 r = lr[0];
+                if (r.y) leaf(r.x, r.y);
+            }
+        }
+    }
+    while (head < tail) {
+        wave_lds_sync();
+        const int g = Q(head);
+        ++head;
+        float e = __builtin_inff();
+        int ch = -1;
+        if (ln < 8) {
+            const float4 a = sc.nodeA[g + ln], b = sc.nodeB[g + ln];
+            e = box_entry(a, b, o, inv);
+            ch = __float_as_int(a.w);
+        }
+        cn += 8;
+        unsigned pm = (unsigned)__ballot(ln < 8 && e <= tMax);
+        while (pm) {
+            const int i = __builtin_ctz(pm);
+            pm &= pm - 1;
+            const float ei = __shfl(e, i);
+            const int ci = __shfl(ch, i);
+            if (!(ei <= tMax)) continue;  // a leaf shrank tMax since the ballot
+            if (ci >= 0) {
+                if (tail - head >= kCoopQ) { ok = false; break; }
+                if (ln == 0) Q(tail) = ci;
+                ++tail;
+            } else {
+                const int2 r = lr[g + i];
+                if (r.y) leaf(r.x, r.y);
+            }
+        }
+        if (!ok) break;
+    }
+    wave_lds_sync();  // (the FIFO's LDS is the BVH stacks': the wave's next walks write it)
+    rprim = best;
+    nn += cn;
+    nt += ct;
+    return ok;
+}
+
 // ============================================================= fast multi-level traversal
 // The reference's unordered BFS (Octtree_Model.h:66-127) only shrinks tMax when its order happens to reach the
 // near leaf, and its answer depends on that order only through near-ties.  Multi-level scenes therefore walk an
@@ -1348,13 +1456,16 @@ __device__ __forceinline__ int traverse_any(const DevScene& sc, int set, V3 o, V
 // Multi-level scenes: the BVH walk alone (no reference-BFS fallback in the calling kernel, whose register budget it
 // would set: trace 128 VGPRs + spill with it, 106 without); amb = the canonical rule could not decide, and the caller
 // hands the ray (or its path vertex) to a kernel that runs the exact traversal.
-template <bool ANYHIT>
+// KZSPEC: waves whose rays share a dominant axis take a copy of the walk with the watertight test's permutation
+// resolved at compile time (4 copies of the walk); otherwise one copy with the permutation per lane.
+template <bool ANYHIT, bool KZSPEC = true>
 __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V3 d, float tMax, float& b0, float& b1,
                                             float& b2, float& t, ctr_t& nn, ctr_t& nt, bool& amb) {
     int kz = dominant_axis(d);
     uint64_t act = __ballot(true);
 #define RT_BVH_KZ(K) \
     return ANYHIT ? bvh_anyhit<K>(sc, set, o, d, tMax, nn, nt, amb) : bvh_closest<K>(sc, set, o, d, tMax, b0, b1, b2, t, nn, nt, amb)
+    if constexpr (!KZSPEC) RT_BVH_KZ(-1);
     if (__ballot(kz == 2) == act) RT_BVH_KZ(2);
     if (__ballot(kz == 0) == act) RT_BVH_KZ(0);
     if (__ballot(kz == 1) == act) RT_BVH_KZ(1);
@@ -1371,7 +1482,10 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 #ifndef RT_MULTI_WAVES
 #define RT_MULTI_WAVES 4
 #endif
-#define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_MULTI_WAVES)))
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES RT_MULTI_WAVES  // the multi-level closest-hit trace (variant builds)
+#endif
+#define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_TRACE_WAVES)))
 #ifndef RT_SHADE1_WAVES
 #define RT_SHADE1_WAVES 4  // the single-leaf simple-path shade (Cornell)
 #endif
@@ -1379,29 +1493,86 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 #define RT_SHADE_WAVES RT_MULTI_WAVES  // the simple-path shade (its shadow rays' any-hit walks)
 #endif
 
+// The analytic shapes after the octree's closest hit, with the running tMax (hitB = the object-space
+// point for a shape), then the hit record at queue position p.
+__device__ __forceinline__ int finish_closest(const DevScene& sc, const TraceIO& io, int p, float4 o4, float4 d4,
+                                              int prim, float b0, float b1, float b2, float t) {
+    if (sc.n_shapes) {
+        float tm = prim >= 0 ? t : 3.402823466e+38f;
+        for (int si = 0; si < sc.n_shapes; ++si) {
+            DevShape sh = ldconst(sc.shapes, si);
+            V3 ph;
+            float th;
+            if (shape_isect(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
+                prim = sc.n_tris + si; b0 = ph.x; b1 = ph.y; b2 = ph.z; t = th; tm = th;
+            }
+        }
+    }
+    io.hitB[p] = make_float4(b0, b1, b2, t);
+    io.hitPrim[p] = prim;
+    return prim;
+}
+
+#ifndef RT_D0_SLOT
+#define RT_D0_SLOT 0
+#endif
+
+// Multi-level closest-hit walks with the watertight test's permutation specialised per wave (RT_TRACE_KZ=1) or per
+// lane (0; one copy of the walk instead of four).
+#ifndef RT_TRACE_KZ
+#define RT_TRACE_KZ 1
+#endif
+
+// The reference BFS for one ambiguous closest-hit ray as a call (RT_TRACE_NOINLINE builds): its registers then do not
+// set the register allocation of the caller's BVH loop.
+struct BfsHit {
+    int prim;
+    float b0, b1, b2, t;
+    unsigned nn, nt;
+};
 template <int QCAP>
+__device__ __attribute__((noinline)) BfsHit bfs_closest_call(const DevScene& sc, int set, V3 o, V3 d) {
+    BfsHit h{};
+    ctr_t nn = 0, nt = 0;
+    h.prim = traverse<QCAP, false, -1>(sc, set, o, d, 3.402823466e+38f, h.b0, h.b1, h.b2, h.t, nn, nt);
+    h.nn = (unsigned)nn;
+    h.nt = (unsigned)nt;
+    return h;
+}
+#ifndef RT_TRACE_NOINLINE
+#define RT_TRACE_NOINLINE 0
+#endif
+
+// FBL (multi-level scenes, path mode: io.fb_pos): the BVH walk alone, the ambiguous rays listed for k_trace_fallback;
+// otherwise the reference BFS runs inline for them.
+template <int QCAP, bool FBL>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
     stage_scene<QCAP, false>(sc, io.set);
     ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
-    // one ray at queue position p: octree (BVH / BFS), then the analytic shapes with the running tMax (DESIGN.md §5;
-    // hitB = object-space point for a shape)
+    // one ray at queue position p: octree (BVH / BFS), then the analytic shapes
     auto trace_one = [&](int p, float4 o4, float4 d4) __attribute__((always_inline)) {
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
-        int prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
-                                             b0, b1, b2, t, nn, nt, nfb);
-        if (sc.n_shapes) {
-            float tm = prim >= 0 ? t : 3.402823466e+38f;
-            for (int si = 0; si < sc.n_shapes; ++si) {
-                DevShape sh = ldconst(sc.shapes, si);
-                V3 ph;
-                float th;
-                if (shape_isect(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
-                    prim = sc.n_tris + si; b0 = ph.x; b1 = ph.y; b2 = ph.z; t = th; tm = th;
+        int prim;
+        if constexpr (QCAP != 1 && FBL) {
+            bool amb = false;
+            prim = traverse_bvh<false, RT_TRACE_KZ != 0>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z),
+                                                         3.402823466e+38f, b0, b1, b2, t, nn, nt, amb);
+            if (amb) {
+                ++nfb;
+                if constexpr (RT_TRACE_NOINLINE) {
+                    const BfsHit h = bfs_closest_call<QCAP>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z));
+                    prim = h.prim; b0 = h.b0; b1 = h.b1; b2 = h.b2; t = h.t;
+                    nn += h.nn; nt += h.nt;
+                } else {  // (rare: vector atomics per lane) k_trace_fallback writes this ray's hit
+                    io.fb_pos[atomicAdd(io.fb_len, 1)] = p;
+                    return;
                 }
             }
+        } else {
+            prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
+                                             b0, b1, b2, t, nn, nt, nfb);
         }
-        io.hitB[p] = make_float4(b0, b1, b2, t);
-        io.hitPrim[p] = prim;
+        prim = finish_closest(sc, io, p, o4, d4, prim, b0, b1, b2, t);
         nh += prim >= 0;
         nr += 1;
     };
@@ -1444,7 +1615,50 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
         int j, base;
         while (tk.next(j, base)) {
             const int idx = base + lane_id();
-            if (idx < tk.len) {
+            if constexpr (FBL && QCAP != 1) {
+                // the BVH walk per lane; then the wave resolves its ambiguous rays one after the other with the
+                // wave-cooperative BFS (all lanes active), so no lane holds the per-thread BFS's registers
+                const bool live = idx < tk.len;
+                const int p = j * io.q.S + idx;
+                float4 o4 = make_float4(0, 0, 0, 0), d4 = o4;
+                float b0 = 0, b1 = 0, b2 = 0, t = 0;
+                int prim = -1;
+                bool amb = false;
+                if (live) {
+                    const int src = io.perm ? io.perm[p] : p;
+                    o4 = io.rayO[src << io.rsh];
+                    d4 = io.rayD[src << io.rsh];
+                    if (io.so) { io.so[2 * p] = o4; io.so[2 * p + 1] = d4; }
+                    prim = traverse_bvh<false, RT_TRACE_KZ != 0>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z),
+                                                                 3.402823466e+38f, b0, b1, b2, t, nn, nt, amb);
+                }
+                uint64_t am = __ballot(live && amb);
+                while (am) {
+                    const int L = __builtin_ctzll(am);
+                    am &= am - 1;
+                    const V3 oL = v3(__shfl(o4.x, L), __shfl(o4.y, L), __shfl(o4.z, L));
+                    const V3 dL = v3(__shfl(d4.x, L), __shfl(d4.y, L), __shfl(d4.z, L));
+                    int cp;
+                    float c0, c1, c2, ctt;
+                    ctr_t cnn = 0, cnt = 0;
+                    const bool ok = bfs_closest_coop(sc, io.set, oL, dL, cp, c0, c1, c2, ctt, cnn, cnt);
+                    if (lane_id() == L) {
+                        ++nfb;
+                        nn += cnn;
+                        nt += cnt;
+                        if (ok) { prim = cp; b0 = c0; b1 = c1; b2 = c2; t = ctt; amb = false; }
+                    }
+                }
+                if (live) {
+                    if (amb) {  // (FIFO overflow, practically never: k_trace_fallback's per-thread BFS)
+                        io.fb_pos[atomicAdd(io.fb_len, 1)] = p;
+                    } else {
+                        prim = finish_closest(sc, io, p, o4, d4, prim, b0, b1, b2, t);
+                        nh += prim >= 0;
+                        nr += 1;
+                    }
+                }
+            } else if (idx < tk.len) {
                 const int p = j * io.q.S + idx;
                 const int src = io.perm ? io.perm[p] : p;
                 const float4 o4 = io.rayO[src << io.rsh], d4 = io.rayD[src << io.rsh];
@@ -1459,6 +1673,30 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
     count_add(ctr, C_RAYS, nr);
     count_add(ctr, C_FALLBACK, nfb);
     if constexpr (QCAP != 1) simd_flush();
+}
+
+// The rays k_trace_closest<Q, true> listed (io.fb_pos): the reference BFS (Octtree_Model.h:66-127, exact order and
+// ties) then the shapes, on a small grid right after it.  Their rays are read where the trace kernel read them: the
+// sorted side queue it wrote (io.so) or the queue itself.
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) k_trace_fallback(DevScene sc, TraceIO io, unsigned long long* ctr) {
+    ctr_t nn = 0, nt = 0, nh = 0, nr = 0;
+    const int n = *io.fb_len;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const int p = io.fb_pos[k];
+        const float4 o4 = io.so ? io.so[2 * p] : io.rayO[p << io.rsh];
+        const float4 d4 = io.so ? io.so[2 * p + 1] : io.rayD[p << io.rsh];
+        float b0 = 0, b1 = 0, b2 = 0, t = 0;
+        int prim = traverse<QCAP, false, -1>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
+                                             b0, b1, b2, t, nn, nt);
+        prim = finish_closest(sc, io, p, o4, d4, prim, b0, b1, b2, t);
+        nh += prim >= 0;
+        nr += 1;
+    }
+    count_add(ctr, C_NODES, nn);
+    count_add(ctr, C_TRIS, nt);
+    count_add(ctr, C_HITS, nh);
+    count_add(ctr, C_RAYS, nr);
 }
 
 // Material bins of a mixed multi-level scene's bounce (BinIO): every hit's queue position is appended to the index
@@ -1725,7 +1963,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         float Ld[8];
         int slot = -1;
         if (live) {
-            slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
+            // (the ray's origin carries its slot; at depth 0 the queue is k_generate's dense camera queue, slot = k,
+            // so the slot's state loads need not wait for the ray's)
+            slot = RT_D0_SLOT && io.depth == 0 ? k : __float_as_int(io.rayO[2 * k].w);
             const int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
@@ -2039,7 +2279,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         int slot = -1;
         bool storedL = false;
         if (live) {
-            slot = __float_as_int(io.rayO[2 * k].w);  // (the ray's origin carries its slot)
+            slot = RT_D0_SLOT && io.depth == 0 ? k : __float_as_int(io.rayO[2 * k].w);  // (k_path_shade)
             int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
@@ -2459,6 +2699,10 @@ __global__ void __launch_bounds__(kBlock) k_film_scatter(int n, const int* __res
 }
 
 // ============================================================================== launch wrappers
+// The fallback passes (the few rays the BVH alone could not decide: 0-100 per launch on CFG3/CFG4) run on a small
+// grid, so their launch neither waits for nor occupies the whole GPU (a resident grid there: CFG3 +0.9 % instead of
+// the BFS-free kernels' full gain).
+static constexpr int kFallbackBlocks = 64;
 static inline int grid_for(int n, int grid) {
     int g = (n + kBlock - 1) / kBlock;
     if (grid > 0 && g > grid) g = grid;
@@ -2508,10 +2752,36 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
     int gb = grid_for(io.q.len ? grid * kBlock : io.q.n, grid);
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
     dim3 b(kBlock);
+    const bool fbl = io.fb_pos != nullptr;
+    if (fbl && (!io.fb_len || qcap == 1)) return hipErrorInvalidValue;
+#define RT_TRACE_CASE(Q)                                                                                          \
+    case Q:                                                                                                       \
+        if (fbl)                                                                                                  \
+            hipLaunchKernelGGL((k_trace_closest<Q, true>), dim3(resident_grid(k_trace_closest<Q, true>, gb, grid)), b, \
+                               0, st, sc, io, ctr);                                                               \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_trace_closest<Q, false>), dim3(resident_grid(k_trace_closest<Q, false>, gb, grid)), \
+                               b, 0, st, sc, io, ctr);                                                            \
+        break;
     switch (qcap) {
-        case 0: hipLaunchKernelGGL(k_trace_closest<0>, dim3(resident_grid(k_trace_closest<0>, gb, grid)), b, 0, st, sc, io, ctr); break;
-        case 1: hipLaunchKernelGGL(k_trace_closest<1>, dim3(resident_grid(k_trace_closest<1>, gb, grid)), b, 0, st, sc, io, ctr); break;
-        case 16: hipLaunchKernelGGL(k_trace_closest<16>, dim3(resident_grid(k_trace_closest<16>, gb, grid)), b, 0, st, sc, io, ctr); break;
+        RT_TRACE_CASE(0)
+        case 1: hipLaunchKernelGGL((k_trace_closest<1, false>), dim3(resident_grid(k_trace_closest<1, false>, gb, grid)), b, 0, st, sc, io, ctr); break;
+        RT_TRACE_CASE(16)
+        default: return hipErrorInvalidValue;
+    }
+#undef RT_TRACE_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_fallback(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
+                                 unsigned long long* ctr) {
+    if (!io.fb_pos || !io.fb_len) return hipErrorInvalidValue;
+    int gb = std::min(grid > 0 ? grid : 1, kFallbackBlocks);
+    if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);  // one ring per resident thread
+    dim3 b(kBlock);
+    switch (qcap) {
+        case 0: hipLaunchKernelGGL(k_trace_fallback<0>, dim3(resident_grid(k_trace_fallback<0>, gb, grid)), b, 0, st, sc, io, ctr); break;
+        case 16: hipLaunchKernelGGL(k_trace_fallback<16>, dim3(resident_grid(k_trace_fallback<16>, gb, grid)), b, 0, st, sc, io, ctr); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2529,10 +2799,6 @@ hipError_t launch_records(hipStream_t st, const DevScene& sc, const DevSpectra* 
     return hipGetLastError();
 }
 
-// The fallback passes (the few rays the BVH alone could not decide: 0-100 per launch on CFG3/CFG4) run on a small
-// grid, so their launch neither waits for nor occupies the whole GPU (a resident grid there: CFG3 +0.9 % instead of
-// the BFS-free kernels' full gain).
-static constexpr int kFallbackBlocks = 64;
 
 hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, const DevScene& sc, const PathIO& io,
                               const ShadowQueueIO& shq, unsigned long long* ctr) {

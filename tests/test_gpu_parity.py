@@ -300,6 +300,49 @@ def test_cfg4_mixed_film_bitexact(cfg4_small, oracle_lib, kind, depth):
     assert bad.sum() == 0, f"{bad.sum()} pixels differ; max |diff| {np.abs(fg - fo).max()}"
 
 
+@pytest.mark.parametrize("kind,depth", [("mis", 5), ("path", 2), ("mis", 1)])
+def test_emitter_filter_on_off_bitexact(monkeypatch, kind, depth):
+    """The last-depth emitter filter of mixed scenes (k_emitter_filter, RTMI_EMIT_FILTER, on by default) drops the
+    rays that can hit no emissive surface before the last trace; its correctness rests on the closest-hit test of an
+    emitter being monotone in tMax.  The film with the filter must equal the film that traces every last-depth ray,
+    bit for bit (several batches on both lanes)."""
+    from computational_ray_tracer_amd import capi
+    cfg = scene.cfg4_mixed(res=(96, 54), spp=(2, 2), frequency=16)
+    cfg.integrator = scene.Integrator(capi.RT_INTEGRATOR_PATH if kind == "path" else capi.RT_INTEGRATOR_PATH_MIS,
+                                      max_depth=depth)
+    monkeypatch.setenv("RTMI_BATCH_SAMPLES", str(96 * 54 * 2))
+    films = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("RTMI_EMIT_FILTER", on)
+        films[on] = Renderer(cfg).render_pass(0, 4)
+    bad = np.any(bits(films["1"]) != bits(films["0"]), axis=1)
+    assert bad.sum() == 0, f"{bad.sum()} pixels differ with / without the emitter filter"
+
+
+def test_many_emissive_triangles_film_bitexact(oracle_lib):
+    """More than kMaxEmitTris (64) emissive triangles: the emitter filter is disabled (DevScene n_emit_tris = -1) and
+    the last depth traces every ray; the film still matches the oracle bit for bit.  The CFG4 mesh is made emissive
+    (a Lambert material with emission, no light record: its hits count as BSDF-sampled emitter hits)."""
+    from computational_ray_tracer_amd import capi
+    cfg = scene.cfg4_mixed(res=(96, 54), spp=(2, 2), frequency=16)
+    m = cfg.model
+    mats = list(m.materials)
+    glow = len(mats)
+    mats.append((scene.CORNELL_WHITE, 3.0))
+    m.materials = mats
+    tm = np.array(m.tri_material, np.int32)
+    mesh = np.arange(len(tm)) >= 12  # the box's 12 wall triangles first, then the mesh
+    assert set(tm[:12].tolist()) == {0, 1, 2, 3} and set(tm[12:].tolist()) == {0} and mesh.sum() > 64
+    tm[mesh] = glow
+    m.tri_material = tm
+    for kind in (capi.RT_INTEGRATOR_PATH_MIS, capi.RT_INTEGRATOR_PATH):
+        cfg.integrator = scene.Integrator(kind, max_depth=3)
+        fg = Renderer(cfg).render_pass(0, 4)
+        fo = oracle_lib.OracleScene(cfg).render(0, 4)
+        bad = np.any(bits(fg) != bits(fo), axis=1)
+        assert bad.sum() == 0, f"{bad.sum()} pixels differ; max |diff| {np.abs(fg - fo).max()}"
+
+
 @pytest.mark.parametrize("cam,filt", [("ortho", "box"), ("pinhole", "gaussian"), ("thinlens", "lanczos"),
                                       ("perspective", "gaussian"), ("perspective", "triangle")])
 def test_cameras_and_filters_bitexact(oracle_lib, cam, filt):

@@ -99,7 +99,7 @@ def test_sort_key_widths(ctx):
 
 @pytest.mark.parametrize("key_range", [1, 16, 1 << 18])
 def test_ray_sort_multi_tile(ctx, key_range):
-    S = 600000  # (a multiple of 64) 4.5 M rays: blocks walk two tiles of 4096
+    S = 700032  # (a multiple of 64) 4.55 M rays: blocks walk two tiles of 4096
     lens = [S, S, S // 2, 1, S, S, S - 1, S]
     assert sum(lens) > 1024 * 4096
     _run(ctx, 0, S, lens, key_range, seed=7 + key_range)
