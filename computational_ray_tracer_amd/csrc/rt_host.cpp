@@ -443,6 +443,7 @@ struct Work {
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
     unsigned* sQKey = nullptr;  // the ray queue's sort keys at queue positions (written by the shade kernels)
     void* sTemp = nullptr;      // the sorts' histograms and meta (sort_temp_bytes)
+    int sPar = 0;               // one-sweep histogram parity of the next sort on this temp buffer (SortRaysIO parity)
     size_t sCap = 0;
     // shadow queue (multi-level octrees): {o, tMax}, {d, slot}, pending contribution (2 x float4)
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
@@ -653,7 +654,9 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
     HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1; HIPCHK(c, dalloc(&w.sS, n));
     HIPCHK(c, dalloc(&w.sVals, n)); HIPCHK(c, dalloc(&w.sValsAlt, n));
     HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n)); HIPCHK(c, dalloc(&w.sQKey, n));
-    HIPCHK(c, hipMalloc(&w.sTemp, sort_temp_bytes()));
+    HIPCHK(c, hipMalloc(&w.sTemp, sort_temp_bytes(n)));
+    HIPCHK(c, hipMemset(w.sTemp, 0, sort_temp_bytes(n)));  // (the one-sweep histograms start zeroed)
+    w.sPar = 0;
     w.sCap = n;
     return RT_OK;
 }
@@ -1181,12 +1184,13 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
             Sq[l] = shard_stride(nS, nsh);  // every queue of this batch: shard j at [j S, j S + len_j)
             SampleIds ids = sample_ids(c, b0);
             GenOut go{w.rayO, w.rayD, nullptr, nullptr, w.pdfA, w.pdfB, rv, lean, 1};
+            // camera rays fill queue 0 densely (positions 0..nS-1: QueueView without lengths); both counter regions
+            // start at zero: k_generate zeroes them (a memset launch here waited for the other lane's resident blocks
+            // in two-lane mode, r05 kernel traces)
+            go.zero = w.d_qcount;
             hipEvent_t e0 = ev_start(c, s);
             HIPCHK(c, launch_generate(s, grid, nS, ids, cam, smp, fd, go));
             ev_mark(c, s, ST_GEN, e0);
-            // camera rays fill queue 0 densely (positions 0..nS-1: QueueView without lengths); both counter regions
-            // start at zero
-            HIPCHK(c, hipMemsetAsync(w.d_qcount, 0, 2 * kQRegion * sizeof(int), s));
         }
         for (int depth = 0; depth <= c->integ.max_depth; ++depth) {
             // the last trace can only add emitter hits, which count only after specular bounces or with MIS
@@ -1201,8 +1205,12 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 const float4* cD = cO + 1;
                 int* qc_cur = w.d_qcount + kQRegion * cur[l];
                 int* qc_nxt = w.d_qcount + kQRegion * nxt;
-                // the next queue's length and the chunk tickets its trace and shade launches will use
-                HIPCHK(c, hipMemsetAsync(qc_nxt, 0, kQRegion * sizeof(int), s));
+                // the next queue's length and the chunk tickets its trace and shade launches will use start at zero:
+                // depth 0 (k_generate zeroed both regions) / the trace kernel zeroes it (below), except before the
+                // emitter filter, which appends to it ahead of the trace
+                const bool efilter0 = c->emit_filter && c->dsc.full && depth == c->integ.max_depth && depth > 0 &&
+                                      c->dsc.n_emit_tris >= 0;
+                if (efilter0) HIPCHK(c, hipMemsetAsync(qc_nxt, 0, kQRegion * sizeof(int), s));
                 hipEvent_t e0;
                 // multi-level octrees: bounce rays sorted by (octant, direction cell, origin Morton code) before
                 // the trace.  The queue length is read back so only live rays are sorted (sorting the capacity with
@@ -1225,6 +1233,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                     qv = QueueView{qc_nxt + kQLen, Sq[l], 0, nsh};
                 }
                 TraceIO tio{cO, cD, qv, 0, w.hitB, w.hitPrim, dyn ? qc_cur + kQTraceTicket : nullptr, 1};
+                if (depth > 0 && !efilter) tio.zero = qc_nxt;
                 if (c->dsc.qcap != 1) {  // ambiguous rays listed for k_trace_fallback (the trace holds no BFS)
                     tio.fb_pos = w.tfb;
                     tio.fb_len = qc_cur + kQTraceFallback;
@@ -1234,7 +1243,8 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 static_assert(kMatClasses == 2, "bin index lists");
                 if (sort_rays && depth > 0 && !efilter) {  // the device reads the queue length itself: no host read
                     SortRaysIO so{w.sQKey, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
-                                  c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l]};
+                                  c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l], w.sCap, w.sPar};
+                    w.sPar ^= 1;
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, so));
                     ev_mark(c, s, ST_SORT, e0);
@@ -1244,7 +1254,11 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 }
                 e0 = ev_start(c, s);
                 HIPCHK(c, launch_trace_closest(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
-                if (tio.fb_pos) HIPCHK(c, launch_trace_fallback(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
+                // (an ambiguous ray is listed only if the cooperative BFS's FIFO overflows, which the octree's exact
+                // queue bound excludes when coop_ok: then no launch, which in two-lane mode would wait for the other
+                // lane's resident blocks, r05 kernel traces: 1.28 ms per bounce)
+                if (tio.fb_pos && !c->dsc.coop_ok)
+                    HIPCHK(c, launch_trace_fallback(s, grid, c->dsc.qcap, dsl, tio, c->d_ctr));
                 ev_mark(c, s, ST_TRACE, e0);
                 PathIO pio{};
                 pio.lean = lean;
@@ -1300,7 +1314,8 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 ev_mark(c, s, ST_SHADE, e0);
                 if (sort_nee) {  // NEE vertices in Morton order of their shading points (no host round trip)
                     SortNeeIO so{w.neeSlot, qc_cur + kQShadowLen, Sq[l], nee_key, w.sKeys, w.sKeysAlt, w.sVals,
-                                 w.sValsAlt, w.sTemp, c->sort_nee_bits};
+                                 w.sValsAlt, w.sTemp, c->sort_nee_bits, w.sCap, w.sPar};
+                    w.sPar ^= 1;
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_nee(s, so));
                     ev_mark(c, s, ST_SORT, e0);
@@ -1308,11 +1323,14 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 if (nee) {  // this bounce's shadow rays, before the next bounce reads L
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_path_nee(s, grid, c->dsc.qcap, dsl, c->d_spec, pio, nio, c->d_ctr));
-                    if (c->dsc.qcap != 1)
+                    // (no fallback launch when k_path_nee resolves its undecided shadow rays itself, coop_ok)
+                    if (c->dsc.qcap != 1 && !c->dsc.coop_ok)
                         HIPCHK(c, launch_path_nee_fallback(s, grid, c->dsc.qcap, dsl, c->d_spec, pio, nio, c->d_ctr));
                     ev_mark(c, s, ST_SHADOW, e0);
                 }
-                if (shq) {
+                // (the deferred shadow rays are resolved in k_path_shade itself when coop_ok: no launch, which in
+                // two-lane mode waits for the other lane's resident blocks, r05 kernel traces: 0.87 ms per bounce)
+                if (shq && !(sqio.defer && c->dsc.coop_ok)) {
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_path_shadow(s, grid, c->dsc.qcap, c->shadow_dfs != 0, dsl, pio, sqio, c->d_ctr));
                     ev_mark(c, s, ST_SHADOW, e0);
@@ -2116,6 +2134,14 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     d.n_materials = (int)mats.size();
     c->scene_full = full;
     d.qcap = qcap;
+    {  // the cooperative BFS's FIFO holds 16-bit group ids (first child = 1 + 8 g) and kCoopFifo of them
+        bool ids16 = true;
+        for (int i = 0; i < nn && ids16; ++i) {
+            const int fc = ob.nodes[i].first_child;
+            if (fc >= 0 && ((fc - 1) % 8 != 0 || (fc - 1) / 8 > 65535)) ids16 = false;
+        }
+        d.coop_ok = qcap != 1 && bound <= kCoopFifo && ids16 ? 1 : 0;
+    }
     d.depth = nn < (1 << 24) ? maxd : 1 << 30;  // DFS stack entries hold 24-bit group ids
     if (qcap == 0) {  // each lane allocates its ring of ring_threads x rs ints (ensure_ring)
         int rs = 1;
@@ -2486,7 +2512,7 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
     void* temp = nullptr;
     if (dalloc(&dkey, cap) || dalloc(&dslot, cap) || dalloc(&dlen, (size_t)kShards * kQStride) || dalloc(&dout, cap) ||
         dalloc(&k0, cap) || dalloc(&k1, cap) || dalloc(&v0, cap) || dalloc(&v1, cap) ||
-        hipMalloc(&temp, sort_temp_bytes()) != hipSuccess)
+        hipMalloc(&temp, sort_temp_bytes(cap)) != hipSuccess || hipMemset(temp, 0, sort_temp_bytes(cap)) != hipSuccess)
         rc = fail(c, RT_E_OOM, "debug sort buffers");
     if (!rc) {
         std::vector<int> hlen((size_t)kShards * kQStride, 0);
@@ -2499,10 +2525,10 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
         if (e == hipSuccess) e = hipMemset(dout, 0xff, cap * 4);
         if (e == hipSuccess) {
             if (which == 0) {
-                SortRaysIO so{dkey, dout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S};
+                SortRaysIO so{dkey, dout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S, cap, 0};
                 e = launch_sort_rays(c->stream, so);
             } else {
-                SortNeeIO so{dslot, dlen, S, dkey, k0, k1, v0, v1, temp, bits_a};
+                SortNeeIO so{dslot, dlen, S, dkey, k0, k1, v0, v1, temp, bits_a, cap, 0};
                 e = launch_sort_nee(c->stream, so);
             }
         }

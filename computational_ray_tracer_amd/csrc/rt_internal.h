@@ -132,6 +132,10 @@ struct DevScene {
     unsigned long long fan_pairs[2];  // single-leaf scenes: bit k (k even) = tiles k, k+1 are a fan pair (a,b,c),(a,c,d)
     int qcap;                       // BFS group FIFO size (compiled variants); 0 = global-memory ring below
     int depth;                      // octree depth (root = 0): any-hit queries walk depth-first when <= kDfsDepth
+    // multi-level octrees: the rays the BVH leaves ambiguous are resolved in the kernel that found them by the
+    // wave-cooperative BFS (rt_kernels.hip bfs_coop), whose FIFO holds kCoopFifo 16-bit group ids; coop_ok = the
+    // octree's exact worst-case BFS queue (rt_octree_info max_queue_groups) fits it, so no fallback launch is needed
+    int coop_ok;
     int* ring;                      // qcap == 0: ring[(pos & ring_mask) * ring_threads + thread]
     int ring_mask;
     int ring_threads;               // launches with qcap == 0 are clamped to this many threads
@@ -153,7 +157,8 @@ struct DevScene {
     const int* emit_shapes;
     int n_emit_shapes;
 };
-static const int kMaxEmitTris = 64;  // emitter filter only with at most this many emissive triangles
+static const int kMaxEmitTris = 64;
+static const int kCoopFifo = 2048;   // entries of the wave-cooperative BFS's group FIFO (16-bit group ids, LDS)  // emitter filter only with at most this many emissive triangles
 
 // device counter slots (u64).  Every wave of a persistent kernel adds its totals at the end, all at about the same
 // time: one counter word per slot serialised those atomics (a fixed ~0.15 ms tail per trace launch), so each slot
@@ -231,6 +236,9 @@ struct GenOut {
                // stores no dimension either (the host derives each depth's); 2: mixed scenes (dimension, prevPdf = 0
                // and the TerminateSecondary flag 0 in R_MISC)
     int rsh = 0;  // ray k at rayO[k << rsh] / rayD[k << rsh] (1: the workspace's interleaved (o, d) pairs)
+    // path mode: the batch's two queue-counter regions (2 kQRegion ints), zeroed by this kernel instead of a memset
+    // launch (in two-lane mode every launch of a lane may wait for the other lane's resident blocks)
+    int* zero = nullptr;
 };
 
 // Ray queues are split into kShards shards, each with its own length and chunk-ticket counters: one returning
@@ -288,6 +296,9 @@ struct TraceIO {
     // trace kernel holds no BFS registers).  nullptr: the BFS runs inline (reference mode, debug entry points).
     int* fb_pos = nullptr;
     int* fb_len = nullptr;
+    // path mode, depths >= 1: the next queue's counter region (kQRegion ints), zeroed by block 0 of this kernel
+    // instead of a memset launch (no kernel of the depth touches it before the shade that appends to it)
+    int* zero = nullptr;
 };
 
 // Material binning of a mixed multi-level scene's bounce (k_bin_materials, after the trace): every hit's queue
@@ -454,8 +465,11 @@ struct SortRaysIO {
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin
     int* len;     // the queue's shard lengths (kQLen region): read, then rewritten for the sorted queue
     int S;        // shard stride (the sorted queue keeps it; its shards split the sorted order evenly)
+    size_t cap;   // items the temp buffer was sized for (sort_temp_bytes(cap))
+    int parity;   // one-sweep: which of the temp buffer's two histogram sets this sort uses (alternate per sort;
+                  // a sort zeroes the other one; the buffer starts zeroed)
 };
-size_t sort_temp_bytes();
+size_t sort_temp_bytes(size_t n);
 hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io);
 struct SortNeeIO {
     int* slot; int* len; int S;                          // the NEE queue (NeeIO slot / len), sorted in place
@@ -463,6 +477,8 @@ struct SortNeeIO {
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp;
     int org_bits;                                        // key: 3 x org_bits Morton code of the shading point
+    size_t cap;                                          // as SortRaysIO
+    int parity;
 };
 hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io);
 hipError_t launch_oct_classify(hipStream_t st, int nnodes, const float* cbox, const int* seg, const int* ent,

@@ -534,6 +534,8 @@ __device__ __forceinline__ void camera_sample(const DevCamera& cam, const DevSam
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_generate(int nS, SampleIds ids, DevCamera cam, DevSampler smp,
                                                      DevFilm film, GenOut out) {
     stage_warp_tables();
+    if (out.zero)
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * kQRegion; i += gridDim.x * blockDim.x) out.zero[i] = 0;
     const bool with_pdf = !out.lean;
     for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nS; s += gridDim.x * blockDim.x) {
         int pixel, index, x, y;
@@ -1050,11 +1052,11 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
     return best;
 }
 
-// The reference BFS (Octtree_Model.h:66-127) for ONE closest-hit ray, run by a whole wave (every lane holds the same
-// ray; all 64 lanes active).  Used for the rays the BVH's canonical rule leaves ambiguous: a lane's own
-// BFS of such a ray tests ~300-600 boxes and ~500-1700 triangles one after the other (CPU counts over 11.6 M rays), a
-// single-lane chain of dependent loads of about a millisecond on the GPU, and it holds 147 VGPRs.  Here the lanes split
-// the work while the decisions stay exactly the node-by-node BFS's:
+// The reference BFS (Octtree_Model.h:66-127) for ONE ray, run by a whole wave (every lane holds the same ray; all 64
+// lanes active).  Used for the rays the BVH's canonical rule leaves ambiguous, in the kernel that
+// found them: a lane's own BFS of such a ray tests ~300-600 boxes and ~500-1700 triangles one after the other (CPU
+// counts over 11.6 M rays), a single-lane chain of dependent loads of about a millisecond, and it holds 147 VGPRs.
+// Here the lanes split the work while the decisions stay exactly the node-by-node BFS's:
 //   - a popped group's 8 child boxes are loaded and tested by lanes 0-7 against the tMax of that moment, then visited in
 //     child order; a child whose box passed is re-tested when a leaf has shrunk tMax meanwhile (the BFS tests child k
 //     after the leaves of children < k), so each box test sees the BFS's tMax;
@@ -1062,42 +1064,68 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
 //     are tested again, in leaf order, with the running tMax — the BFS's own test sequence, since a triangle (or box)
 //     that fails with some tMax fails with every smaller one (both tests are monotone in tMax; the canonical rule
 //     rests on the same property), so the skipped tests are exactly failing ones;
-//   - the FIFO of child groups lives in the wave's part of the BVH-stack LDS (its BVH walks are over): kCoopQ entries.
-// Returns false if the FIFO would overflow (the caller then lists the ray for k_trace_fallback's per-thread BFS).
-static constexpr int kCoopQ = kBvhStack * 128;  // ints: the wave's 64 columns of g_bstk (2 ints per uint2 entry)
-static_assert((kCoopQ & (kCoopQ - 1)) == 0, "the cooperative BFS FIFO is a power-of-two ring");
-__device__ __forceinline__ bool bfs_closest_coop(const DevScene& sc, int set, V3 o, V3 d, int& rprim, float& rb0,
-                                                 float& rb1, float& rb2, float& rt, ctr_t& nn, ctr_t& nt) {
+//   - ANY (shadow rays, fixed tMax): occluded iff some reachable leaf has a passing triangle — the first one found
+//     ends the search, as it ends the BFS;
+//   - the FIFO holds 16-bit group ids (first child = 1 + 8 g) in the wave's own columns of an LDS stack array (its
+//     walks are over; other waves of the block may still be walking in theirs): kCoopFifo entries.
+// Returns false if the FIFO would overflow; the host launches no fallback kernel when the octree's exact worst-case
+// queue fits (DevScene coop_ok), so a false return then never happens.
+struct CoopFifo {
+    unsigned short* base;  // the wave's row 0
+    int row_stride;        // 16-bit words between rows
+    int shift;             // log2 of the wave's 16-bit words per row
+    __device__ __forceinline__ unsigned short& at(int e) const {
+        e &= kCoopFifo - 1;
+        return base[(e >> shift) * row_stride + (e & ((1 << shift) - 1))];
+    }
+};
+static_assert(kBvhStack * 256 >= kCoopFifo && kAnyStack * 128 >= kCoopFifo && (kCoopFifo & (kCoopFifo - 1)) == 0,
+              "the cooperative BFS FIFO fits the wave's stack columns");
+__device__ __forceinline__ CoopFifo coop_fifo_bstk() {  // g_bstk: uint2 per (row, thread)
+    return CoopFifo{reinterpret_cast<unsigned short*>(g_bstk) + 4 * (threadIdx.x & ~63u), 4 * kBlock, 8};
+}
+__device__ __forceinline__ CoopFifo coop_fifo_astk() {  // g_astk: unsigned per (row, thread)
+    return CoopFifo{reinterpret_cast<unsigned short*>(g_astk) + 2 * (threadIdx.x & ~63u), 2 * kBlock, 7};
+}
+template <bool ANY>
+__device__ __forceinline__ bool bfs_coop(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, const CoopFifo& Q,
+                                         int& rprim, float& rb0, float& rb1, float& rb2, float& rt, ctr_t& nn,
+                                         ctr_t& nt) {
     const int ln = lane_id();
-    int* qb = reinterpret_cast<int*>(g_bstk) + 2 * (threadIdx.x & ~63);  // row r of the wave: qb[r * 2 kBlock + 0..127]
-    auto Q = [&](int e) -> int& { e &= kCoopQ - 1; return qb[(e >> 7) * (2 * kBlock) + (e & 127)]; };
     const V3 inv = v3(1 / d.x, 1 / d.y, 1 / d.z);
     const TriRay R = make_triray<-1>(o, d);
     const int2* __restrict__ lr = sc.leafRange[set];
     const float4* __restrict__ tiles = sc.tiles[set];
-    float tMax = 3.402823466e+38f;
+    float tMax = tMaxInit;
     int best = -1;
     int head = 0, tail = 0;
     ctr_t cn = 0, ct = 0;
+    bool found = false;  // ANY: an occluder
     auto leaf = [&](int lf, int lc) {
-        for (int base = 0; base < lc; base += 64) {
+        for (int base = 0; base < lc && !found; base += 64) {
             const int k = base + ln;
             bool c = false;
+            float b0, b1, b2, t;
             if (k < lc) {
                 const float4* tp = tiles + 3 * (lf + k);
-                float b0, b1, b2, t;
                 c = tri_intersect<-1>(R, tMax, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMax;
             }
             uint64_t m = __ballot(c);
-            while (m) {  // the candidates in leaf order, with the running tMax (uniform: every lane the same test)
-                const int l = __builtin_ctzll(m);
-                m &= m - 1;
-                const float4* tp = tiles + 3 * (lf + base + l);
-                const float4 A = tp[0], B = tp[1], Cc = tp[2];
-                float b0, b1, b2, t;
-                if (tri_intersect<-1>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
-                    best = __float_as_int(Cc.y);
-                    tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+            if constexpr (ANY) {
+                if (m) {
+                    found = true;
+                    best = __shfl(c ? __float_as_int(tiles[3 * (lf + k) + 2].y) : 0, __builtin_ctzll(m));
+                }
+            } else {
+                while (m) {  // the candidates in leaf order, with the running tMax (uniform: every lane the same test)
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const float4* tp = tiles + 3 * (lf + base + l);
+                    const float4 A = tp[0], B = tp[1], Cc = tp[2];
+                    if (tri_intersect<-1>(R, tMax, A, B, Cc, b0, b1, b2, t) && t < tMax) {
+                        best = __float_as_int(Cc.y);
+                        tMax = t; rb0 = b0; rb1 = b1; rb2 = b2; rt = t;
+                    }
                 }
             }
         }
@@ -1110,7 +1138,7 @@ __device__ __forceinline__ bool bfs_closest_coop(const DevScene& sc, int set, V3
         if (box_entry(a, b, o, inv) <= tMax) {
             const int ch = __float_as_int(a.w);
             if (ch >= 0) {
-                if (ln == 0) Q(tail) = ch;
+                if (ln == 0) Q.at(tail) = (unsigned short)((ch - 1) >> 3);
                 ++tail;
             } else {
                 const int2 r = lr[0];
@@ -1118,9 +1146,9 @@ __device__ __forceinline__ bool bfs_closest_coop(const DevScene& sc, int set, V3
             }
         }
     }
-    while (head < tail) {
+    while (head < tail && !found) {
         wave_lds_sync();
-        const int g = Q(head);
+        const int g = 8 * (int)Q.at(head) + 1;
         ++head;
         float e = __builtin_inff();
         int ch = -1;
@@ -1131,15 +1159,15 @@ __device__ __forceinline__ bool bfs_closest_coop(const DevScene& sc, int set, V3
         }
         cn += 8;
         unsigned pm = (unsigned)__ballot(ln < 8 && e <= tMax);
-        while (pm) {
+        while (pm && !found) {
             const int i = __builtin_ctz(pm);
             pm &= pm - 1;
             const float ei = __shfl(e, i);
             const int ci = __shfl(ch, i);
-            if (!(ei <= tMax)) continue;  // a leaf shrank tMax since the ballot
+            if (!ANY && !(ei <= tMax)) continue;  // a leaf shrank tMax since the ballot
             if (ci >= 0) {
-                if (tail - head >= kCoopQ) { ok = false; break; }
-                if (ln == 0) Q(tail) = ci;
+                if (tail - head >= kCoopFifo) { ok = false; break; }
+                if (ln == 0) Q.at(tail) = (unsigned short)((ci - 1) >> 3);
                 ++tail;
             } else {
                 const int2 r = lr[g + i];
@@ -1148,7 +1176,7 @@ __device__ __forceinline__ bool bfs_closest_coop(const DevScene& sc, int set, V3
         }
         if (!ok) break;
     }
-    wave_lds_sync();  // (the FIFO's LDS is the BVH stacks': the wave's next walks write it)
+    wave_lds_sync();  // (the FIFO's LDS is the walks' stacks: the wave's next walks write it)
     rprim = best;
     nn += cn;
     nt += ct;
@@ -1548,6 +1576,8 @@ __device__ __attribute__((noinline)) BfsHit bfs_closest_call(const DevScene& sc,
 template <int QCAP, bool FBL>
 __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(DevScene sc, TraceIO io, unsigned long long* ctr) {
     stage_scene<QCAP, false>(sc, io.set);
+    if (io.zero && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < kQRegion; i += blockDim.x) io.zero[i] = 0;
     ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
     // one ray at queue position p: octree (BVH / BFS), then the analytic shapes
     auto trace_one = [&](int p, float4 o4, float4 d4) __attribute__((always_inline)) {
@@ -1641,7 +1671,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                     int cp;
                     float c0, c1, c2, ctt;
                     ctr_t cnn = 0, cnt = 0;
-                    const bool ok = bfs_closest_coop(sc, io.set, oL, dL, cp, c0, c1, c2, ctt, cnn, cnt);
+                    const bool ok = bfs_coop<false>(sc, io.set, oL, dL, 3.402823466e+38f, coop_fifo_bstk(), cp, c0, c1,
+                                                    c2, ctt, cnn, cnt);
                     if (lane_id() == L) {
                         ++nfb;
                         nn += cnn;
@@ -2076,21 +2107,45 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         // Multi-level octrees: the BVH alone; a ray it cannot decide goes to the shadow queue with its pending
         // contribution (k_path_shadow runs the exact traversal and adds it in the same order).
         bool deferShadow = false;
+        int hit = -1;
         if (wantShadow) {
             float b0, b1, b2, t;
-            int hit;
             if constexpr (QCAP != 1) hit = traverse_bvh<true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt, deferShadow);
             else hit = traverse_any<QCAP, true>(sc, 0, so, sd, stmax, b0, b1, b2, t, snn, snt, sfb);
-            if (!deferShadow) {
-                ++nsh;
-                if (hit < 0) {
-                    float L[8];
-                    rload8_or_zero(io.rec, slot, R_L, L, d0);
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) L[i] += Ld[i];
-                    rstore8(io.rec, slot, R_L, L);
-                    storedL = true;
+        }
+        if constexpr (QCAP != 1) {
+            // the shadow rays the BVH could not decide: the wave resolves them one at a time with the cooperative
+            // any-hit BFS (exact), so no k_path_shadow launch follows when the octree's queue bound fits its FIFO
+            if (shq.defer && sc.coop_ok) {
+                uint64_t am = __ballot(deferShadow);
+                while (am) {
+                    const int Ls = __builtin_ctzll(am);
+                    am &= am - 1;
+                    const V3 oL = v3(__shfl(so.x, Ls), __shfl(so.y, Ls), __shfl(so.z, Ls));
+                    const V3 dL = v3(__shfl(sd.x, Ls), __shfl(sd.y, Ls), __shfl(sd.z, Ls));
+                    int cp;
+                    float c0, c1, c2, ct;
+                    ctr_t cnn = 0, cnt = 0;
+                    bfs_coop<true>(sc, 0, oL, dL, __shfl(stmax, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct, cnn, cnt);
+                    if (lane_id() == Ls) {
+                        hit = cp;
+                        deferShadow = false;
+                        ++sfb;
+                        snn += cnn;
+                        snt += cnt;
+                    }
                 }
+            }
+        }
+        if (wantShadow && !deferShadow) {
+            ++nsh;
+            if (hit < 0) {
+                float L[8];
+                rload8_or_zero(io.rec, slot, R_L, L, d0);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) L[i] += Ld[i];
+                rstore8(io.rec, slot, R_L, L);
+                storedL = true;
             }
         }
         if constexpr (QCAP != 1) {
@@ -2483,11 +2538,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
 // tMax, then the analytic shapes: scene_occluded), then L += ((x (Le D65(λ))) wgt) for the visible lights in the
 // same order — the inline loop's arithmetic term for term.  Only the shadow rays and L are live here.
 // scene_occluded over the BVH alone (multi-level octrees): amb = the canonical rule could not decide
-__device__ __forceinline__ bool scene_occluded_bvh(const DevScene& sc, V3 o, V3 d, float tmax, ctr_t& nn, ctr_t& nt,
-                                                   bool& amb) {
-    float b0, b1, b2, t;
-    if (traverse_bvh<true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt, amb) >= 0) return true;
-    if (amb) return false;
+__device__ __forceinline__ bool shapes_occluded(const DevScene& sc, V3 o, V3 d, float tmax) {
     for (int si = 0; si < sc.n_shapes; ++si) {
         DevShape sh = ldconst(sc.shapes, si);
         V3 ph;
@@ -2495,6 +2546,13 @@ __device__ __forceinline__ bool scene_occluded_bvh(const DevScene& sc, V3 o, V3 
         if (shape_isect(sh, o, d, tmax, ph, th)) return true;
     }
     return false;
+}
+__device__ __forceinline__ bool scene_occluded_bvh(const DevScene& sc, V3 o, V3 d, float tmax, ctr_t& nn, ctr_t& nt,
+                                                   bool& amb) {
+    float b0, b1, b2, t;
+    if (traverse_bvh<true>(sc, 0, o, d, tmax, b0, b1, b2, t, nn, nt, amb) >= 0) return true;
+    if (amb) return false;
+    return shapes_occluded(sc, o, d, tmax);
 }
 
 // FB = false: the NEE queue.  On multi-level octrees a vertex with a shadow ray the BVH alone cannot decide is not
@@ -2515,8 +2573,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     // the throughput of the continued path (NeeIO)
     const float InvPi = 0.31830988618379067154f;
     const int nuv4 = (nl + 1) / 2;
-    auto vertex = [&](int slot) __attribute__((always_inline)) {
-        const float4* r = nee.rec + (size_t)slot * nf4;
+    // COOP (multi-level NEE queue): every lane of the wave calls vertex() in step (live = it has a vertex), so the
+    // light loop reconverges after each light and the wave resolves the shadow rays the BVH could not decide with the
+    // cooperative any-hit BFS (exact) instead of listing their vertices for k_path_nee<Q, true> (no fallback launch
+    // when the octree's queue bound fits its FIFO, DevScene coop_ok)
+    constexpr bool COOP = QCAP != 1 && !FB;
+    auto vertex = [&](int slot, bool live) __attribute__((always_inline)) {
+        const float4* r = nee.rec + (size_t)(live ? slot : 0) * nf4;  // (not live: slot 0's record, unused)
         const float4 p4 = r[N_PO];
         const V3 po = v3(p4.x, p4.y, p4.z);
         const unsigned tag = __float_as_uint(p4.w);
@@ -2526,18 +2589,42 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         ctr_t nv = 0;
         bool defer = false;
         for (int li = 0; li < nl; ++li) {
-            if (wg[li] < 0) continue;  // light not sampled (cos <= 0)
-            ++nv;
-            const LightRay lr = light_ray(ldconst(sc.lights, li), po, uv[2 * li], uv[2 * li + 1]);
-            bool occ;
-            if constexpr (QCAP != 1 && !FB) {
-                occ = scene_occluded_bvh(sc, po, lr.wi, lr.tmax, snn, snt, defer);
-                if (defer) break;
-            } else {
-                occ = scene_occluded<QCAP>(sc, po, lr.wi, lr.tmax, snn, snt, sfb);
+            const bool act = live && !defer && wg[li] >= 0;  // (wg < 0: light not sampled, cos <= 0)
+            bool occ = false, amb = false;
+            LightRay lr{};
+            if (act) {
+                ++nv;
+                lr = light_ray(ldconst(sc.lights, li), po, uv[2 * li], uv[2 * li + 1]);
+                if constexpr (COOP) occ = scene_occluded_bvh(sc, po, lr.wi, lr.tmax, snn, snt, amb);
+                else occ = scene_occluded<QCAP>(sc, po, lr.wi, lr.tmax, snn, snt, sfb);
             }
-            if (!occ) vis |= 1ull << li;
+            if constexpr (COOP) {
+                if (sc.coop_ok) {
+                    uint64_t am = __ballot(amb);
+                    while (am) {
+                        const int Ls = __builtin_ctzll(am);
+                        am &= am - 1;
+                        const V3 oL = v3(__shfl(po.x, Ls), __shfl(po.y, Ls), __shfl(po.z, Ls));
+                        const V3 dL = v3(__shfl(lr.wi.x, Ls), __shfl(lr.wi.y, Ls), __shfl(lr.wi.z, Ls));
+                        int cp;
+                        float c0, c1, c2, ct;
+                        ctr_t cnn = 0, cnt = 0;
+                        bfs_coop<true>(sc, 0, oL, dL, __shfl(lr.tmax, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct, cnn,
+                                       cnt);
+                        if (lane_id() == Ls) {  // the octree's answer, then the analytic shapes (scene_occluded_bvh)
+                            occ = cp >= 0 || shapes_occluded(sc, po, lr.wi, lr.tmax);
+                            amb = false;
+                            ++sfb;
+                            snn += cnn;
+                            snt += cnt;
+                        }
+                    }
+                }
+                if (amb) defer = true;  // (coop_ok == 0: the vertex goes to k_path_nee<Q, true>)
+            }
+            if (act && !defer && !occ) vis |= 1ull << li;
         }
+        if (!live) return;
         if (defer) {  // (rare: vector atomics per lane)
             nee.fb_slot[atomicAdd(nee.fb_len, 1)] = slot;
             return;
@@ -2584,15 +2671,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     };
     if constexpr (FB) {
         const int n = *nee.fb_len;
-        for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) vertex(nee.fb_slot[k]);
+        for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+            vertex(nee.fb_slot[k], true);
     } else {
         const QueueView q{nee.len, io.q.S, 0, io.q.ns};
         std::conditional_t<QCAP == 1, QueueItemsOne, QueueItems<QCAP != 1>> items(nee.ticket, q);
         int qj, qidx;
         bool live;
         while (items.next(qj, qidx, live)) {
-            if (!live) continue;  // (no block-level synchronisation in this kernel)
-            vertex(nee.slot[qj * q.S + qidx]);
+            if constexpr (COOP) {  // (wave tickets: the wave's lanes step together)
+                vertex(live ? nee.slot[qj * q.S + qidx] : 0, live);
+            } else {
+                if (!live) continue;  // (no block-level synchronisation in this kernel)
+                vertex(nee.slot[qj * q.S + qidx], true);
+            }
         }
     }
     count_add(ctr, C_SNODES, snn);
