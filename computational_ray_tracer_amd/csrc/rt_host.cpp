@@ -443,7 +443,6 @@ struct Work {
     unsigned *sKeys = nullptr, *sKeysAlt = nullptr;
     unsigned* sQKey = nullptr;  // the ray queue's sort keys at queue positions (written by the shade kernels)
     void* sTemp = nullptr;      // the sorts' histograms and meta (sort_temp_bytes)
-    int sPar = 0;               // one-sweep histogram parity of the next sort on this temp buffer (SortRaysIO parity)
     size_t sCap = 0;
     // shadow queue (multi-level octrees): {o, tMax}, {d, slot}, pending contribution (2 x float4)
     float4 *shO = nullptr, *shD = nullptr, *shLA = nullptr, *shLB = nullptr;
@@ -654,9 +653,7 @@ int ensure_sort_workspace(rt_ctx* c, Work& w, size_t n) {
     HIPCHK(c, dalloc(&w.sO, 2 * n)); w.sD = w.sO + 1; HIPCHK(c, dalloc(&w.sS, n));
     HIPCHK(c, dalloc(&w.sVals, n)); HIPCHK(c, dalloc(&w.sValsAlt, n));
     HIPCHK(c, dalloc(&w.sKeys, n)); HIPCHK(c, dalloc(&w.sKeysAlt, n)); HIPCHK(c, dalloc(&w.sQKey, n));
-    HIPCHK(c, hipMalloc(&w.sTemp, sort_temp_bytes(n)));
-    HIPCHK(c, hipMemset(w.sTemp, 0, sort_temp_bytes(n)));  // (the one-sweep histograms start zeroed)
-    w.sPar = 0;
+    HIPCHK(c, hipMalloc(&w.sTemp, sort_temp_bytes()));
     w.sCap = n;
     return RT_OK;
 }
@@ -1243,8 +1240,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 static_assert(kMatClasses == 2, "bin index lists");
                 if (sort_rays && depth > 0 && !efilter) {  // the device reads the queue length itself: no host read
                     SortRaysIO so{w.sQKey, w.sS, w.sKeys, w.sKeysAlt, w.sVals, w.sValsAlt, w.sTemp,
-                                  c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l], w.sCap, w.sPar};
-                    w.sPar ^= 1;
+                                  c->sort_dir_bits, c->sort_org_bits, qc_cur + kQLen, Sq[l]};
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_rays(s, so));
                     ev_mark(c, s, ST_SORT, e0);
@@ -1314,8 +1310,7 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
                 ev_mark(c, s, ST_SHADE, e0);
                 if (sort_nee) {  // NEE vertices in Morton order of their shading points (no host round trip)
                     SortNeeIO so{w.neeSlot, qc_cur + kQShadowLen, Sq[l], nee_key, w.sKeys, w.sKeysAlt, w.sVals,
-                                 w.sValsAlt, w.sTemp, c->sort_nee_bits, w.sCap, w.sPar};
-                    w.sPar ^= 1;
+                                 w.sValsAlt, w.sTemp, c->sort_nee_bits};
                     e0 = ev_start(c, s);
                     HIPCHK(c, launch_sort_nee(s, so));
                     ev_mark(c, s, ST_SORT, e0);
@@ -2512,7 +2507,7 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
     void* temp = nullptr;
     if (dalloc(&dkey, cap) || dalloc(&dslot, cap) || dalloc(&dlen, (size_t)kShards * kQStride) || dalloc(&dout, cap) ||
         dalloc(&k0, cap) || dalloc(&k1, cap) || dalloc(&v0, cap) || dalloc(&v1, cap) ||
-        hipMalloc(&temp, sort_temp_bytes(cap)) != hipSuccess || hipMemset(temp, 0, sort_temp_bytes(cap)) != hipSuccess)
+        hipMalloc(&temp, sort_temp_bytes()) != hipSuccess)
         rc = fail(c, RT_E_OOM, "debug sort buffers");
     if (!rc) {
         std::vector<int> hlen((size_t)kShards * kQStride, 0);
@@ -2525,10 +2520,10 @@ static int impl_rt_debug_sort(rt_ctx* c, int which, int S, const int32_t* shard_
         if (e == hipSuccess) e = hipMemset(dout, 0xff, cap * 4);
         if (e == hipSuccess) {
             if (which == 0) {
-                SortRaysIO so{dkey, dout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S, cap, 0};
+                SortRaysIO so{dkey, dout, k0, k1, v0, v1, temp, bits_a, bits_b, dlen, S};
                 e = launch_sort_rays(c->stream, so);
             } else {
-                SortNeeIO so{dslot, dlen, S, dkey, k0, k1, v0, v1, temp, bits_a, cap, 0};
+                SortNeeIO so{dslot, dlen, S, dkey, k0, k1, v0, v1, temp, bits_a};
                 e = launch_sort_nee(c->stream, so);
             }
         }

@@ -465,11 +465,8 @@ struct SortRaysIO {
     int dir_bits, org_bits;                               // key: octant, 2 x dir_bits direction, 3 x org_bits origin
     int* len;     // the queue's shard lengths (kQLen region): read, then rewritten for the sorted queue
     int S;        // shard stride (the sorted queue keeps it; its shards split the sorted order evenly)
-    size_t cap;   // items the temp buffer was sized for (sort_temp_bytes(cap))
-    int parity;   // one-sweep: which of the temp buffer's two histogram sets this sort uses (alternate per sort;
-                  // a sort zeroes the other one; the buffer starts zeroed)
 };
-size_t sort_temp_bytes(size_t n);
+size_t sort_temp_bytes();
 hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io);
 struct SortNeeIO {
     int* slot; int* len; int S;                          // the NEE queue (NeeIO slot / len), sorted in place
@@ -477,8 +474,6 @@ struct SortNeeIO {
     unsigned* keys; unsigned* keys_alt; int* vals; int* vals_alt;
     void* temp;
     int org_bits;                                        // key: 3 x org_bits Morton code of the shading point
-    size_t cap;                                          // as SortRaysIO
-    int parity;
 };
 hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io);
 hipError_t launch_oct_classify(hipStream_t st, int nnodes, const float* cbox, const int* seg, const int* ent,

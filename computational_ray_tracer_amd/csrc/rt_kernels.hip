@@ -1541,10 +1541,6 @@ __device__ __forceinline__ int finish_closest(const DevScene& sc, const TraceIO&
     return prim;
 }
 
-#ifndef RT_D0_SLOT
-#define RT_D0_SLOT 0
-#endif
-
 // Multi-level closest-hit walks with the watertight test's permutation specialised per wave (RT_TRACE_KZ=1) or per
 // lane (0; one copy of the walk instead of four).
 #ifndef RT_TRACE_KZ
@@ -1996,7 +1992,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         if (live) {
             // (the ray's origin carries its slot; at depth 0 the queue is k_generate's dense camera queue, slot = k,
             // so the slot's state loads need not wait for the ray's)
-            slot = RT_D0_SLOT && io.depth == 0 ? k : __float_as_int(io.rayO[2 * k].w);
+            slot = io.depth == 0 ? k : __float_as_int(io.rayO[2 * k].w);
             const int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
@@ -2334,7 +2330,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         int slot = -1;
         bool storedL = false;
         if (live) {
-            slot = RT_D0_SLOT && io.depth == 0 ? k : __float_as_int(io.rayO[2 * k].w);  // (k_path_shade)
+            slot = io.depth == 0 ? k : __float_as_int(io.rayO[2 * k].w);  // (as k_path_shade)
             int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];

@@ -288,238 +288,6 @@ __global__ void __launch_bounds__(1 << RB) k_rs_scatter(RsPass p) {
     }
 }
 
-// ---------------------------------------------------------------------------------------------------------------
-// One-sweep form (Adinets & Merrill 2022, decoupled look-back): the digit counts of every pass are taken in ONE read
-// of the keys up front (k_os_hist: global per-pass histograms, plus the status words zeroed), then each pass is ONE
-// kernel (k_os_pass): tiles are claimed in order from a counter, a tile publishes its per-digit count, looks back over
-// the tiles before it for its exclusive per-digit prefix (thread d spins on digit d's status words until it meets an
-// inclusive one), publishes its inclusive prefix and scatters exactly as k_rs_scatter does (stable: tiles in order,
-// items ranked in order within a tile).  1 + passes launches per sort instead of 1 + 3 passes: in two-lane mode every
-// launch of a lane can wait for the other lane's resident blocks (r05 kernel traces), and the per-pass histogram
-// reads go.  A tile's status word: bits 30-31 the flag (0 not ready, 1 its own count, 2 the inclusive prefix), bits
-// 0-29 the count.  The global histograms and tile counters alternate between two parities per temp buffer: a sort
-// zeroes the other parity's (the next sort accumulates into it), the status words are zeroed by k_os_hist.
-#ifndef RT_RS_ONESWEEP
-#define RT_RS_ONESWEEP 1
-#endif
-constexpr int kOsMaxPasses = 4;
-constexpr unsigned kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsCount = (1u << 30) - 1u;
-constexpr int kOsMinTile = kRsIpt * 256;  // the smallest tile (8-bit digits): sizes the status array
-struct OsTemp {
-    int* meta;          // [0] n, [1 .. kShards + 1] the shard prefix (as k_rs_prep)
-    int* ghist;         // [parity][pass][kRsBinsMax]
-    int* tiles;         // [parity][pass] tile counters (one per 64-B line)
-    unsigned* status;   // [pass][tile][1 << RB]
-    int max_tiles;      // tiles the status array holds per pass
-};
-__host__ __device__ inline size_t os_meta_ints() { return 64; }
-__host__ __device__ inline size_t os_ghist_ints() { return 2 * (size_t)kOsMaxPasses * kRsBinsMax; }
-__host__ __device__ inline size_t os_tile_ints() { return 2 * (size_t)kOsMaxPasses * 16; }
-inline int os_max_tiles(size_t n) { return (int)((n + kOsMinTile - 1) / kOsMinTile) + 1; }
-OsTemp os_temp(void* temp, size_t cap) {
-    OsTemp o;
-    int* b = static_cast<int*>(temp);
-    o.meta = b;
-    o.ghist = b + os_meta_ints();
-    o.tiles = o.ghist + os_ghist_ints();
-    o.status = reinterpret_cast<unsigned*>(o.tiles + os_tile_ints());
-    o.max_tiles = os_max_tiles(cap);
-    return o;
-}
-
-// every block: the shard prefix in LDS (block 0 also to meta), the status words of this sort zeroed, and the digit
-// counts of every pass over a grid-stride share of the items, added to the sort's global histograms
-template <int SRC, int RB>
-__global__ void __launch_bounds__(1 << RB) k_os_hist(RsPass p, OsTemp o, int par, int passes, int per, int bits) {
-    constexpr int kRsBins = 1 << RB, kRsThreads = kRsBins, kTile = kRsIpt * kRsThreads;
-    __shared__ int h[kOsMaxPasses][kRsBins];
-    __shared__ int lmeta[2 + kShards];
-    const int tid = threadIdx.x;
-    if (tid == 0) {
-        int q = 0;
-        for (int j = 0; j < kShards; ++j) {
-            lmeta[1 + j] = q;
-            q += p.len[j * kQStride];
-        }
-        lmeta[1 + kShards] = q;
-        lmeta[0] = q;
-    }
-    for (int i = 0; i < kOsMaxPasses; ++i) h[i][tid] = 0;
-    __syncthreads();
-    const int n = lmeta[0];
-    if (blockIdx.x == 0 && tid < 2 + kShards) o.meta[tid] = lmeta[tid];
-    // the status words the passes will use: ceil(n / kTile) tiles per pass (a pass's array has max_tiles rows)
-    const size_t nrow = (size_t)((n + kTile - 1) / kTile) * kRsBins;
-    for (int i = 0; i < passes; ++i) {
-        unsigned* st = o.status + (size_t)i * o.max_tiles * kRsBins;
-        for (size_t k = (size_t)blockIdx.x * kRsThreads + tid; k < nrow; k += (size_t)gridDim.x * kRsThreads) st[k] = 0u;
-    }
-    RsPass q = p;
-    q.meta = lmeta;
-    for (int k = blockIdx.x * kRsThreads + tid; k < n; k += gridDim.x * kRsThreads) {
-        unsigned key;
-        int val;
-        rs_load<SRC>(q, k, key, val);
-        for (int i = 0; i < passes; ++i) {
-            const int sh = i * per, nb = bits - sh < per ? bits - sh : per;
-            atomicAdd(&h[i][(key >> sh) & ((1u << nb) - 1u)], 1);
-        }
-    }
-    __syncthreads();
-    for (int i = 0; i < passes; ++i)
-        if (h[i][tid]) atomicAdd(&o.ghist[((size_t)par * kOsMaxPasses + i) * kRsBinsMax + tid], h[i][tid]);
-}
-
-template <int SRC, int DST, int RB>
-__global__ void __launch_bounds__(1 << RB) k_os_pass(RsPass p, OsTemp o, int par, int pass) {
-    constexpr int kRsBins = 1 << RB, kRsThreads = kRsBins, kRsTile = kRsIpt * kRsThreads;
-    constexpr int NW = kRsThreads / 64;
-    __shared__ int wcnt[NW][kRsBins];
-    __shared__ int wpre[NW][kRsBins];
-    __shared__ unsigned skey[kRsTile];
-    __shared__ int sval[kRsTile];
-    __shared__ int dstart[kRsBins];  // tile-local start of digit d (the tile in digit order)
-    __shared__ int rstart[kRsBins];  // destination of digit d's first item of the tile
-    __shared__ int gstart[kRsBins];  // the digit's first destination in the whole output
-    __shared__ int wsum[NW];
-    __shared__ int s_tile;
-    const int n = p.meta[0];
-    const int ntiles = (n + kRsTile - 1) / kRsTile;
-    const int tid = threadIdx.x, w = tid >> 6, lane = rs_lane();
-    const unsigned mask = (1u << p.nbits) - 1u;
-    int* tctr = o.tiles + ((size_t)par * kOsMaxPasses + pass) * 16;
-    if (blockIdx.x == 0 && pass == 0) {  // the next sort's histograms and tile counters (the other parity)
-        const int q = par ^ 1;
-        for (int i = tid; i < kOsMaxPasses * kRsBinsMax; i += kRsThreads) o.ghist[(size_t)q * kOsMaxPasses * kRsBinsMax + i] = 0;
-        if (tid < kOsMaxPasses) o.tiles[((size_t)q * kOsMaxPasses + tid) * 16] = 0;
-    }
-    {  // the digits' first destinations: exclusive scan of this pass's global counts (Hillis-Steele in wpre[0])
-        int* sc = wpre[0];
-        const int v = o.ghist[((size_t)par * kOsMaxPasses + pass) * kRsBinsMax + tid];
-        sc[tid] = v;
-        __syncthreads();
-        for (int off = 1; off < kRsBins; off <<= 1) {
-            const int y = tid >= off ? sc[tid - off] : 0;
-            __syncthreads();
-            sc[tid] += y;
-            __syncthreads();
-        }
-        gstart[tid] = sc[tid] - v;
-    }
-    const int S2 = shard_stride(n, kShards);  // the sorted queue: item k' at shard k' / S2
-    if (DST != DST_ARRAY && blockIdx.x == 0 && tid < kShards) {
-        const int cc = n - tid * S2;
-        p.len[tid * kQStride] = cc < 0 ? 0 : (cc > S2 ? S2 : cc);
-    }
-    const uint64_t lt = (1ull << lane) - 1ull;
-    unsigned* st = o.status + (size_t)pass * o.max_tiles * kRsBins;
-    while (true) {
-        __syncthreads();
-        if (tid == 0) s_tile = atomicAdd(tctr, 1);
-        __syncthreads();
-        const int t = s_tile;
-        if (t >= ntiles) break;
-        const int t0 = t * kRsTile, b1 = min(t0 + kRsTile, n);
-        unsigned key[kRsIpt];
-        int val[kRsIpt], dst[kRsIpt];
-#pragma unroll
-        for (int j = 0; j < kRsIpt; ++j) {
-            const int k = t0 + j * kRsThreads + tid;
-            key[j] = 0;
-            val[j] = 0;
-            if (k < b1) rs_load<SRC>(p, k, key[j], val[j]);
-        }
-        int run = 0;  // digit tid's items of this tile so far
-#pragma unroll
-        for (int j = 0; j < kRsIpt; ++j) {
-            const bool valid = t0 + j * kRsThreads + tid < b1;
-            const unsigned dg = (key[j] >> p.shift) & mask;
-            uint64_t m = __ballot(valid);
-            for (int bit = 0; bit < p.nbits; ++bit) {
-                const uint64_t bb = __ballot((dg >> bit) & 1u);
-                m &= ((dg >> bit) & 1u) ? bb : ~bb;
-            }
-            const int rank = __popcll(m & lt);
-#pragma unroll
-            for (int i = 0; i < NW; ++i) wcnt[i][tid] = 0;
-            lds_barrier();
-            if (valid && rank == 0) wcnt[w][dg] = __popcll(m);
-            lds_barrier();
-            {
-                int r = run;
-#pragma unroll
-                for (int i = 0; i < NW; ++i) {
-                    wpre[i][tid] = r;
-                    r += wcnt[i][tid];
-                }
-                run = r;
-            }
-            lds_barrier();
-            dst[j] = valid ? wpre[w][dg] + rank : -1;  // tile-local position within the digit
-        }
-        // publish this tile's count of digit tid, look back for the tiles before it, publish the inclusive prefix
-        const int cnt = run;
-        int excl = 0;
-        if (t == 0) {
-            __hip_atomic_store(st + tid, kOsInc | (unsigned)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(st + (size_t)t * kRsBins + tid, kOsAgg | (unsigned)cnt, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            int spins = 0;
-            for (int j = t - 1; j >= 0;) {
-                const unsigned v = __hip_atomic_load(st + (size_t)j * kRsBins + tid, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                if ((v >> 30) == 0u) {  // tile j has not published yet (it was claimed earlier: it runs)
-                    // (bounded: a protocol fault gives a wrong order, which the sort tests catch, not a hung GPU)
-                    if (++spins > (1 << 22)) break;
-                    continue;
-                }
-                excl += (int)(v & kOsCount);
-                if ((v >> 30) == 2u) break;
-                --j;
-            }
-            __hip_atomic_store(st + (size_t)t * kRsBins + tid, kOsInc | (unsigned)(excl + cnt), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // the tile in digit order in LDS, then stored in runs of consecutive destinations (as k_rs_scatter)
-        int x = cnt;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int y = __shfl_up(x, off);
-            x += lane >= off ? y : 0;
-        }
-        if (lane == 63) wsum[w] = x;
-        lds_barrier();
-        int base = 0;
-#pragma unroll
-        for (int i = 0; i < NW; ++i) base += i < w ? wsum[i] : 0;
-        dstart[tid] = base + x - cnt;
-        rstart[tid] = gstart[tid] + excl;
-        lds_barrier();
-#pragma unroll
-        for (int j = 0; j < kRsIpt; ++j)
-            if (dst[j] >= 0) {
-                const unsigned dg = (key[j] >> p.shift) & mask;
-                const int l = dstart[dg] + dst[j];
-                skey[l] = key[j];
-                sval[l] = val[j];
-            }
-        lds_barrier();
-        const int tn = b1 - t0;
-        for (int l = tid; l < tn; l += kRsThreads) {
-            const unsigned kk = skey[l];
-            const unsigned dg = (kk >> p.shift) & mask;
-            const int d = rstart[dg] + (l - dstart[dg]);
-            if constexpr (DST == DST_ARRAY) {
-                p.keys_out[d] = kk;
-                p.vals_out[d] = sval[l];
-            } else {
-                p.nslot[(d / S2) * p.S + d % S2] = sval[l];
-            }
-        }
-    }
-}
-
 template <int SRC, int DST, int RB>
 void rs_launch(hipStream_t st, const RsPass& p) {
     hipLaunchKernelGGL((k_rs_hist<SRC, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p);
@@ -529,36 +297,11 @@ void rs_launch(hipStream_t st, const RsPass& p) {
 
 // the passes of a `bits`-bit key, <= RB bits each (split evenly), ping-ponging between the two arrays
 template <int SRC, int DST, int RB>
-void os_launch(hipStream_t st, const RsPass& p, const OsTemp& o, int par, int pass) {
-    hipLaunchKernelGGL((k_os_pass<SRC, DST, RB>), dim3(kRsGrid), dim3(1 << RB), 0, st, p, o, par, pass);
-}
-
-template <int SRC, int DST, int RB>
-hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* kb, int* va, int* vb, const OsTemp* os,
-                   int par) {
+hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* kb, int* va, int* vb) {
     static_assert(RB >= 6 && (1 << RB) <= kRsBinsMax, "digit width");
     // (the NEE queue is sorted in place: its first pass must finish reading the slots before any is rewritten)
     const int passes = std::max((bits + RB - 1) / RB, DST == DST_NEEQ ? 2 : 1);
     const int per = (bits + passes - 1) / passes;
-    if (os && passes <= kOsMaxPasses) {  // one-sweep: 1 + passes launches
-        hipLaunchKernelGGL((k_os_hist<SRC, RB>), dim3(kRsGrid / 4), dim3(1 << RB), 0, st, p, *os, par, passes, per,
-                           bits);
-        p.meta = os->meta;
-        for (int i = 0; i < passes; ++i) {
-            p.shift = i * per;
-            p.nbits = bits - p.shift < per ? bits - p.shift : per;
-            const bool first = i == 0, last = i == passes - 1;
-            p.keys_out = (i & 1) ? kb : ka;
-            p.vals_out = (i & 1) ? vb : va;
-            if (first && last) os_launch<SRC, DST, RB>(st, p, *os, par, i);
-            else if (first) os_launch<SRC, DST_ARRAY, RB>(st, p, *os, par, i);
-            else if (last) os_launch<SRC_ARRAY, DST, RB>(st, p, *os, par, i);
-            else os_launch<SRC_ARRAY, DST_ARRAY, RB>(st, p, *os, par, i);
-            p.keys_in = p.keys_out;
-            p.vals_in = p.vals_out;
-        }
-        return hipGetLastError();
-    }
     hipLaunchKernelGGL(k_rs_prep, dim3(1), dim3(64), 0, st, p.len, const_cast<int*>(p.meta));
     for (int i = 0; i < passes; ++i) {
         p.shift = i * per;
@@ -578,46 +321,34 @@ hipError_t rs_sort(hipStream_t st, int bits, RsPass p, unsigned* ka, unsigned* k
 
 }  // namespace
 
-// the classic passes' histograms and meta, then (one-sweep) its histograms, tile counters and status words for a
-// queue of up to n items
-static size_t classic_temp_ints() { return (size_t)kRsGrid * kRsBinsMax + kRsBinsMax + 64; }
-size_t sort_temp_bytes(size_t n) {
-    return sizeof(int) * (classic_temp_ints() + os_meta_ints() + os_ghist_ints() + os_tile_ints() +
-                          (size_t)kOsMaxPasses * os_max_tiles(n) * kRsBinsMax);
-}
-
-static void rs_temp(void* temp, size_t cap, RsPass& p, OsTemp& o) {
-    int* hist = static_cast<int*>(temp);
-    p.hist = hist;
-    p.tot = hist + (size_t)kRsGrid * kRsBinsMax;
-    p.meta = p.tot + kRsBinsMax;
-    o = os_temp(hist + classic_temp_ints(), cap);
-}
+size_t sort_temp_bytes() { return sizeof(int) * ((size_t)kRsGrid * kRsBinsMax + kRsBinsMax + 64); }
 
 hipError_t launch_sort_rays(hipStream_t st, const SortRaysIO& io) {
     RsPass p{};
-    OsTemp o;
-    rs_temp(io.temp, io.cap, p, o);
+    int* hist = static_cast<int*>(io.temp);
+    p.hist = hist;
+    p.tot = hist + (size_t)kRsGrid * kRsBinsMax;
+    p.meta = p.tot + kRsBinsMax;
     p.S = io.S;
     p.qkey = io.qkey;
     p.nslot = io.perm;
     p.len = io.len;
     const int bits = 3 + 2 * io.dir_bits + 3 * io.org_bits;
-    return rs_sort<SRC_RAYQ, DST_PERM, RT_RS_RAY_BITS>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt,
-                                                       RT_RS_ONESWEEP ? &o : nullptr, io.parity);
+    return rs_sort<SRC_RAYQ, DST_PERM, RT_RS_RAY_BITS>(st, bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 hipError_t launch_sort_nee(hipStream_t st, const SortNeeIO& io) {
     RsPass p{};
-    OsTemp o;
-    rs_temp(io.temp, io.cap, p, o);
+    int* hist = static_cast<int*>(io.temp);
+    p.hist = hist;
+    p.tot = hist + (size_t)kRsGrid * kRsBinsMax;
+    p.meta = p.tot + kRsBinsMax;
     p.S = io.S;
     p.qkey = io.key;
     p.qslot = io.slot;
     p.nslot = io.slot;  // in place: the first pass copied the slots into the values
     p.len = io.len;
-    return rs_sort<SRC_NEEQ, DST_NEEQ, RT_RS_NEE_BITS>(st, 3 * io.org_bits, p, io.keys, io.keys_alt, io.vals,
-                                                       io.vals_alt, RT_RS_ONESWEEP ? &o : nullptr, io.parity);
+    return rs_sort<SRC_NEEQ, DST_NEEQ, RT_RS_NEE_BITS>(st, 3 * io.org_bits, p, io.keys, io.keys_alt, io.vals, io.vals_alt);
 }
 
 }  // namespace rtmi
