@@ -513,6 +513,7 @@ struct rt_ctx {
     float bvh_any_cost = 2.f;
     int bvh_any_leaf = 4;
     int force_amb = -1;        // RTMI_FORCE_AMB=k (test knob, DevScene amb_force / amb_mask): -1 off
+    int coop = 1;              // RTMI_COOP=0 (test knob): undecided rays to the fallback kernels (DevScene coop_ok 0)
     int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
     int emit_filter = 1;       // RTMI_EMIT_FILTER=0: the last depth of a mixed scene traces every ray (A/B)
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
@@ -1623,6 +1624,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_BVH_LEAF")) c->bvh_max_leaf = std::max(1, std::min(15, std::atoi(e)));
     parse_bvh_any(c->bvh_any_cost, c->bvh_any_leaf);
     if (const char* e = std::getenv("RTMI_FORCE_AMB")) c->force_amb = std::max(-1, std::min(30, std::atoi(e)));
+    if (const char* e = std::getenv("RTMI_COOP")) c->coop = std::atoi(e) != 0;
     if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
     if (const char* e = std::getenv("RTMI_EMIT_FILTER")) c->emit_filter = std::atoi(e);
     if (const char* e = std::getenv("RTMI_SORT_BITS")) {
@@ -2135,7 +2137,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
             const int fc = ob.nodes[i].first_child;
             if (fc >= 0 && ((fc - 1) % 8 != 0 || (fc - 1) / 8 > 65535)) ids16 = false;
         }
-        d.coop_ok = qcap != 1 && bound <= kCoopFifo && ids16 ? 1 : 0;
+        d.coop_ok = c->coop && qcap != 1 && bound <= kCoopFifo && ids16 ? 1 : 0;
     }
     d.depth = nn < (1 << 24) ? maxd : 1 << 30;  // DFS stack entries hold 24-bit group ids
     if (qcap == 0) {  // each lane allocates its ring of ring_threads x rs ints (ensure_ring)

@@ -108,11 +108,16 @@ def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, which):
     assert st["nodes_tested"] / st["rays"] < 60 and st["tris_tested"] / st["rays"] < 16, st
 
 
+@pytest.mark.parametrize("coop", ["1", "0"])
 @pytest.mark.parametrize("kind", ["cfg3_path", "cfg3_shadowq", "cfg4_mis", "cfg4_path"])
-def test_forced_fallback_paths_film_bitexact(oracle_lib, monkeypatch, kind):
+def test_forced_fallback_paths_film_bitexact(oracle_lib, monkeypatch, kind, coop):
     """A quarter of all BVH queries forced ambiguous (RTMI_FORCE_AMB=2): the exact fallbacks carry them and the
-    film is bit-exact against the oracle, with the fallback counters far above their natural rate."""
+    film is bit-exact against the oracle, with the fallback counters far above their natural rate.  coop 1: the
+    wave-cooperative BFS in the kernel that found them (the bench scenes' default); coop 0 (RTMI_COOP=0,
+    as for octrees whose BFS queue bound exceeds its FIFO): the fallback kernels k_trace_fallback, k_path_shadow and
+    k_path_nee<Q, true>."""
     monkeypatch.setenv("RTMI_FORCE_AMB", "2")
+    monkeypatch.setenv("RTMI_COOP", coop)
     if kind.startswith("cfg3"):
         if kind == "cfg3_shadowq":
             monkeypatch.setenv("RTMI_SHADOW_QUEUE", "1")
