@@ -1367,107 +1367,6 @@ __device__ __forceinline__ bool bvh8_walk(const float4* __restrict__ nodes, cons
     return !overflow;
 }
 
-// A lane's sequence of any-hit queries (k_path_nee: its vertex's shadow rays, the sampled lights in light order) walked
-// back to back in ONE speculative while-while loop over the any-hit BVH: a lane whose walk ends — a sure occluder
-// found, or nothing left to visit — reports it (finish) and sets up its next ray (setup) while the wave's other lanes
-// go on, so a wave waits once for the lane with the longest sequence instead of once per light for the slowest lane
-// of that light.  Each ray's walk, its canonical any-hit rule and its answer are bvh_anyhit's (the watertight test's
-// permutation per lane, KZ = -1).  setup(i, o, d, tmax) -> false: ray i is not cast; finish(i, occluded, amb).
-template <class Setup, class Finish>
-__device__ __forceinline__ void bvh_anyhit_seq(const DevScene& sc, int n, bool live, Setup&& setup, Finish&& finish,
-                                               ctr_t& nn, ctr_t& nt) {
-    const float4* __restrict__ nodes = sc.bvh[kBvhAny];
-    const float* __restrict__ tiles = sc.btiles[kBvhAny];
-    unsigned* stw = g_astk + threadIdx.x;
-    Bvh8Ray r;
-    TriRay R;
-    float tMax = 0.f, sure = 0.f;
-    int sp = 0, node = -1, lf = 0, lc = 0, i = -1;
-    bool overflow = false, window = false, occ = false;
-    auto start = [&]() -> bool {  // the lane's next ray, false when none is left
-        V3 o, d;
-        float tm;
-        while (++i < n) {
-            if (!setup(i, o, d, tm)) continue;
-            if (bvh_refuses(sc, o, d)) {
-                finish(i, false, true);
-                continue;
-            }
-            r.inv = bvh_inv(d);
-            r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
-            R = make_triray<-1>(o, d);
-            tMax = tm;
-            sure = tm - canon_window(tm, sc.wabs);
-            sp = 0; node = 0; lf = 0; lc = 0;
-            overflow = window = occ = false;
-            return true;
-        }
-        return false;
-    };
-    bool active = live && start();
-    while (true) {
-        while (true) {  // node steps (bvh8_walk<true>): lanes without a leaf open nodes, lanes holding one speculate
-            const bool more = active && (node >= 0 || (node == -1 && sp > 0));
-            if (__ballot(lc == 0 && more) == 0) break;
-            if (!more) continue;
-            if (node == -1) {
-                --sp;
-                node = (int)stw[sp * kBlock];
-            }
-            if (node >= 0) {
-                RT_SIMD_TICK(4);
-                const BvhNode8 bn = load_node8(nodes, node);
-                nn += __popc(bn.N1.w);
-                unsigned k[8];
-                node_keys(bn, r, tMax, k, true);
-                node = -1;
-#pragma unroll
-                for (int j = 7; j >= 1; --j)
-                    if (k[j] != kNoChild) {
-                        if (sp >= kAnyStack) overflow = true;
-                        else stw[sp++ * kBlock] = (unsigned)child_word(bn, k[j]);
-                    }
-                if (k[0] != kNoChild) node = child_word(bn, k[0]);
-            }
-            if (node < -1 && lc == 0) {
-                decode_leaf(node, lf, lc);
-                node = -1;
-            }
-        }
-        if (__ballot(active) == 0) break;
-        if (active) {
-            bool ended = lc == 0;  // (after the node steps a lane without a leaf has nothing left to visit)
-            if (!ended) {
-                const int m = lc < kLeafStep ? lc : kLeafStep;
-                const float* tp = tiles + 9 * lf;
-                float4 A = ld_f4u(tp), B = ld_f4u(tp + 4);
-                float C = tp[8];
-                for (int q = 0; q < m; ++q) {
-                    float4 nA = A, nB = B;
-                    float nC = C;
-                    if (q + 1 < m) { nA = ld_f4u(tp + 9 * q + 9); nB = ld_f4u(tp + 9 * q + 13); nC = tp[9 * q + 17]; }
-                    ++nt;
-                    RT_SIMD_TICK(6);
-                    float b0, b1, b2, t;
-                    if (tri_intersect<-1>(R, tMax, A, B, make_float4(C, 0.f, 0.f, 0.f), b0, b1, b2, t) && t < tMax) {
-                        if (t < sure) { occ = true; break; }
-                        window = true;
-                    }
-                    A = nA; B = nB; C = nC;
-                }
-                lf += m;
-                lc -= m;
-                if (occ) ended = true;
-                else if (lc == 0 && node < -1) { decode_leaf(node, lf, lc); node = -1; }
-            }
-            if (ended) {
-                finish(i, occ, !occ && (window || overflow));
-                active = start();
-            }
-        }
-    }
-}
-
 // closest hit over the BVH: returns the triangle id (or -1) with (b0, b1, b2, t); amb = the BFS must decide
 template <int KZ>
 __device__ __forceinline__ int bvh_closest(const DevScene& sc, int set, V3 o, V3 d, float tMaxInit, float& rb0,
@@ -2670,10 +2569,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     // the throughput of the continued path (NeeIO)
     const float InvPi = 0.31830988618379067154f;
     const int nuv4 = (nl + 1) / 2;
-    #ifndef RT_NEE_SEQ
-#define RT_NEE_SEQ 0
-#endif
-// COOP (multi-level NEE queue): every lane of the wave calls vertex() in step (live = it has a vertex), so the
+    // COOP (multi-level NEE queue): every lane of the wave calls vertex() in step (live = it has a vertex), so the
     // light loop reconverges after each light and the wave resolves the shadow rays the BVH could not decide with the
     // cooperative any-hit BFS (exact) instead of listing their vertices for k_path_nee<Q, true> (no fallback launch
     // when the octree's queue bound fits its FIFO, DevScene coop_ok)
@@ -2688,57 +2584,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         uint64_t vis = 0;
         ctr_t nv = 0;
         bool defer = false;
-#if RT_NEE_SEQ
-        if constexpr (COOP) {
-            // the vertex's shadow rays back to back in one walk loop (bvh_anyhit_seq), then the undecided ones by the
-            // cooperative BFS, light by light
-            uint32_t ambm = 0;
-            bvh_anyhit_seq(
-                sc, nl, live,
-                [&](int li, V3& o, V3& d, float& tm) -> bool {
-                    if (wg[li] < 0) return false;  // light not sampled (cos <= 0)
-                    ++nv;
-                    const LightRay lr = light_ray(ldconst(sc.lights, li), po, uv[2 * li], uv[2 * li + 1]);
-                    o = po; d = lr.wi; tm = lr.tmax;
-                    return true;
-                },
-                [&](int li, bool occ, bool amb) {
-                    if (amb) {
-                        ambm |= 1u << li;
-                    } else if (!occ) {  // the octree does not occlude: the analytic shapes (scene_occluded_bvh)
-                        const LightRay lr = light_ray(ldconst(sc.lights, li), po, uv[2 * li], uv[2 * li + 1]);
-                        if (!shapes_occluded(sc, po, lr.wi, lr.tmax)) vis |= 1ull << li;
-                    }
-                },
-                snn, snt);
-            for (int li = 0; li < nl; ++li) {
-                bool amb = (ambm >> li) & 1u;
-                if (sc.coop_ok) {
-                    const LightRay lr = light_ray(ldconst(sc.lights, li), po, uv[2 * li], uv[2 * li + 1]);
-                    uint64_t am = __ballot(amb);
-                    while (am) {
-                        const int Ls = __builtin_ctzll(am);
-                        am &= am - 1;
-                        const V3 oL = v3(__shfl(po.x, Ls), __shfl(po.y, Ls), __shfl(po.z, Ls));
-                        const V3 dL = v3(__shfl(lr.wi.x, Ls), __shfl(lr.wi.y, Ls), __shfl(lr.wi.z, Ls));
-                        int cp;
-                        float c0, c1, c2, ct;
-                        ctr_t cnn = 0, cnt = 0;
-                        bfs_coop<true>(sc, 0, oL, dL, __shfl(lr.tmax, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct, cnn,
-                                       cnt);
-                        if (lane_id() == Ls) {
-                            if (!(cp >= 0 || shapes_occluded(sc, po, lr.wi, lr.tmax))) vis |= 1ull << li;
-                            amb = false;
-                            ++sfb;
-                            snn += cnn;
-                            snt += cnt;
-                        }
-                    }
-                }
-                if (amb) defer = true;  // (coop_ok == 0: the vertex goes to k_path_nee<Q, true>)
-            }
-        } else
-#endif
         for (int li = 0; li < nl; ++li) {
             const bool act = live && !defer && wg[li] >= 0;  // (wg < 0: light not sampled, cos <= 0)
             bool occ = false, amb = false;
