@@ -1547,26 +1547,6 @@ __device__ __forceinline__ int finish_closest(const DevScene& sc, const TraceIO&
 #define RT_TRACE_KZ 1
 #endif
 
-// The reference BFS for one ambiguous closest-hit ray as a call (RT_TRACE_NOINLINE builds): its registers then do not
-// set the register allocation of the caller's BVH loop.
-struct BfsHit {
-    int prim;
-    float b0, b1, b2, t;
-    unsigned nn, nt;
-};
-template <int QCAP>
-__device__ __attribute__((noinline)) BfsHit bfs_closest_call(const DevScene& sc, int set, V3 o, V3 d) {
-    BfsHit h{};
-    ctr_t nn = 0, nt = 0;
-    h.prim = traverse<QCAP, false, -1>(sc, set, o, d, 3.402823466e+38f, h.b0, h.b1, h.b2, h.t, nn, nt);
-    h.nn = (unsigned)nn;
-    h.nt = (unsigned)nt;
-    return h;
-}
-#ifndef RT_TRACE_NOINLINE
-#define RT_TRACE_NOINLINE 0
-#endif
-
 // FBL (multi-level scenes, path mode: io.fb_pos): the BVH walk alone, the ambiguous rays listed for k_trace_fallback;
 // otherwise the reference BFS runs inline for them.
 template <int QCAP, bool FBL>
@@ -1583,16 +1563,10 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
             bool amb = false;
             prim = traverse_bvh<false, RT_TRACE_KZ != 0>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z),
                                                          3.402823466e+38f, b0, b1, b2, t, nn, nt, amb);
-            if (amb) {
+            if (amb) {  // (multi-level scenes run on tickets, below: this static-chunk form is not launched)
                 ++nfb;
-                if constexpr (RT_TRACE_NOINLINE) {
-                    const BfsHit h = bfs_closest_call<QCAP>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z));
-                    prim = h.prim; b0 = h.b0; b1 = h.b1; b2 = h.b2; t = h.t;
-                    nn += h.nn; nt += h.nt;
-                } else {  // (rare: vector atomics per lane) k_trace_fallback writes this ray's hit
-                    io.fb_pos[atomicAdd(io.fb_len, 1)] = p;
-                    return;
-                }
+                io.fb_pos[atomicAdd(io.fb_len, 1)] = p;
+                return;
             }
         } else {
             prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
@@ -1658,7 +1632,9 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                     prim = traverse_bvh<false, RT_TRACE_KZ != 0>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z),
                                                                  3.402823466e+38f, b0, b1, b2, t, nn, nt, amb);
                 }
-                uint64_t am = __ballot(live && amb);
+                // (coop_ok == 0: the octree's BFS queue may exceed the FIFO, and the host launches k_trace_fallback:
+                // the ambiguous rays are listed for it directly)
+                uint64_t am = sc.coop_ok ? __ballot(live && amb) : 0ull;
                 while (am) {
                     const int L = __builtin_ctzll(am);
                     am &= am - 1;
@@ -1679,6 +1655,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                 if (live) {
                     if (amb) {  // (FIFO overflow, practically never: k_trace_fallback's per-thread BFS)
                         io.fb_pos[atomicAdd(io.fb_len, 1)] = p;
+                        if (!sc.coop_ok) ++nfb;  // (coop rays are counted above)
                     } else {
                         prim = finish_closest(sc, io, p, o4, d4, prim, b0, b1, b2, t);
                         nh += prim >= 0;
