@@ -674,7 +674,22 @@ RT_DEV bool trisimple_isect(const DevShape& s, V3 orig, V3 dir, float tMax, V3& 
     ph = vadd(orig, vmul(dir, t)); th = t;
     return true;
 }
+// A conservative cull ahead of the exact tests: a ray segment [0, tMax] whose closest approach to the shape's padded
+// render-space bounding sphere lies outside it cannot hit the shape, so the exact test (two 4x4 transforms, square
+// roots, divisions) would return false — skipping it changes no result.  The slack 1e-4 |c - o|^2 covers the rounding
+// of this test and of the exact one far from the origin; a degenerate direction (d.d not > 0, NaN) is never culled.
+RT_DEV bool shape_culled(const DevShape& s, V3 o, V3 d, float tMax) {
+    const V3 oc = v3(s.bs[0] - o.x, s.bs[1] - o.y, s.bs[2] - o.z);
+    const float dd = vdot(d, d);
+    if (!(dd > 0.f)) return false;
+    float t = vdot(oc, d) * __builtin_amdgcn_rcpf(dd);
+    t = t < 0.f ? 0.f : t;
+    t = t > tMax ? tMax : t;
+    const V3 q = v3(oc.x - d.x * t, oc.y - d.y * t, oc.z - d.z * t);
+    return vdot(q, q) > s.bs[3] + 1e-4f * vdot(oc, oc);
+}
 RT_DEV bool shape_isect(const DevShape& s, V3 o, V3 d, float tMax, V3& ph, float& th) {
+    if (shape_culled(s, o, d, tMax)) return false;
     V3 oo = m4_point(s.r2o, o), dd = m4_dir(s.r2o, d);
     if (s.type == 0) return sphere_isect(s, oo, dd, tMax, ph, th);
     if (s.type == 1) return disk_isect(s, oo, dd, tMax, ph, th);

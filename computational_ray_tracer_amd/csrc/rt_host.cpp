@@ -51,6 +51,56 @@ inline void m4v(const float* M, float x, float y, float z, float w, float o[4]) 
         o[r] = (a0 + a1) + (a2 + a3);
     }
 }
+// The render-space bounding sphere of an analytic shape for the kernels' conservative cull (rt_device.h
+// shape_culled): the object-space box of the shape (sphere: [-r, r]^2 x [zmin, zmax]; disk: [-ro, ro]^2 x {h};
+// triangle: its vertices' box) through the inverse of render_to_object — the transform the exact test applies — in
+// double, then centre = the box centre, radius = its half diagonal, padded by 1e-3 relative and 1e-3 (1 + |centre|)
+// absolute.  A singular transform or a non-finite result disables the cull for the shape (bs[3] = inf).
+void shape_bound(DevShape& d) {
+    double a[4][8];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) { a[r][c] = d.r2o[c * 4 + r]; a[r][4 + c] = r == c ? 1.0 : 0.0; }
+    bool ok = true;
+    for (int c = 0; c < 4 && ok; ++c) {  // Gauss-Jordan with partial pivoting
+        int pr = c;
+        for (int r = c + 1; r < 4; ++r) if (std::fabs(a[r][c]) > std::fabs(a[pr][c])) pr = r;
+        if (!(std::fabs(a[pr][c]) > 1e-30)) { ok = false; break; }
+        for (int k = 0; k < 8; ++k) std::swap(a[c][k], a[pr][k]);
+        const double iv = 1.0 / a[c][c];
+        for (int k = 0; k < 8; ++k) a[c][k] *= iv;
+        for (int r = 0; r < 4; ++r)
+            if (r != c) { const double f = a[r][c]; for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k]; }
+    }
+    double lo[3], hi[3];
+    if (d.type == 0) { lo[0] = lo[1] = -d.r; hi[0] = hi[1] = d.r; lo[2] = d.zmin; hi[2] = d.zmax; }
+    else if (d.type == 1) { lo[0] = lo[1] = -d.ro; hi[0] = hi[1] = d.ro; lo[2] = hi[2] = d.h; }
+    else {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(std::min(d.p1[k], d.p2[k]), d.p3[k]);
+            hi[k] = std::max(std::max(d.p1[k], d.p2[k]), d.p3[k]);
+        }
+    }
+    double wlo[3] = {1e300, 1e300, 1e300}, whi[3] = {-1e300, -1e300, -1e300};
+    for (int corner = 0; corner < 8 && ok; ++corner) {
+        const double p[3] = {(corner & 1) ? hi[0] : lo[0], (corner & 2) ? hi[1] : lo[1], (corner & 4) ? hi[2] : lo[2]};
+        for (int r = 0; r < 3; ++r) {
+            const double w = a[r][4] * p[0] + a[r][5] * p[1] + a[r][6] * p[2] + a[r][7];
+            wlo[r] = std::min(wlo[r], w);
+            whi[r] = std::max(whi[r], w);
+        }
+    }
+    double c[3], h2 = 0.0, cm = 0.0;
+    for (int r = 0; r < 3; ++r) {
+        c[r] = 0.5 * (wlo[r] + whi[r]);
+        h2 += 0.25 * (whi[r] - wlo[r]) * (whi[r] - wlo[r]);
+        cm = std::max(cm, std::fabs(c[r]));
+    }
+    const double rp = std::sqrt(h2) * 1.001 + 1e-3 * (1.0 + cm);
+    for (int r = 0; r < 3; ++r) d.bs[r] = (float)c[r];
+    d.bs[3] = (float)(rp * rp);
+    if (!ok || !std::isfinite(d.bs[0]) || !std::isfinite(d.bs[1]) || !std::isfinite(d.bs[2]) || !std::isfinite(d.bs[3]))
+        d.bs[3] = std::numeric_limits<float>::infinity();
+}
 inline F3 m3v(const float* M, F3 v) {
     float o[3];
     for (int r = 0; r < 3; ++r) o[r] = (M[0 * 3 + r] * v.x + M[1 * 3 + r] * v.y) + M[2 * 3 + r] * v.z;
@@ -1993,6 +2043,7 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         std::memcpy(d.o2r, h.object_to_render, 64); std::memcpy(d.r2o, h.render_to_object, 64);
         std::memcpy(d.n2r, h.normal_to_render, 36);
         std::memcpy(d.p1, h.p, 12); std::memcpy(d.p2, h.p + 3, 12); std::memcpy(d.p3, h.p + 6, 12);
+        shape_bound(d);
     }
     std::vector<DevLight> lights(s->n_lights);
     bool full = s->n_shapes > 0 || s->n_lights != 1;

@@ -104,6 +104,7 @@ struct DevShape {                   // rt_shape (Shapes.h:209-907)
     float r, zmin, zmax, h, ri, ro;
     float o2r[16], r2o[16], n2r[9];
     float p1[3], p2[3], p3[3];
+    float bs[4];  // render-space bounding sphere of the shape: centre, padded radius^2 (rt_host.cpp shape_bound)
 };
 
 struct DevScene {
