@@ -286,6 +286,75 @@ def test_cfg4_trace_with_shapes_bitexact(cfg4_small, oracle_lib):
     assert 0.2 < og.mean() < 0.9
 
 
+def _unit(v):
+    return v / np.linalg.norm(v, axis=-1, keepdims=True)
+
+
+def test_shape_cull_grazing_rays_bitexact(oracle_lib):
+    """The kernels skip an analytic shape's exact test when the ray segment passes outside its padded render-space
+    bounding sphere (rt_device.h shape_culled, rt_host.cpp shape_bound).  Exact only if the bound holds for every
+    transform: shapes under rotation and non-uniform scale (a sphere, a ring disk, a TriangleSimple), rays grazing
+    their silhouettes at offsets from 1e-6 to 1e-2 of the size, rays from 1e5 away, and shadow queries ending just
+    before / at / after the hit — closest hits and occlusion must be the oracle's bit for bit, with both outcomes
+    present among the grazing rays."""
+    cfg = scene.cfg4_mixed(res=(48, 27), spp=(2, 2), frequency=16)
+    m = cfg.model
+    mat = m.shapes[0].material
+    S = np.diag([1.7, 0.6, 1.2, 1.0])
+    sph = scene.translate((260.0, 300.0, 260.0)) @ scene.rotate(30.0, (1, 0, 0)) @ scene.rotate(45.0, (0, 1, 0)) @ S
+    dsk = scene.translate((380.0, 250.0, 380.0)) @ scene.rotate(60.0, (0, 0, 1)) @ np.diag([1.3, 0.8, 1.0, 1.0])
+    tri = scene.translate((120.0, 330.0, 200.0)) @ scene.rotate(20.0, (0, 1, 0))
+    extra = [scene.Sphere(sph, mat, radius=40.0),
+             scene.Disk(dsk, mat, height=5.0, inner_radius=12.0, outer_radius=50.0),
+             scene.TriangleSimple(tri, mat, p=((0.0, 0.0, 0.0), (90.0, 10.0, 0.0), (20.0, 70.0, 30.0)))]
+    m.shapes = list(m.shapes) + extra
+    rng = np.random.default_rng(11)
+    eps = np.array([-1e-2, -1e-4, -1e-6, 0.0, 1e-6, 1e-4, 1e-2])
+    ro_all, rd_all = [], []
+    for sh in extra:
+        o2r = np.asarray(sh.rigid, float) @ scene.PERM_YZ
+        n = 3000
+        if isinstance(sh, scene.Sphere):
+            u = _unit(rng.normal(size=(n, 3)))
+            p = sh.radius * u * (1.0 + rng.choice(eps, n))[:, None]
+            t = _unit(np.cross(u, rng.normal(size=(n, 3))))
+        elif isinstance(sh, scene.Disk):
+            a = rng.uniform(0, 2 * np.pi, n)
+            rad = np.where(rng.random(n) < 0.5, sh.outer_radius, sh.inner_radius) * (1.0 + rng.choice(eps, n))
+            p = np.stack([rad * np.cos(a), rad * np.sin(a), np.full(n, sh.height)], 1)
+            t = _unit(np.stack([-np.sin(a), np.cos(a), rng.normal(scale=0.3, size=n)], 1))
+        else:
+            P = np.array(sh.p, float)
+            i = rng.integers(0, 3, n)
+            w = rng.random(n)[:, None]
+            p = P[i] * (1 - w) + P[(i + 1) % 3] * w                       # on an edge
+            p += _unit(rng.normal(size=(n, 3))) * rng.choice(eps, n)[:, None] * 90.0
+            t = _unit(rng.normal(size=(n, 3)))
+        po = p - 200.0 * t                                                 # start 200 back along the tangent
+        ow = (o2r @ np.c_[po, np.ones(n)].T).T[:, :3]
+        dw = _unit((o2r[:3, :3] @ t.T).T)
+        far = rng.random(n) < 0.2                                           # 20 %: from 1e5 away, the same line
+        ow[far] = ow[far] - 1e5 * dw[far]
+        ro_all.append(ow)
+        rd_all.append(dw)
+    ro = np.concatenate(ro_all).astype(np.float32)
+    rd = np.concatenate(rd_all).astype(np.float32)
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    pg, bg = g.trace(ro, rd, False)
+    po_, bo, _ = o.trace(ro, rd, False)
+    ntri = len(m.indices)
+    assert np.array_equal(pg, po_)
+    assert np.array_equal(bits(bg), bits(bo))
+    first = ntri + 4                                                       # the transformed shapes' prim ids
+    hit_extra = (po_ >= first).mean()
+    assert 0.15 < hit_extra < 0.85, hit_extra
+    t = np.where(po_ >= 0, bo[:, 3], 1e3).astype(np.float32)
+    tmax = (t * rng.choice([0.999, 1.0, 1.001, 2.0], size=len(t))).astype(np.float32)
+    og = g.occluded(ro, rd, tmax)
+    assert np.array_equal(og, o.occluded(ro, rd, tmax))
+    assert 0.1 < og.mean() < 0.9
+
+
 @pytest.mark.parametrize("kind,depth", [("path", 5), ("mis", 5), ("mis", 1), ("path", 2)])
 def test_cfg4_mixed_film_bitexact(cfg4_small, oracle_lib, kind, depth):
     """Mixed scene: diffuse / mirror / BK7 glass spheres, quad + disk + point + distant lights; NEE (and MIS).
