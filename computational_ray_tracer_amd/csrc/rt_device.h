@@ -688,8 +688,11 @@ RT_DEV bool shape_culled(const DevShape& s, V3 o, V3 d, float tMax) {
     const V3 q = v3(oc.x - d.x * t, oc.y - d.y * t, oc.z - d.z * t);
     return vdot(q, q) > s.bs[3] + 1e-4f * vdot(oc, oc);
 }
+// CULL = false: the exact test alone (kernels of single-leaf scenes, where the cull's registers would raise the
+// allocation of a kernel that never meets a shape in the bench scenes)
+template <bool CULL = true>
 RT_DEV bool shape_isect(const DevShape& s, V3 o, V3 d, float tMax, V3& ph, float& th) {
-    if (shape_culled(s, o, d, tMax)) return false;
+    if (CULL && shape_culled(s, o, d, tMax)) return false;
     V3 oo = m4_point(s.r2o, o), dd = m4_dir(s.r2o, d);
     if (s.type == 0) return sphere_isect(s, oo, dd, tMax, ph, th);
     if (s.type == 1) return disk_isect(s, oo, dd, tMax, ph, th);

@@ -1513,7 +1513,10 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES RT_MULTI_WAVES  // the multi-level closest-hit trace (variant builds)
 #endif
-#define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? 1 : RT_TRACE_WAVES)))
+#ifndef RT_TRACE1_WAVES
+#define RT_TRACE1_WAVES 1  // the single-leaf closest-hit trace: unbudgeted (variant builds)
+#endif
+#define RT_WAVES_ATTR(Q) __attribute__((amdgpu_waves_per_eu((Q) == 1 ? RT_TRACE1_WAVES : RT_TRACE_WAVES)))
 #ifndef RT_SHADE1_WAVES
 #define RT_SHADE1_WAVES 4  // the single-leaf simple-path shade (Cornell)
 #endif
@@ -1523,6 +1526,7 @@ __device__ __forceinline__ int traverse_bvh(const DevScene& sc, int set, V3 o, V
 
 // The analytic shapes after the octree's closest hit, with the running tMax (hitB = the object-space
 // point for a shape), then the hit record at queue position p.
+template <bool CULL>
 __device__ __forceinline__ int finish_closest(const DevScene& sc, const TraceIO& io, int p, float4 o4, float4 d4,
                                               int prim, float b0, float b1, float b2, float t) {
     if (sc.n_shapes) {
@@ -1531,7 +1535,7 @@ __device__ __forceinline__ int finish_closest(const DevScene& sc, const TraceIO&
             DevShape sh = ldconst(sc.shapes, si);
             V3 ph;
             float th;
-            if (shape_isect(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
+            if (shape_isect<CULL>(sh, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), tm, ph, th)) {
                 prim = sc.n_tris + si; b0 = ph.x; b1 = ph.y; b2 = ph.z; t = th; tm = th;
             }
         }
@@ -1572,7 +1576,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
             prim = traverse_any<QCAP, false>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
                                              b0, b1, b2, t, nn, nt, nfb);
         }
-        prim = finish_closest(sc, io, p, o4, d4, prim, b0, b1, b2, t);
+        prim = finish_closest<QCAP != 1>(sc, io, p, o4, d4, prim, b0, b1, b2, t);
         nh += prim >= 0;
         nr += 1;
     };
@@ -1657,7 +1661,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                         io.fb_pos[atomicAdd(io.fb_len, 1)] = p;
                         if (!sc.coop_ok) ++nfb;  // (coop rays are counted above)
                     } else {
-                        prim = finish_closest(sc, io, p, o4, d4, prim, b0, b1, b2, t);
+                        prim = finish_closest<QCAP != 1>(sc, io, p, o4, d4, prim, b0, b1, b2, t);
                         nh += prim >= 0;
                         nr += 1;
                     }
@@ -1693,7 +1697,7 @@ __global__ void __launch_bounds__(kBlock) k_trace_fallback(DevScene sc, TraceIO 
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
         int prim = traverse<QCAP, false, -1>(sc, io.set, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), 3.402823466e+38f,
                                              b0, b1, b2, t, nn, nt);
-        prim = finish_closest(sc, io, p, o4, d4, prim, b0, b1, b2, t);
+        prim = finish_closest<QCAP != 1>(sc, io, p, o4, d4, prim, b0, b1, b2, t);
         nh += prim >= 0;
         nr += 1;
     }
