@@ -1899,7 +1899,7 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 // pending contribution added on a miss) and a cosine-hemisphere bounce (Get2D, β *= R) appended to the next queue.
 // Sampler state (PCG state + dimension) lives per path slot.
 __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevFilm& film, const PathIO& io, int slot,
-                                                Smp& sm, int smp_kind, int smp_seed) {
+                                                Smp& sm, int smp_kind, int smp_seed, int dim_loaded = -1) {
     int pixel, index, x, y;
     sample_of(ids, slot, pixel, index);
     pixel_xy(film, pixel, x, y);
@@ -1914,14 +1914,15 @@ __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevF
         sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
     }
     sm.px = x; sm.py = y; sm.index = index;
-    sm.dim = io.dim >= 0 ? io.dim : __float_as_int(recf(io.rec, slot, R_MISC)->x);
+    sm.dim = io.dim >= 0 ? io.dim : dim_loaded >= 0 ? dim_loaded : __float_as_int(recf(io.rec, slot, R_MISC)->x);
 }
 // the PCG increment of a path never changes after generation: only the 8-byte state half is written back
-__device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm) {
+// store_dim = false: the caller writes the dimension with the rest of R_MISC (one 16-B store)
+__device__ __forceinline__ void save_sampler(const PathIO& io, int slot, const Smp& sm, bool store_dim = true) {
     const uint2 st = make_uint2((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32));
     if (io.rec.rng8) rng8_state(io.rec)[slot] = st;
     else *reinterpret_cast<uint2*>(recf(io.rec, slot, R_RNG)) = st;
-    if (io.dim < 0) *reinterpret_cast<int*>(recf(io.rec, slot, R_MISC)) = sm.dim;
+    if (io.dim < 0 && store_dim) *reinterpret_cast<int*>(recf(io.rec, slot, R_MISC)) = sm.dim;
 }
 // cosine-hemisphere direction (Sampling.h:449-454) in the pbrt CoordinateSystem frame of nrm; false when z == 0
 __device__ __forceinline__ bool cosine_bounce(float u0, float u1, V3 nrm, V3& wi, float& z) {
@@ -2311,7 +2312,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         int slot = -1;
         bool storedL = false;
         if (live) {
-            slot = io.depth == 0 ? k : __float_as_int(io.rayO[2 * k].w);  // (as k_path_shade)
+            // (one 16-B load gives the slot and the origin: binned items are scattered queue positions)
+            const float4 o4 = io.rayO[2 * k];
+            slot = io.depth == 0 ? k : __float_as_int(o4.w);  // (as k_path_shade)
             int prim = io.hitPrim[k];
             if (prim >= 0) {
                 float lam[8], beta[8];
@@ -2322,7 +2325,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                 } else {
                     rload8(io.rec, slot, R_BETA, beta);
                 }
-                float4 o4 = io.rayO[2 * k], d4 = io.rayD[2 * k];
+                const float4 d4 = io.rayD[2 * k];
                 V3 ro = v3(o4.x, o4.y, o4.z), rdw = v3(d4.x, d4.y, d4.z);
                 V3 rayd = vnorm(rdw);
                 float4 hb = io.hitB[k];
@@ -2357,7 +2360,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                     lidx = s.light;
                 }
                 const DevMaterial mt = mat_at(sc, lds_mats, mid);
-                float prevPdf = rec_prev_pdf(io.rec, slot);
+                // R_MISC (dimension, prevPdf, TerminateSecondary flag) read once and written back once, as a float4:
+                // the record is slot-indexed, so every narrow access of a wave is 64 scattered requests
+                float4 misc = *recf(io.rec, slot, R_MISC);
+                const float prevPdf = misc.y;
                 if (MC != 2 && mt.emit > 0) {  // one-sided pure emitter, ends the path
                     if (front) {
                         float L[8];
@@ -2393,14 +2399,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         wantNext = true;
                         nO = make_float4(po.x, po.y, po.z, 0.f);
                         nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                        rec_set_prev_pdf(io.rec, slot, 0.f);
+                        misc.y = 0.f;
+                        *recf(io.rec, slot, R_MISC) = misc;
                     } else {
                         Smp sm;
-                        restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed);
+                        restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed, __float_as_int(misc.x));
                         if (MC != 1 && mt.type == 2) {  // smooth dielectric
                             if (mt.eta == 0) {  // dispersive BK7: TerminateSecondary (spectrum.h:302-310)
                                 if (io.lean == 2) {  // the pdfs are not stored: flag it, k_path_film divides
-                                    reinterpret_cast<float*>(recf(io.rec, slot, R_MISC))[2] = 1.f;
+                                    misc.z = 1.f;
                                 } else {
                                     float pdf[8];
                                     load8(io.pdfA, io.pdfB, slot, pdf);
@@ -2435,7 +2442,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                             wantNext = true;
                             nO = make_float4(po.x, po.y, po.z, 0.f);
                             nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                            rec_set_prev_pdf(io.rec, slot, 0.f);
+                            misc.y = 0.f;
                         } else if constexpr (MC != 2) {  // Lambert: NEE per light (k_path_nee), then a cosine bounce
                             V3 po = vadd(p, vmul(nrm, off));
                             float4* nr = nee.rec + (size_t)slot * nee_f4;
@@ -2493,13 +2500,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                                 wantNext = true;
                                 nO = make_float4(po.x, po.y, po.z, 0.f);
                                 nD = make_float4(wi.x, wi.y, wi.z, 0.f);
-                                rec_set_prev_pdf(io.rec, slot, z * InvPi);
+                                misc.y = z * InvPi;
                             }
                             if (wantNee)
                                 nr[N_PO] = make_float4(po.x, po.y, po.z,
                                                        __uint_as_float((unsigned)mid | (bounced ? 0x80000000u : 0u)));
                         }
-                        save_sampler(io, slot, sm);
+                        save_sampler(io, slot, sm, io.dim >= 0);
+                        if (io.dim < 0) misc.x = __int_as_float(sm.dim);
+                        *recf(io.rec, slot, R_MISC) = misc;
                     }
                 }
             }
