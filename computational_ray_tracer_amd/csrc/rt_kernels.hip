@@ -90,12 +90,10 @@ __device__ __forceinline__ uint4 as_u4(float4 v) {
     return make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w));
 }
 __device__ __forceinline__ BvhNode8 load_node8(const float4* __restrict__ nodes, int node) {
-    // two explicit paths (ds_read / global_load), not one generic pointer (flat loads)
-    if (node < kBvhTopNodes) {
-        const float4* N = g_top + kBvhNodeRead * node;
-        return BvhNode8{N[0], as_u4(N[1]), as_u4(N[2]), as_u4(N[3]), as_u4(N[4])};
-    }
-    const float4* N = nodes + (size_t)kBvhNodeF4 * node;
+    // one generic pointer (LDS top levels or global): five flat 16-B loads.  Two explicit paths (ds_read /
+    // global_load) compiled to six global loads per node, the phi of the two paths splitting the last quantised
+    // plane (r05_ab15: CFG3 +2.2 %, CFG4 +1.2 % with the flat loads)
+    const float4* N = node < kBvhTopNodes ? g_top + kBvhNodeRead * node : nodes + (size_t)kBvhNodeF4 * node;
     return BvhNode8{N[0], as_u4(N[1]), as_u4(N[2]), as_u4(N[3]), as_u4(N[4])};
 }
 // the simple path's per-triangle shading inputs on single-leaf scenes (<= 64 triangles): world vertices and the
