@@ -2582,11 +2582,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
         const unsigned tag = __float_as_uint(p4.w);
         const float* uv = reinterpret_cast<const float*>(r + N_UV);
         const float* wg = uv + 4 * nuv4;
+        // the sampled lights (weight >= 0; < 0: not sampled, cos <= 0) as a bit mask, from the weights read four per
+        // 16-B load up front instead of one 4-B load at the top of every light's iteration
+        uint64_t wmask = 0;
+        for (int q = 0; q < (nl + 3) >> 2; ++q) {
+            const float4 w4 = reinterpret_cast<const float4*>(wg)[q];
+            wmask |= (uint64_t)((w4.x >= 0.f ? 1u : 0u) | (w4.y >= 0.f ? 2u : 0u) | (w4.z >= 0.f ? 4u : 0u) |
+                                (w4.w >= 0.f ? 8u : 0u)) << (4 * q);
+        }
         uint64_t vis = 0;
         ctr_t nv = 0;
         bool defer = false;
         for (int li = 0; li < nl; ++li) {
-            const bool act = live && !defer && wg[li] >= 0;  // (wg < 0: light not sampled, cos <= 0)
+            const bool act = live && !defer && ((wmask >> li) & 1u);
             bool occ = false, amb = false;
             LightRay lr{};
             if (act) {
@@ -2646,11 +2654,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                 rload8(io.rec, slot, R_L, L);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) x[i] = beta[i] * (R[i] * InvPi);
+                float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);  // the weights again, four per 16-B load
+                int wq = -1;
                 for (int li = 0; li < nl; ++li) {
                     if (!((vis >> li) & 1)) continue;
                     const DevLight Lt = ldconst(sc.lights, li);
                     const float sc_le = Lt.type <= 1 ? sc.materials[Lt.material].emit : Lt.scale;
-                    const float wgt = wg[li];
+                    if ((li >> 2) != wq) {
+                        wq = li >> 2;
+                        w4 = reinterpret_cast<const float4*>(wg)[wq];
+                    }
+                    const int l4 = li & 3;
+                    const float wgt = l4 == 0 ? w4.x : l4 == 1 ? w4.y : l4 == 2 ? w4.z : w4.w;
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         float Le = sc_le * d65_query(sp, lam[i]);
