@@ -558,7 +558,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
                     make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
                                (uint32_t)(sm.rng.inc >> 32));
             if (out.lean != 1)  // (dimension, prevPdf 0, TerminateSecondary flag 0)
-                *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, 0.f);
+                *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, __int_as_float(pixel));
             if (!out.lean) {
                 const float one[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
                 const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1896,21 +1896,24 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 // Le at depth 0 only (one-sided), then terminate; otherwise NEE on the quad light (Get2D, shadow ray traced inline,
 // pending contribution added on a miss) and a cosine-hemisphere bounce (Get2D, β *= R) appended to the next queue.
 // Sampler state (PCG state + dimension) lives per path slot.
+// dim_loaded / pixel_loaded >= 0: the dimension / pixel id from an R_MISC the caller already read (mixed scenes:
+// k_generate keeps the pixel in R_MISC.w), so the slot's pixel is not gathered from the work list
 __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevFilm& film, const PathIO& io, int slot,
-                                                Smp& sm, int smp_kind, int smp_seed, int dim_loaded = -1) {
+                                                Smp& sm, int smp_kind, int smp_seed, int dim_loaded = -1,
+                                                int pixel_loaded = -1) {
     int pixel, index, x, y;
-    sample_of(ids, slot, pixel, index);
-    pixel_xy(film, pixel, x, y);
-    if (io.rec.rng8) {
-        const uint2 st = rng8_state(io.rec)[slot];
-        sm.rng.state = (uint64_t)st.x | ((uint64_t)st.y << 32);
-        // the increment SetSequence gave the path (rng.h:36-39); Sobol keeps its index in the state
-        sm.rng.inc = smp_kind == 2 ? 0ull : (hash_pixel(x, y, smp_seed) << 1u) | 1u;
+    if (pixel_loaded >= 0 && !ids.ex_pixel) {
+        pixel = pixel_loaded;
+        index = ids.index_begin + (ids.np_div.m ? intdiv(slot, ids.np_div) : slot / ids.n_pixels);
     } else {
-        const uint4 rs = *reinterpret_cast<const uint4*>(recf(io.rec, slot, R_RNG));
-        sm.rng.state = (uint64_t)rs.x | ((uint64_t)rs.y << 32);
-        sm.rng.inc = (uint64_t)rs.z | ((uint64_t)rs.w << 32);
+        sample_of(ids, slot, pixel, index);
     }
+    pixel_xy(film, pixel, x, y);
+    // the PCG state; the increment SetSequence gave the path (rng.h:36-39) is recomputed from the pixel hash instead
+    // of read back (Sobol keeps its index in the state): one 8-B load per restore
+    const uint2 st = io.rec.rng8 ? rng8_state(io.rec)[slot] : *reinterpret_cast<const uint2*>(recf(io.rec, slot, R_RNG));
+    sm.rng.state = (uint64_t)st.x | ((uint64_t)st.y << 32);
+    sm.rng.inc = smp_kind == 2 ? 0ull : (hash_pixel(x, y, smp_seed) << 1u) | 1u;
     sm.px = x; sm.py = y; sm.index = index;
     sm.dim = io.dim >= 0 ? io.dim : dim_loaded >= 0 ? dim_loaded : __float_as_int(recf(io.rec, slot, R_MISC)->x);
 }
@@ -2401,7 +2404,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         *recf(io.rec, slot, R_MISC) = misc;
                     } else {
                         Smp sm;
-                        restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed, __float_as_int(misc.x));
+                        restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed, __float_as_int(misc.x),
+                                        __float_as_int(misc.w));
                         if (MC != 1 && mt.type == 2) {  // smooth dielectric
                             if (mt.eta == 0) {  // dispersive BK7: TerminateSecondary (spectrum.h:302-310)
                                 if (io.lean == 2) {  // the pdfs are not stored: flag it, k_path_film divides
