@@ -214,7 +214,7 @@ struct SampleIds {
 };
 
 // Path state of a slot (path mode): 8 float4 fields — λ[8] at R_LAM.., β[8] at R_BETA.., L[8] at R_L.., the PCG
-// state + increment (uint4) at R_RNG (the kernels read back only the state: the increment is the pixel hash's),
+// state (uint2) and, in the record layout, the pixel id at R_RNG (the increment is recomputed from the pixel hash),
 // (dimension, prevPdf, TerminateSecondary flag, pixel id) at R_MISC — at p + f * fs + slot * ss.  Multi-level
 // scenes, whose coherence sort leaves slots scattered over a wave, store a slot as ONE 128-B record (fs 1, ss 8):
 // one cache line per access instead of one per field (CFG3 +10 %, CFG4 +8 %).  Single-leaf scenes keep their

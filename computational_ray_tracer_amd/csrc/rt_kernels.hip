@@ -554,9 +554,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
             if (out.rec.rng8)
                 rng8_state(out.rec)[s] = make_uint2((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32));
             else
-                *reinterpret_cast<uint4*>(recf(out.rec, s, R_RNG)) =
-                    make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)sm.rng.inc,
-                               (uint32_t)(sm.rng.inc >> 32));
+                *reinterpret_cast<uint4*>(recf(out.rec, s, R_RNG)) =  // (state, pixel id: restore_sampler)
+                    make_uint4((uint32_t)sm.rng.state, (uint32_t)(sm.rng.state >> 32), (uint32_t)pixel, 0u);
             if (out.lean != 1)  // (dimension, prevPdf 0, TerminateSecondary flag 0)
                 *recf(out.rec, s, R_MISC) = make_float4(__int_as_float(sm.dim), 0.f, 0.f, __int_as_float(pixel));
             if (!out.lean) {
@@ -1901,6 +1900,17 @@ __global__ void k_records(DevScene sc, const DevSpectra* sp, DevFilm film, Shade
 __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevFilm& film, const PathIO& io, int slot,
                                                 Smp& sm, int smp_kind, int smp_seed, int dim_loaded = -1,
                                                 int pixel_loaded = -1) {
+    // the PCG state; the increment SetSequence gave the path (rng.h:36-39) is recomputed from the pixel hash instead
+    // of read back (Sobol keeps its index in the state).  The record layout keeps the pixel id beside the state
+    // (k_generate), so one 16-B load gives both and the work list is not gathered.
+    uint2 st;
+    if (io.rec.rng8) {
+        st = rng8_state(io.rec)[slot];
+    } else {
+        const uint4 rs = *reinterpret_cast<const uint4*>(recf(io.rec, slot, R_RNG));
+        st = make_uint2(rs.x, rs.y);
+        pixel_loaded = (int)rs.z;
+    }
     int pixel, index, x, y;
     if (pixel_loaded >= 0 && !ids.ex_pixel) {
         pixel = pixel_loaded;
@@ -1909,9 +1919,6 @@ __device__ __forceinline__ void restore_sampler(const SampleIds& ids, const DevF
         sample_of(ids, slot, pixel, index);
     }
     pixel_xy(film, pixel, x, y);
-    // the PCG state; the increment SetSequence gave the path (rng.h:36-39) is recomputed from the pixel hash instead
-    // of read back (Sobol keeps its index in the state): one 8-B load per restore
-    const uint2 st = io.rec.rng8 ? rng8_state(io.rec)[slot] : *reinterpret_cast<const uint2*>(recf(io.rec, slot, R_RNG));
     sm.rng.state = (uint64_t)st.x | ((uint64_t)st.y << 32);
     sm.rng.inc = smp_kind == 2 ? 0ull : (hash_pixel(x, y, smp_seed) << 1u) | 1u;
     sm.px = x; sm.py = y; sm.index = index;
