@@ -25,7 +25,7 @@ RT_SENSOR_XYZ, RT_SENSOR_CANON_EOS_100D, RT_SENSOR_COUNT = 0, 1, 18
 RT_OCTREE_BUILD_DEVICE, RT_OCTREE_BUILD_HOST = 0, 1
 RT_ILLUM_D65, RT_ILLUM_A, RT_ILLUM_D50, RT_ILLUM_F1, RT_ILLUM_ACES_D60, RT_ILLUM_COUNT = 0, 1, 2, 3, 15, 16
 RT_INTEGRATOR_REFERENCE, RT_INTEGRATOR_PATH, RT_INTEGRATOR_PATH_MIS = 0, 1, 2
-ABI_VERSION = 8
+ABI_VERSION = 9
 RT_MAX_DEVICES = 16
 QUEUE_SHARDS = 8  # RT_QUEUE_SHARDS
 
@@ -103,7 +103,7 @@ class rt_stats(C.Structure):
                 ("ms_generate", C.c_double), ("ms_trace", C.c_double), ("ms_shade", C.c_double),
                 ("ms_shadow", C.c_double), ("ms_film", C.c_double), ("launches_trace", C.c_int64),
                 ("launches_shade", C.c_int64), ("fallback_rays", C.c_int64), ("shadow_fallback_rays", C.c_int64),
-                ("ms_sort", C.c_double), ("nee_vertices", C.c_int64)]
+                ("ms_sort", C.c_double), ("nee_vertices", C.c_int64), ("coop_overflows", C.c_int64)]
 
 
 class rt_sample_record(C.Structure):

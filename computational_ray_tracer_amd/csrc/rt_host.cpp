@@ -2385,6 +2385,7 @@ static int get_stats_one(rt_ctx* c, rt_stats* out) {
     s.fallback_rays = (int64_t)h[C_FALLBACK];
     s.shadow_fallback_rays = (int64_t)h[C_SFALLBACK];
     s.nee_vertices = (int64_t)h[C_NEEVTX];
+    s.coop_overflows = (int64_t)h[C_COOPOVF];
 #if RT_SIMD_STATS
     unsigned long long sm[8];
     simd_stats_read(sm);
@@ -2750,6 +2751,7 @@ static int impl_rt_get_stats(rt_ctx* c, rt_stats* out) {
         sum.launches_trace += s.launches_trace; sum.launches_shade += s.launches_shade;
         sum.fallback_rays += s.fallback_rays; sum.shadow_fallback_rays += s.shadow_fallback_rays;
         sum.nee_vertices += s.nee_vertices;
+        sum.coop_overflows += s.coop_overflows;
         return RT_OK;
     });
     if (!rc) *out = sum;

@@ -158,8 +158,8 @@ struct DevScene {
     const int* emit_shapes;
     int n_emit_shapes;
 };
-static const int kMaxEmitTris = 64;
-static const int kCoopFifo = 2048;   // entries of the wave-cooperative BFS's group FIFO (16-bit group ids, LDS)  // emitter filter only with at most this many emissive triangles
+static const int kMaxEmitTris = 64;  // emitter filter only with at most this many emissive triangles
+static const int kCoopFifo = 2048;   // entries of the wave-cooperative BFS's group FIFO (16-bit group ids, LDS)
 
 // device counter slots (u64).  Every wave of a persistent kernel adds its totals at the end, all at about the same
 // time: one counter word per slot serialised those atomics (a fixed ~0.15 ms tail per trace launch), so each slot
@@ -168,7 +168,7 @@ static const int kCoopFifo = 2048;   // entries of the wave-cooperative BFS's gr
 void simd_stats_read(unsigned long long* out);  // rt_kernels.hip (measurement builds)
 #endif
 enum { C_NODES = 0, C_TRIS, C_HITS, C_RAYS, C_SHADOW, C_SAMPLES, C_SNODES, C_STRIS, C_FALLBACK, C_SFALLBACK,
-       C_NEEVTX, C_NCOUNTERS = 16 };
+       C_NEEVTX, C_COOPOVF, C_NCOUNTERS = 16 };  // C_COOPOVF: cooperative-BFS FIFO overflows (coop_ok: must stay 0)
 constexpr int kCtrSubs = 32;   // words per counter slot
 constexpr int kCtrLine = 32;   // u64 between words: 256 B
 constexpr size_t kCtrWords = (size_t)C_NCOUNTERS * kCtrSubs * kCtrLine;

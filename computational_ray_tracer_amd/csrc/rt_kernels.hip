@@ -1560,7 +1560,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
     stage_scene<QCAP, false>(sc, io.set);
     if (io.zero && blockIdx.x == 0)
         for (int i = threadIdx.x; i < kQRegion; i += blockDim.x) io.zero[i] = 0;
-    ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0;
+    ctr_t nn = 0, nt = 0, nh = 0, nr = 0, nfb = 0, novf = 0;
     // one ray at queue position p: octree (BVH / BFS), then the analytic shapes
     auto trace_one = [&](int p, float4 o4, float4 d4) __attribute__((always_inline)) {
         float b0 = 0, b1 = 0, b2 = 0, t = 0;
@@ -1646,8 +1646,8 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                     am &= am - 1;
                     const V3 oL = v3(__shfl(o4.x, L), __shfl(o4.y, L), __shfl(o4.z, L));
                     const V3 dL = v3(__shfl(d4.x, L), __shfl(d4.y, L), __shfl(d4.z, L));
-                    int cp;
-                    float c0, c1, c2, ctt;
+                    int cp = -1;
+                    float c0 = 0.f, c1 = 0.f, c2 = 0.f, ctt = 0.f;  // (a miss stores zeros, as the BFS does)
                     ctr_t cnn = 0, cnt = 0;
                     const bool ok = bfs_coop<false>(sc, io.set, oL, dL, 3.402823466e+38f, coop_fifo_bstk(), cp, c0, c1,
                                                     c2, ctt, cnn, cnt);
@@ -1656,12 +1656,17 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
                         nn += cnn;
                         nt += cnt;
                         if (ok) { prim = cp; b0 = c0; b1 = c1; b2 = c2; t = ctt; amb = false; }
+                        else ++novf;
                     }
                 }
                 if (live) {
-                    if (amb) {  // (FIFO overflow, practically never: k_trace_fallback's per-thread BFS)
+                    if (amb) {  // (coop_ok == 0: k_trace_fallback's per-thread BFS decides the ray)
                         io.fb_pos[atomicAdd(io.fb_len, 1)] = p;
                         if (!sc.coop_ok) ++nfb;  // (coop rays are counted above)
+                        // coop_ok promised that the FIFO cannot overflow, so no fallback launch follows: a broken
+                        // promise is counted (C_COOPOVF, rt_stats coop_overflows; the tests require 0) and the ray
+                        // stored as a miss instead of leaving the previous bounce's hit at this position
+                        else { io.hitPrim[p] = -1; io.hitB[p] = make_float4(0.f, 0.f, 0.f, 0.f); }
                     } else {
                         prim = finish_closest<QCAP != 1>(sc, io, p, o4, d4, prim, b0, b1, b2, t);
                         nh += prim >= 0;
@@ -1682,6 +1687,7 @@ __global__ void __launch_bounds__(kBlock) RT_WAVES_ATTR(QCAP) k_trace_closest(De
     count_add(ctr, C_HITS, nh);
     count_add(ctr, C_RAYS, nr);
     count_add(ctr, C_FALLBACK, nfb);
+    if constexpr (QCAP != 1) count_add(ctr, C_COOPOVF, novf);
     if constexpr (QCAP != 1) simd_flush();
 }
 
@@ -1967,7 +1973,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     // atomic and one round of barriers per chunk: Cornell +3.5 %, r03)
     __shared__ float4 pend[QCAP == 1 ? 2 * kBlock : 1];
     bool pend0 = false;
-    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0, novf = 0;
     // lean depth 0: k_generate stored no β = 1 / L = 0, so they start in registers and every path's L is written
     const bool d0 = io.lean && io.depth == 0;
     // multi-level octrees: per-wave tickets and appends (per-ray cost varies by 100x); single leaf: per block
@@ -2114,11 +2120,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                     am &= am - 1;
                     const V3 oL = v3(__shfl(so.x, Ls), __shfl(so.y, Ls), __shfl(so.z, Ls));
                     const V3 dL = v3(__shfl(sd.x, Ls), __shfl(sd.y, Ls), __shfl(sd.z, Ls));
-                    int cp;
+                    int cp = -1;
                     float c0, c1, c2, ct;
                     ctr_t cnn = 0, cnt = 0;
-                    bfs_coop<true>(sc, 0, oL, dL, __shfl(stmax, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct, cnn, cnt);
+                    const bool ok =
+                        bfs_coop<true>(sc, 0, oL, dL, __shfl(stmax, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct, cnn, cnt);
                     if (lane_id() == Ls) {
+                        novf += !ok;  // (coop_ok: never; counted, C_COOPOVF)
                         hit = cp;
                         deferShadow = false;
                         ++sfb;
@@ -2183,6 +2191,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
     count_add(ctr, C_SFALLBACK, sfb);
+    if constexpr (QCAP != 1) count_add(ctr, C_COOPOVF, novf);
     if constexpr (QCAP != 1) simd_flush();
 }
 
@@ -2580,7 +2589,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                                                                        NeeIO nee, unsigned long long* ctr) {
     stage_spectra(sp);
     stage_scene<QCAP>(sc, 0);
-    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0, nvx = 0;
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0, nvx = 0, novf = 0;
     const int nl = sc.n_lights, nf4 = nee_stride(nl);
     // one path vertex: visibility of each sampled light, then the unoccluded lights' contributions in order, then
     // the throughput of the continued path (NeeIO)
@@ -2627,12 +2636,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         am &= am - 1;
                         const V3 oL = v3(__shfl(po.x, Ls), __shfl(po.y, Ls), __shfl(po.z, Ls));
                         const V3 dL = v3(__shfl(lr.wi.x, Ls), __shfl(lr.wi.y, Ls), __shfl(lr.wi.z, Ls));
-                        int cp;
+                        int cp = -1;
                         float c0, c1, c2, ct;
                         ctr_t cnn = 0, cnt = 0;
-                        bfs_coop<true>(sc, 0, oL, dL, __shfl(lr.tmax, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct, cnn,
-                                       cnt);
+                        const bool ok = bfs_coop<true>(sc, 0, oL, dL, __shfl(lr.tmax, Ls), coop_fifo_astk(), cp, c0,
+                                                       c1, c2, ct, cnn, cnt);
                         if (lane_id() == Ls) {  // the octree's answer, then the analytic shapes (scene_occluded_bvh)
+                            novf += !ok;        // (coop_ok: never; counted, C_COOPOVF)
                             occ = cp >= 0 || shapes_occluded(sc, po, lr.wi, lr.tmax);
                             amb = false;
                             ++sfb;
@@ -2720,6 +2730,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
     count_add(ctr, C_SHADOW, nsh);
     count_add(ctr, C_SFALLBACK, sfb);
     count_add(ctr, C_NEEVTX, nvx);
+    if constexpr (QCAP != 1) count_add(ctr, C_COOPOVF, novf);
     if constexpr (QCAP != 1 && !FB) simd_flush();
 }
 

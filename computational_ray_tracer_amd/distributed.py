@@ -89,22 +89,24 @@ def _rank():
 
 
 def reduce_film(film, dst=0):
-    """Sum the per-rank films onto `dst` (torch.distributed; backend nccl = RCCL on ROCm, or gloo)."""
+    """Sum the per-rank films onto `dst` (torch.distributed; backend nccl = RCCL on ROCm, or gloo).  The collective
+    is issued whenever a process group exists, at world size 1 too (tests/test_gpu_configs.py runs RCCL that way on
+    the one-GPU box); without a group the film is already the whole frame."""
     import torch.distributed as dist
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM)
     return film
 
 
-def init_distributed(backend="nccl", timeout_s=None, device_id=None):
+def init_distributed(backend="nccl", timeout_s=None, device_id=None, force=False):
     """One process per GPU (torchrun's RANK / WORLD_SIZE / MASTER_* environment).  Every collective gets a finite
     timeout (RTMI_DIST_TIMEOUT seconds, default 300) and, on RCCL, asynchronous error handling that tears the process
     down, so a rank that dies or hangs makes the others fail with a non-zero exit instead of waiting forever.
-    Returns (world, rank)."""
+    At world size 1 no group is created unless `force` (the world-1 RCCL test).  Returns (world, rank)."""
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if timeout_s is None:
             timeout_s = float(os.environ.get("RTMI_DIST_TIMEOUT", "300"))
         if backend == "nccl":
@@ -124,7 +126,7 @@ def timed_steps(step, steps, warmup, sync, samples, reset=None):
     Returns dict(dt=max seconds, total=samples over all ranks, ranks=[{rank, samples, s}, ...])."""
     import torch
     import torch.distributed as dist
-    multi = dist.is_initialized() and dist.get_world_size() > 1
+    multi = dist.is_initialized()  # (a world-1 group too: its barrier and all_gather run)
     for _ in range(warmup):
         step()
     sync()

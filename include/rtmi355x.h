@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 8
+#define RT_ABI_VERSION 9
 
 typedef enum {
     RT_OK = 0,
@@ -217,6 +217,9 @@ typedef struct {
     int64_t shadow_fallback_rays;    /* the same for any-hit (shadow) rays                */
     double ms_sort;                  /* multi-level octrees: coherence sort of bounce rays (HIP events)  */
     int64_t nee_vertices;            /* mixed scenes: path vertices whose light samples k_path_nee traced */
+    int64_t coop_overflows;          /* multi-level octrees: rays whose wave-cooperative BFS ran out of FIFO while the
+                                        octree's exact queue bound promised it could not (DevScene coop_ok); always 0
+                                        unless that bound is wrong — the tests require 0 */
 } rt_stats;   /* multi-device contexts: every field summed over the devices */
 
 /* Per-sample record for parity (stage outputs of one (pixel, index) camera sample). */

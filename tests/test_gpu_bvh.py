@@ -135,6 +135,7 @@ def test_forced_fallback_paths_film_bitexact(oracle_lib, monkeypatch, kind, coop
     st = g.stats()
     assert st["fallback_rays"] > 0.1 * st["rays"], st
     assert st["shadow_fallback_rays"] > 0.1 * st["shadow_rays"], st
+    assert st["coop_overflows"] == 0, st        # the cooperative BFS's FIFO bound held
 
 
 @pytest.mark.parametrize("any_bvh", ["0/4", "default"])
@@ -155,3 +156,35 @@ def test_any_hit_bvh_choice_film_bitexact(oracle_lib, monkeypatch, any_bvh):
         fg = g.render_pass(0, 4)
         fo = oracle_lib.OracleScene(cfg).render(0, 4)
         assert np.array_equal(bits(fg), bits(fo))
+
+
+def _coop_push_replay(child):
+    """The cooperative BFS's FIFO (rt_kernels.hip bfs_coop) with every box test passing: the root is a group of one;
+    popping group g visits its 8 nodes in slot order and pushes the group of each internal child.  Returns the
+    largest number of queued groups right after a push — what bfs_coop's `tail - head` reaches."""
+    q, head, worst = [], 0, 0
+    if child[0] >= 0:
+        q.append(int(child[0]))
+        worst = 1
+    while head < len(q):
+        g = q[head]
+        head += 1
+        for i in range(8):
+            c = int(child[g + i])
+            if c >= 0:
+                q.append(c)
+                worst = max(worst, len(q) - head)
+    return worst
+
+
+@pytest.mark.parametrize("which", ["cfg3", "cfg4", "cfg0"])
+def test_coop_fifo_bound_matches_push_order(which):
+    """the host skips every fallback launch when the octree's exact worst-case queue fits the cooperative
+    BFS's FIFO (DevScene coop_ok, kCoopFifo = 2048 entries).  The host's bound (rt_octree_info max_queue_groups)
+    must equal a replay of bfs_coop's own push order, so a change to either side shows up here."""
+    cfg = scene.cfg0_reference(res=(32, 32), n_index=1) if which == "cfg0" else _mesh_cfg(which)
+    oc = Renderer(cfg).octree()
+    assert oc["depth"] >= 2
+    assert _coop_push_replay(oc["child"]) == oc["max_queue_groups"]
+    if which != "cfg0":
+        assert oc["max_queue_groups"] <= 2048   # the bench meshes run with coop_ok (no fallback launch)

@@ -737,6 +737,7 @@ def test_bvh_fast_path_counters(cfg3_pair):
     assert st["tris_tested"] / st["rays"] < 12, st
     assert st["fallback_rays"] <= 1e-3 * st["rays"], st
     assert st["shadow_fallback_rays"] <= 1e-2 * st["shadow_rays"], st
+    assert st["coop_overflows"] == 0, st
 
 
 @pytest.mark.parametrize("nl,single_leaf", [(1, False), (2, True), (6, False), (6, True)])
