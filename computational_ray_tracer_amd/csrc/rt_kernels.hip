@@ -788,7 +788,30 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                     const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
                     const float gx = o.x - sc.cl_guard.x, gy = o.y - sc.cl_guard.y, gz = o.z - sc.cl_guard.z;
                     const bool far = gx * gx + gy * gy + gz * gz > sc.cl_guard.w;  // pad not sized for it
-                    if (kCompact && kClusterTris == 2 && ncl <= kCompactMaxClusters) {
+                    if (ANYHIT && kClusterTris == 2) {
+                        // Shadow rays: each lane walks its own hit clusters, the tiles read from LDS (g_leaf1), so
+                        // the wave runs as many candidate steps as its busiest lane has hit clusters instead of one
+                        // per cluster any lane of the wave hit (Cornell bounce vertices: 0.75 hit clusters per shadow
+                        // ray, but most of the 18 hit by some lane; r06_ab2: shade stage -10 %, Cornell +4.5 %).
+                        // The candidate mask is exactly the per-cluster loop's, so pass 2 is unchanged.  Closest-hit
+                        // bounce rays keep the compacted pairs below (this loop measured trace +8 % for them).
+                        uint32_t hm = cluster_mask(cl, ncl, far, o, inv, cl_t);
+                        nt += cluster_tris(hm, ncl, r.y);
+                        while (hm) {
+                            const int c = __builtin_ctz(hm);
+                            hm &= hm - 1;
+                            const float4* tp = RT_LEAF1(tiles, r.x, 2 * c);
+                            unsigned bits;
+                            if ((fp >> (2 * c)) & 1) {
+                                bits = tri_candidate_pair<KZ>(R, tp[0], tp[1], tp[2], tp[4], tp[5]);
+                            } else {
+                                bits = tri_candidate<KZ>(R, tp[0], tp[1], tp[2]) ? 1u : 0u;
+                                if (2 * c + 1 < r.y && tri_candidate<KZ>(R, tp[3], tp[4], tp[5])) bits |= 2u;
+                            }
+                            cand |= (uint64_t)bits << (2 * c);
+                        }
+                        k = r.y;
+                    } else if (kCompact && kClusterTris == 2 && ncl <= kCompactMaxClusters) {
                         // Each lane box-tests every cluster against its own ray; the passing (lane, cluster) pairs
                         // are appended to the wave's LDS list in cluster order (ballot + mbcnt), and the active
                         // lanes then split the list evenly: lane j runs the candidate tests of pairs j, j + n, ...
