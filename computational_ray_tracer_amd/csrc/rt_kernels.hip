@@ -2056,9 +2056,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                     V3 p = vadd(vadd(vmul(p0, hb.x), vmul(p1, hb.y)), vmul(p2, hb.z));
                     float off = 1e-4f * (1.0f + max3f(fabsf(p.x), fabsf(p.y), fabsf(p.z)));
                     V3 po = vadd(p, vmul(nrm, off));
-                    float R[8];
+                    // kLate (single leaf): both sampler draws and the geometry first, then one pass over the hero
+                    // wavelengths that forms R(λ), the light term and β R per wavelength, so no R[8] array lives
+                    // beside Ld[8] and β (the same operations per element; Cornell +1 %, r06_ab4; multi-level
+                    // scenes keep R formed first: CFG3 −2 % with the late pass, r06_ab2)
+                    constexpr bool kLate = QCAP == 1;
+                    float R[8], le = 0.f, wgt = 0.f;
+                    if constexpr (!kLate) {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.x, mt.y, mt.z, lam[i]);
+                        for (int i = 0; i < 8; ++i) R[i] = sigmoid_eval(mt.x, mt.y, mt.z, lam[i]);
+                    }
                     Smp sm;
                     restore_sampler(ids, film, io, slot, sm, smp.kind, smp.seed);
                     // --- NEE on the quad light
@@ -2075,12 +2082,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         float cs = vdot(nrm, wi);
                         float cl = -vdot(v3(Lq.n[0], Lq.n[1], Lq.n[2]), wi);
                         if (cs > 0 && cl > 0) {
-                            float le = sc.materials[Lq.material].emit;
+                            le = sc.materials[Lq.material].emit;
                             float G = (cs * cl) / dist2;
-                            float wgt = G * Lq.area;
+                            wgt = G * Lq.area;
+                            if constexpr (!kLate) {
 #pragma unroll
-                            for (int i = 0; i < 8; ++i)
-                                Ld[i] = ((beta[i] * (R[i] * InvPi)) * (le * d65_query(sp, lam[i]))) * wgt;
+                                for (int i = 0; i < 8; ++i)
+                                    Ld[i] = ((beta[i] * (R[i] * InvPi)) * (le * d65_query(sp, lam[i]))) * wgt;
+                            }
                             wantShadow = true;
                             so = po;
                             sd = wi;
@@ -2096,15 +2105,46 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
                         V3 wi;
                         float z;
                         if (cosine_bounce(u0, u1, nrm, wi, z)) {
+                            if constexpr (!kLate) {
 #pragma unroll
-                            for (int i = 0; i < 8; ++i) beta[i] *= R[i];
-                            rstore8(io.rec, slot, R_BETA, beta);
+                                for (int i = 0; i < 8; ++i) beta[i] *= R[i];
+                                rstore8(io.rec, slot, R_BETA, beta);
+                            }
                             wantNext = true;
                             nO = make_float4(po.x, po.y, po.z, 0.f);
                             nD = make_float4(wi.x, wi.y, wi.z, 0.f);
                         }
                         save_sampler(io, slot, sm);
                     }
+                    if constexpr (kLate) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const float Ri = sigmoid_eval(mt.x, mt.y, mt.z, lam[i]);
+                            Ld[i] = ((beta[i] * (Ri * InvPi)) * (le * d65_query(sp, lam[i]))) * wgt;
+                            beta[i] *= Ri;
+                        }
+                        if (wantNext) rstore8(io.rec, slot, R_BETA, beta);
+                    }
+                }
+            }
+        }
+        // single leaf: the bounce ray leaves before the shadow ray is traced, so it is not live across the traversal
+        if constexpr (QCAP == 1) {
+            nO.w = __int_as_float(slot);  // the ray's origin carries its slot
+            if (items.r == 1) {  // first item of the chunk
+                if (wantNext) { pend[2 * threadIdx.x] = nO; pend[2 * threadIdx.x + 1] = nD; }
+                pend0 = wantNext;
+            } else {
+                int p0, p1;
+                block_append2(io.nCount, pend0, wantNext, lds, p0, p1);
+                if (pend0) {
+                    const float4 o0 = pend[2 * threadIdx.x], d0v = pend[2 * threadIdx.x + 1];
+                    io.nO[2 * p0] = o0; io.nD[2 * p0] = d0v;
+                    if (io.nkey.key) io.nkey.key[p0] = ray_sort_key(o0, d0v, io.nkey);
+                }
+                if (wantNext) {
+                    io.nO[2 * p1] = nO; io.nD[2 * p1] = nD;
+                    if (io.nkey.key) io.nkey.key[p1] = ray_sort_key(nO, nD, io.nkey);
                 }
             }
         }
@@ -2183,26 +2223,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
             const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             rstore8(io.rec, slot, R_L, z);
         }
-        if constexpr (QCAP == 1) {
-            nO.w = __int_as_float(slot);  // the ray's origin carries its slot
-            if (items.r == 1) {  // first item of the chunk
-                if (wantNext) { pend[2 * threadIdx.x] = nO; pend[2 * threadIdx.x + 1] = nD; }
-                pend0 = wantNext;
-            } else {
-                int p0, p1;
-                block_append2(io.nCount, pend0, wantNext, lds, p0, p1);
-                if (pend0) {
-                    const float4 o0 = pend[2 * threadIdx.x], d0v = pend[2 * threadIdx.x + 1];
-                    io.nO[2 * p0] = o0; io.nD[2 * p0] = d0v;
-                    if (io.nkey.key) io.nkey.key[p0] = ray_sort_key(o0, d0v, io.nkey);
-                }
-                if (wantNext) {
-                    io.nO[2 * p1] = nO; io.nD[2 * p1] = nD;
-                    if (io.nkey.key) io.nkey.key[p1] = ray_sort_key(nO, nD, io.nkey);
-                }
-            }
-            continue;
-        }
+        if constexpr (QCAP == 1) continue;  // (its bounce ray was appended above)
         const int pn = queue_append<WAVE>(io.nCount + qj * kQStride, wantNext, lds) + qj * io.q.S;
         if (wantNext) {
             nO.w = __int_as_float(slot);  // the ray's origin carries its slot
