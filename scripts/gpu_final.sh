@@ -4,6 +4,7 @@
 #   b: >= 8-step bench lines of every BASELINE config (the default line with the CPU baseline; CFG4 / CFG5 lines with
 #      the 8-shard tile-efficiency projection)
 #   c: where the Cornell kernels wait (SQ wait / LDS / SMEM counters, gpu_pmc_wait.sh)
+#   rp: the default bench command under rocprofv3 --kernel-trace --stats
 #   ab: a, then b with a's counters installed
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
 TAG=${TAG:-r05a}
@@ -23,6 +24,12 @@ b)
   ;;
 c)
   CFG=cornell TAG=$TAG bash scripts/gpu_pmc_wait.sh || exit 1
+  ;;
+rp)  # the default bench command itself under rocprofv3 --kernel-trace --stats (its summary goes to profiles/)
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_default_$TAG -o rp --output-format csv -- \
+    python3 bench.py --steps 8 --warmup 2 --cpu-seconds 5 > gpurun_out/bench_default_under_rocprof_$TAG.log 2>&1
+  rc=$?; echo "rocprof default rc=$rc"; tail -n 1 gpurun_out/bench_default_under_rocprof_$TAG.log | cut -c1-200
+  [ $rc -ne 0 ] && exit $rc
   ;;
 ab)  # a, the new counters installed into this copy's profiles/ (the bench reads them), then b
   PART=a TAG=$TAG bash scripts/gpu_final.sh || exit 1
