@@ -535,12 +535,10 @@ RT_DEV bool tri_candidate_x(const TriRay& R, XV q0, XV q1, XV q2) {
     bool zero = (e0 == 0.0f) | (e1 == 0.0f) | (e2 == 0.0f);
     bool mixed = ((e0 < 0) | (e1 < 0) | (e2 < 0)) & ((e0 > 0) | (e1 > 0) | (e2 > 0));
     if (!zero & mixed) return false;
-    if (zero) {
-        e0 = (float)((double)p2y * (double)p1x - (double)p2x * (double)p1y);
-        e1 = (float)((double)p0y * (double)p2x - (double)p0x * (double)p2y);
-        e2 = (float)((double)p1y * (double)p0x - (double)p1x * (double)p0y);
-        if (((e0 < 0) | (e1 < 0) | (e2 < 0)) & ((e0 > 0) | (e1 > 0) | (e2 > 0))) return false;
-    }
+    // An edge exactly 0: the reference recomputes the edges in double (tri_intersect does), which this filter
+    // skips — it keeps the triangle as a candidate, and the full test of pass 2 decides it exactly.  (Rare; the
+    // double block's registers set the single-leaf kernels' allocation.)
+    if (zero) return true;
     float det = e0 + e1 + e2;
     if (det == 0) return false;
     p0z *= R.Sz; p1z *= R.Sz; p2z *= R.Sz;
