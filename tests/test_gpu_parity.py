@@ -796,3 +796,65 @@ def test_nee_morton_sort_bitexact(oracle_lib, monkeypatch, spec):
     assert bad.sum() == 0, f"{bad.sum()} pixels differ; max |diff| {np.abs(fg - fo).max()}"
     st = r.stats()
     assert st["shadow_rays"] > 0 and st["ms_sort"] > 0
+
+
+def _cornell_edge_rays(cfg, rng):
+    """Rays that put an edge function of the single-leaf test exactly at 0: axis-parallel rays through every vertex
+    of the Cornell box (after the watertight test's translation the vertex sits at the origin of the sheared frame),
+    and through points of its axis-aligned edges, interleaved with random rays so that waves mix dominant axes (the
+    compacted pass 1) as well as share one (the ballot path)."""
+    from test_canonical_traversal import _world_tris
+    tris = _world_tris(cfg.model).astype(np.float32)
+    verts = np.unique(tris.reshape(-1, 3), axis=0)
+    lo, hi = verts.min(0), verts.max(0)
+    c = (lo + hi) / 2
+    ro, rd = [], []
+    for v in verts:
+        for ax in range(3):
+            for sgn in (1.0, -1.0):
+                d = np.zeros(3, np.float32)
+                d[ax] = sgn
+                o = v.copy()
+                o[ax] = c[ax] - sgn * 0.25 * (hi[ax] - lo[ax])   # inside the box, the ray passes through v
+                ro.append(o); rd.append(d)
+    for t in tris:                                           # points on the edges (midpoints, quarter points)
+        for a, b in ((0, 1), (1, 2), (2, 0)):
+            for f in (0.25, 0.5):
+                p = (t[a] + np.float32(f) * (t[b] - t[a])).astype(np.float32)
+                ax = int(np.argmax(np.abs(p - c)))
+                d = np.zeros(3, np.float32)
+                d[ax] = 1.0 if p[ax] > c[ax] else -1.0
+                o = p.copy()
+                o[ax] = c[ax]
+                ro.append(o); rd.append(d)
+    ro, rd = np.array(ro, np.float32), np.array(rd, np.float32)
+    by_axis = np.argsort(np.argmax(np.abs(rd), 1), kind="stable")   # waves sharing a dominant axis: the ballot path
+    ro, rd = ro[by_axis], rd[by_axis]
+    n = len(ro)
+    rr = (c + (rng.random((n, 3)) - 0.5) * (hi - lo) * 0.9).astype(np.float32)
+    dd = rng.normal(size=(n, 3)).astype(np.float32)
+    dd /= np.linalg.norm(dd, axis=1, keepdims=True)
+    mix_o, mix_d = np.empty((2 * n, 3), np.float32), np.empty((2 * n, 3), np.float32)
+    mix_o[0::2], mix_d[0::2], mix_o[1::2], mix_d[1::2] = ro, rd, rr, dd
+    return np.concatenate([ro, mix_o]), np.concatenate([rd, mix_d])
+
+
+def test_single_leaf_vertex_and_edge_rays_bitexact(oracle_lib):
+    """Round 6 changed the single-leaf tests: the candidate filter keeps a triangle with an exactly-zero edge for the
+    exact pass 2 (no double recompute), and shadow rays walk their own hit clusters per lane.  Rays through vertices
+    and along edges of the Cornell box (zero edges by construction) must still match the oracle bit for bit, for
+    closest hit and for the any-hit query at the hit distance x {0.5, 0.999, 1, 1.001, 2} (tolerance 0)."""
+    cfg = scene.cfg_cornell(res=(32, 32), spp_side=1)
+    g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
+    ro, rd = _cornell_edge_rays(cfg, np.random.default_rng(11))
+    pg, bg = g.trace(ro, rd, True)
+    po, bo, _ = o.trace(ro, rd, True)
+    assert (po >= 0).mean() > 0.5
+    assert np.array_equal(pg, po)
+    assert np.array_equal(bits(bg), bits(bo))
+    hit = po >= 0
+    for f in (0.5, 0.999, 1.0, 1.001, 2.0):
+        tm = (bo[hit, 3] * np.float32(f)).astype(np.float32)
+        og = g.occluded(ro[hit], rd[hit], tm)
+        oo = o.occluded(ro[hit], rd[hit], tm)
+        assert np.array_equal(np.asarray(og, bool), np.asarray(oo, bool)), f
