@@ -2005,6 +2005,11 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
         for (int st = 0; st < (c->cull ? 2 : 1); ++st)
             scene_bvh(sw, st, c->bvh_node_cost, c->bvh_max_leaf, bvh[st], wabs, oguard);
         if (c->bvh_any_cost > 0) scene_bvh(sw, 0, c->bvh_any_cost, c->bvh_any_leaf, bvh[kBvhAny], wabs, oguard);
+    } else {
+        // single leaf: the same window for the closest-hit pass 2's nearest-first order (rt_kernels.hip traverse)
+        float mc = 0.f;
+        for (const F3& p : sw.wv) mc = std::max(mc, std::max(std::fabs(p.x), std::max(std::fabs(p.y), std::fabs(p.z))));
+        wabs = mc * 0x1p-20f;
     }
     c->info.n_nodes = nn;
     c->info.n_leaf_refs = (int)c->h_refs.size();

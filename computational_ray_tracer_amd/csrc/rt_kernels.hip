@@ -51,12 +51,16 @@ struct CompactWave {
     unsigned short pair[64 * kCompactMaxClusters];  // lane | cluster << 6
 };
 __shared__ CompactWave g_cmp[kBlock / 64];  // one per wave, shared by every single-leaf traversal call site
-// the single leaf's tiles (<= 64 triangles, 3 KB) staged in LDS at kernel start by every kernel that traverses it
+// the single leaf's tiles (<= 64 triangles, 3 KB) and its culling clusters' boxes (<= 32, 1 KB) staged in LDS at
+// kernel start by every kernel that traverses it
 __shared__ float4 g_leaf1[3 * 64];
+__shared__ float4 g_cl1[2 * 32];
 __device__ __forceinline__ void stage_leaf1(const DevScene& sc, int set) {
     const int2 r = sc.leafRange[set][0];
     if (r.y <= 64)
         for (int i = threadIdx.x; i < 3 * r.y; i += blockDim.x) g_leaf1[i] = sc.tiles[set][3 * r.x + i];
+    if (sc.n_clusters[set] <= 32)
+        for (int i = threadIdx.x; i < 2 * sc.n_clusters[set]; i += blockDim.x) g_cl1[i] = sc.clusters[set][i];
     __syncthreads();
 }
 #define RT_LEAF1(tiles, base, j) (g_leaf1 + 3 * (j))
@@ -784,10 +788,14 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 // (shadow rays compacted too: Cornell -7 % in r01, -6.5 % in r04)
                 constexpr bool kCompact = !ANYHIT && KZ < 0;
                 constexpr bool kCull = ANYHIT || KZ >= 0 || kCompact;
-                if (kCull && ncl * kClusterTris >= r.y && ncl <= 32) {
+                const bool ncl_ok = ncl * kClusterTris >= r.y && ncl <= 32;  // the clusters cover the leaf
+                auto far1 = [&](V3 p) {  // the pad is not sized for rays starting this far out: no cluster is skipped
+                    const float gx = p.x - sc.cl_guard.x, gy = p.y - sc.cl_guard.y, gz = p.z - sc.cl_guard.z;
+                    return gx * gx + gy * gy + gz * gz > sc.cl_guard.w;
+                };
+                if (kCull && ncl_ok) {
                     const float cl_t = ANYHIT ? tMax : 3.402823466e+38f;
-                    const float gx = o.x - sc.cl_guard.x, gy = o.y - sc.cl_guard.y, gz = o.z - sc.cl_guard.z;
-                    const bool far = gx * gx + gy * gy + gz * gz > sc.cl_guard.w;  // pad not sized for it
+                    const bool far = far1(o);
                     if (ANYHIT && kClusterTris == 2) {
                         // Shadow rays: each lane walks its own hit clusters, the tiles read from LDS (g_leaf1), so
                         // the wave runs as many candidate steps as its busiest lane has hit clusters instead of one
@@ -905,6 +913,65 @@ __device__ __forceinline__ int traverse(const DevScene& sc, int set, V3 o, V3 d,
                 for (; k < r.y; ++k) {
                     int e = 3 * (r.x + k);
                     if (tri_candidate<KZ>(R, ldc4(tiles, e), ldc4(tiles, e + 1), ldc4(tiles, e + 2))) cand |= 1ull << k;
+                }
+                // Closest hit, nearest cluster first (the canonical rule of §6b on the single leaf).  The leaf-order
+                // pass below tests every candidate; here a lane tests the candidate cluster its ray enters first,
+                // then only the clusters entered within cut = t1 + 2 W(t1), and keeps the two smallest t.  If the
+                // runner-up lies beyond t1 + W(t1) the leaf-order pass must end on t1's triangle with the same
+                // (b, t): it is accepted robustly whatever hit came before it, and no later hit can be accepted.
+                // The skipped clusters' triangles lie beyond their padded boxes' entry, so beyond t1 + W.  Near
+                // ties (shared edges, coplanar faces) fall through to the exact leaf-order pass.
+                if (!ANYHIT && kClusterTris == 2 && cand && ncl_ok) {
+                    const bool far_o = far1(o);
+                    auto entry = [&](int c) {
+                        if (far_o) return 0.f;
+                        const float4 A = g_cl1[2 * c], B = g_cl1[2 * c + 1];
+                        const float x0 = (A.x - o.x) * inv.x, x1 = (B.x - o.x) * inv.x;
+                        const float y0 = (A.y - o.y) * inv.y, y1 = (B.y - o.y) * inv.y;
+                        const float z0 = (A.z - o.z) * inv.z, z1 = (B.z - o.z) * inv.z;
+                        return fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.f));
+                    };
+                    float t1 = __builtin_inff(), t2 = __builtin_inff(), cut = __builtin_inff();
+                    int w1 = -1;
+                    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+                    auto test_cluster = [&](int c) {
+                        uint32_t bits = (uint32_t)(cand >> (2 * c)) & 3u;
+                        while (bits) {
+                            const int j = 2 * c + __builtin_ctz(bits);
+                            bits &= bits - 1;
+                            const float4* tp = RT_LEAF1(tiles, r.x, j);
+                            float b0, b1, b2, t;
+                            if (tri_intersect<KZ>(R, tMaxInit, tp[0], tp[1], tp[2], b0, b1, b2, t) && t < tMaxInit) {
+                                if (t < t1) {
+                                    t2 = t1; t1 = t; w1 = j; c0 = b0; c1 = b1; c2 = b2;
+                                    cut = t1 + 2.f * (t1 * 0x1p-16f + sc.wabs);
+                                } else if (t < t2) {
+                                    t2 = t;
+                                }
+                            }
+                        }
+                    };
+                    uint64_t cm = (cand | (cand >> 1)) & 0x5555555555555555ull;  // bit 2c: cluster c has candidates
+                    int cn = -1;
+                    float en = __builtin_inff();
+                    for (uint64_t m = cm; m; m &= m - 1) {
+                        const int c = __builtin_ctzll(m) >> 1;
+                        const float e = entry(c);
+                        if (e < en || cn < 0) { en = e; cn = c; }
+                    }
+                    test_cluster(cn);
+                    cm &= ~(1ull << (2 * cn));
+                    for (; cm; cm &= cm - 1) {
+                        const int c = __builtin_ctzll(cm) >> 1;
+                        if (!(entry(c) > cut)) test_cluster(c);
+                    }
+                    if (!(t2 <= t1 + (t1 * 0x1p-16f + sc.wabs))) {  // decided (t1 = inf: no hit at all)
+                        if (w1 >= 0) {
+                            rb0 = c0; rb1 = c1; rb2 = c2; rt = t1;
+                            return __float_as_int(RT_LEAF1(tiles, r.x, w1)[2].y);
+                        }
+                        return -1;
+                    }
                 }
                 while (cand) {
                     int j = __builtin_ctzll(cand);
