@@ -19,8 +19,9 @@
 //        [origin_a + lo 2^(e_a-127), origin_a + hi 2^(e_a-127)] ⊇ its triangles' box padded by `pad` (exact:
 //        lo = floor, hi = ceil of the exact quotients, computed in double)
 //   N5..N7 = zero (line padding)
-// The top kBvhTopLevels levels are laid out breadth-first at the front (nodes [0, kBvhTopNodes), staged in LDS by
-// the kernels), every deeper subtree depth-first after them: a node's internal children are one contiguous block,
+// The top of the tree is laid out breadth-first at the front (every node with an id below kBvhTopNodes has its
+// children block reserved in breadth-first order; those nodes are staged in LDS by the kernels), every deeper subtree
+// depth-first after them: a node's internal children are one contiguous block,
 // its leaf children's tiles one contiguous run, in the same depth-first order as the nodes (treelet-contiguous).
 // Tiles (compact, round 4): 9 floats (36 B) per triangle, p0.xyz p1.xyz p2.xyz, packed back to back in leaf order, and
 // the triangle id of each tile in a parallel int array (read once per ray, for the winning tile only).  The octree
@@ -307,32 +308,24 @@ struct Collapse {
         for (int c : ch)
             if (B.nodes[c].left >= 0) emit(c, base + k++, depth + 1);
     }
-    // the top kBvhTopLevels levels breadth-first (nodes [0, kBvhTopNodes) at most, staged in LDS by the kernels),
-    // every deeper subtree depth-first after them
+    // breadth-first while the node's id is below kBvhTopNodes (the nodes staged in LDS by the kernels), every node
+    // after that depth-first (9 nodes: the root and its children; 73: three full levels)
     void emit_root(int root) {
-        std::vector<std::pair<int, int>> level = {{root, reserve(1)}};
-        for (int depth = 0; depth < kBvhTopLevels && !level.empty(); ++depth) {
-            depth_max = std::max(depth_max, depth);
-            std::vector<std::pair<int, int>> next;
-            std::vector<std::vector<int>> chs;
-            std::vector<int> bases;
-            for (const auto& [n2, me] : level) {
-                chs.push_back(children8(n2));
-                const int ni = n_internal(chs.back());
-                bases.push_back(ni ? reserve(ni) : 0);
-            }
-            for (size_t i = 0; i < level.size(); ++i) {
-                write_node(level[i].second, chs[i], bases[i]);
-                int k = 0;
-                for (int c : chs[i])
-                    if (B.nodes[c].left >= 0) next.emplace_back(c, bases[i] + k++);
-            }
-            if (depth + 1 >= kBvhTopLevels) {
-                for (const auto& [n2, me] : next) emit(n2, me, depth + 1);
-                break;
-            }
-            level = std::move(next);
+        struct Item { int n2, me, depth; };
+        std::vector<Item> fifo{{root, reserve(1), 0}};
+        size_t h = 0;
+        for (; h < fifo.size() && fifo[h].me < kBvhTopNodes; ++h) {
+            const Item it = fifo[h];
+            depth_max = std::max(depth_max, it.depth);
+            const std::vector<int> ch = children8(it.n2);
+            const int ni = n_internal(ch);
+            const int base = ni ? reserve(ni) : 0;
+            write_node(it.me, ch, base);
+            int k = 0;
+            for (int c : ch)
+                if (B.nodes[c].left >= 0) fifo.push_back({c, base + k++, it.depth + 1});
         }
+        for (; h < fifo.size(); ++h) emit(fifo[h].n2, fifo[h].me, fifo[h].depth);
     }
 };
 

@@ -175,14 +175,14 @@ constexpr size_t kCtrWords = (size_t)C_NCOUNTERS * kCtrSubs * kCtrLine;
 __host__ __device__ inline size_t ctr_word(int slot, int sub) { return ((size_t)slot * kCtrSubs + sub) * kCtrLine; }
 
 // host: 8-wide compressed BVH build (rt_bvh.cpp; node layout there): kBvhNodeF4 float4 (128 B) per node.
-// The top levels of every BVH are laid out breadth-first: nodes [0, kBvhTopNodes) (1 + 8, or 1 + 8 + 64 with
-// RT_BVH_TOP_LEVELS=3), staged in LDS by the multi-level traversal kernels.
+// The top of every BVH is laid out breadth-first: nodes [0, kBvhTopNodes) (9 = the root and its children; 73 = three
+// full levels), staged in LDS by the multi-level traversal kernels.
 static const int kBvhNodeF4 = 8, kBvhNodeRead = 5;  // float4 per node / float4 the kernels read (N0..N4)
-#ifndef RT_BVH_TOP_LEVELS
-#define RT_BVH_TOP_LEVELS 2
+#ifndef RT_BVH_TOP_NODES
+#define RT_BVH_TOP_NODES 9
 #endif
-static const int kBvhTopLevels = RT_BVH_TOP_LEVELS, kBvhTopNodes = RT_BVH_TOP_LEVELS == 3 ? 73 : 9;
-static_assert(RT_BVH_TOP_LEVELS == 2 || RT_BVH_TOP_LEVELS == 3, "staged top levels");
+static const int kBvhTopNodes = RT_BVH_TOP_NODES;
+static_assert(kBvhTopNodes >= 9 && kBvhTopNodes <= 102, "staged top nodes: the root's children at least, 4 blocks per CU");
 static const int kBvhMaxLeaf = 4;  // triangles per closest-hit leaf (SAH may stop earlier; r03 A/B with the speculative
                                    // walk: 4 vs 8 CFG3 +1 %, CFG4 +1.1 %; 5, 6 between)
 static const int kBvhAny = 2;                         // DevScene bvh / btiles index of the any-hit BVH
