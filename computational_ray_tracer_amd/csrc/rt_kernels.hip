@@ -2311,13 +2311,65 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(QCA
 // with no path state live (full occupancy; DFS: depth-first any-hit, exact for a fixed tMax, §6).  An unoccluded
 // ray adds its contribution to L exactly as the inline code would: per slot one shadow ray per bounce, launched
 // between this bounce's shade and the next one's, so every L sees its additions in the same order.
-template <int QCAP, bool DFS>
-__global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
+// LEAN (every shadow ray queued, coop_ok): the BVH walk alone, the wave resolving the undecided rays with the
+// cooperative any-hit BFS, as k_path_shade does inline — no per-thread BFS registers.
+#ifndef RT_SHADOWQ_WAVES
+#define RT_SHADOWQ_WAVES 5
+#endif
+template <int QCAP, bool DFS, bool LEAN = false>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LEAN ? RT_SHADOWQ_WAVES : 1))) k_path_shadow(DevScene sc, PathIO io, ShadowQueueIO shq, unsigned long long* ctr) {
     stage_scene<QCAP>(sc, 0);
-    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0;
+    ctr_t snn = 0, snt = 0, nsh = 0, sfb = 0, novf = 0;
     WaveTickets tk(shq.shTicket, QueueView{shq.shCount, io.q.S, 0, io.q.ns});
     int qj, base;
     while (tk.next(qj, base)) {
+        if constexpr (LEAN && QCAP != 1) {
+            const bool live = base + lane_id() < tk.len;
+            const int k = qj * io.q.S + base + lane_id();
+            float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = o4;
+            int hit = -1;
+            bool amb = false;
+            if (live) {
+                o4 = shq.shO[k];
+                d4 = shq.shD[k];
+                float b0, b1, b2, t;
+                hit = traverse_bvh<true>(sc, 0, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), o4.w, b0, b1, b2, t, snn,
+                                         snt, amb);
+            }
+            uint64_t am = __ballot(live && amb);
+            while (am) {
+                const int Ls = __builtin_ctzll(am);
+                am &= am - 1;
+                const V3 oL = v3(__shfl(o4.x, Ls), __shfl(o4.y, Ls), __shfl(o4.z, Ls));
+                const V3 dL = v3(__shfl(d4.x, Ls), __shfl(d4.y, Ls), __shfl(d4.z, Ls));
+                int cp = -1;
+                float c0, c1, c2, ct;
+                ctr_t cnn = 0, cnt = 0;
+                const bool ok = bfs_coop<true>(sc, 0, oL, dL, __shfl(o4.w, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct,
+                                               cnn, cnt);
+                if (lane_id() == Ls) {
+                    novf += !ok;  // (coop_ok: never; counted, C_COOPOVF)
+                    hit = cp;
+                    ++sfb;
+                    snn += cnn;
+                    snt += cnt;
+                }
+            }
+            if (live) {
+                ++nsh;
+                if (hit < 0) {
+                    const int slot = __float_as_int(d4.w);
+                    const float4 la = shq.shLA[k], lb = shq.shLB[k];
+                    const float Ld[8] = {la.x, la.y, la.z, la.w, lb.x, lb.y, lb.z, lb.w};
+                    float L[8];
+                    rload8(io.rec, slot, R_L, L);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) L[i] += Ld[i];
+                    rstore8(io.rec, slot, R_L, L);
+                }
+            }
+            continue;
+        }
         if (base + lane_id() >= tk.len) continue;  // (reconverges at the loop latch, before the next ticket)
         const int k = qj * io.q.S + base + lane_id();
         float4 o4 = shq.shO[k], d4 = shq.shD[k];
@@ -2340,6 +2392,7 @@ __global__ void __launch_bounds__(kBlock) k_path_shadow(DevScene sc, PathIO io, 
     count_add(ctr, C_STRIS, snt);
     count_add(ctr, C_SHADOW, nsh);
     count_add(ctr, C_SFALLBACK, sfb);
+    if constexpr (LEAN) count_add(ctr, C_COOPOVF, novf);
 }
 
 // ------------------------------------------------------------------- path mode, general scenes (§8 a21/a22)
@@ -3050,7 +3103,10 @@ hipError_t launch_path_shadow(hipStream_t st, int grid, int qcap, bool dfs, cons
     dim3 b(kBlock);
 #define RT_SHADOW_CASE(Q)                                                                                        \
     case Q:                                                                                                      \
-        if (dfs)                                                                                                 \
+        if (!shq.defer && sc.coop_ok)                                                                            \
+            hipLaunchKernelGGL((k_path_shadow<Q, false, true>), dim3(resident_grid(k_path_shadow<Q, false, true>, gb, grid)), \
+                               b, 0, st, sc, io, shq, ctr);                                                           \
+        else if (dfs)                                                                                            \
             hipLaunchKernelGGL((k_path_shadow<Q, true>), dim3(resident_grid(k_path_shadow<Q, true>, gb, grid)), b, \
                                0, st, sc, io, shq, ctr);                                                              \
         else                                                                                                     \
