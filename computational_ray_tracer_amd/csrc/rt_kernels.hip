@@ -2343,7 +2343,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LEA
                 const V3 oL = v3(__shfl(o4.x, Ls), __shfl(o4.y, Ls), __shfl(o4.z, Ls));
                 const V3 dL = v3(__shfl(d4.x, Ls), __shfl(d4.y, Ls), __shfl(d4.z, Ls));
                 int cp = -1;
-                float c0, c1, c2, ct;
+                float c0 = 0.f, c1 = 0.f, c2 = 0.f, ct = 0.f;  // (any hit: only the primitive is written)
                 ctr_t cnn = 0, cnt = 0;
                 const bool ok = bfs_coop<true>(sc, 0, oL, dL, __shfl(o4.w, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct,
                                                cnn, cnt);
