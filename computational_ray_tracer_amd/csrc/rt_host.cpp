@@ -566,6 +566,7 @@ struct rt_ctx {
     int coop = 1;              // RTMI_COOP=0 (test knob): undecided rays to the fallback kernels (DevScene coop_ok 0)
     int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
     int emit_filter = 1;       // RTMI_EMIT_FILTER=0: the last depth of a mixed scene traces every ray (A/B)
+    int debug_path = 0;        // RTMI_DEBUG_PATH_KERNELS=1 (tests): rt_debug_trace runs path mode's trace kernel
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
@@ -1677,6 +1678,7 @@ static int create_one(const rt_options* opt, rt_ctx** out) {
     if (const char* e = std::getenv("RTMI_COOP")) c->coop = std::atoi(e) != 0;
     if (const char* e = std::getenv("RTMI_MAT_BINS")) c->mat_bins = std::atoi(e);
     if (const char* e = std::getenv("RTMI_EMIT_FILTER")) c->emit_filter = std::atoi(e);
+    if (const char* e = std::getenv("RTMI_DEBUG_PATH_KERNELS")) c->debug_path = std::atoi(e) != 0;
     if (const char* e = std::getenv("RTMI_SORT_BITS")) {
         int db = 3, ob = 4, om = -1;
         const int got = std::sscanf(e, "%d/%d/%d", &db, &ob, &om);
@@ -2495,21 +2497,34 @@ static int impl_rt_debug_trace(rt_ctx* c, int n, const float* ro, const float* r
         d[i] = make_float4(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2], 0.f);
     }
     float4 *dO = nullptr, *dD = nullptr, *dH = nullptr;
-    int* dP = nullptr;
+    int *dP = nullptr, *dT = nullptr, *dF = nullptr;
+    // RTMI_DEBUG_PATH_KERNELS (multi-level scenes): the kernel path mode launches — wave tickets, the BVH walk, the
+    // cooperative BFS for the undecided rays (or k_trace_fallback without coop_ok) — instead of the per-thread one
+    const bool path_kernel = c->debug_path && c->dsc.qcap != 1;
     int rc = ensure_ring(c, c->ws[0]);
     if (!rc) rc = order_after_previous(c, c->stream);
-    if (!rc && (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dH, n) || dalloc(&dP, n)))
+    if (!rc && (dalloc(&dO, n) || dalloc(&dD, n) || dalloc(&dH, n) || dalloc(&dP, n) ||
+                (path_kernel && (dalloc(&dT, 2 * kQStride) || dalloc(&dF, n)))))
         rc = fail(c, RT_E_OOM, "debug trace buffers");
     if (!rc) {
         TraceIO io{dO, dD, QueueView{nullptr, shard_stride(n, 1), n, 1}, (use_cull && c->cull) ? 1 : 0, dH, dP};
-        if (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+        if (path_kernel) {  // (ticket counter at dT[0], fallback list length at dT[kQStride])
+            io.ticket = dT;
+            io.fb_pos = dF;
+            io.fb_len = dT + kQStride;
+        }
+        const DevScene& ls = lane_scene(c, c->ws[0]);
+        if ((path_kernel && hipMemsetAsync(dT, 0, 2 * kQStride * sizeof(int), c->stream) != hipSuccess) ||
+            hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-            launch_trace_closest(c->stream, 0, c->dsc.qcap, lane_scene(c, c->ws[0]), io, c->d_ctr) != hipSuccess ||
+            launch_trace_closest(c->stream, 0, c->dsc.qcap, ls, io, c->d_ctr) != hipSuccess ||
+            (path_kernel && !c->dsc.coop_ok &&
+             launch_trace_fallback(c->stream, 64, c->dsc.qcap, ls, io, c->d_ctr) != hipSuccess) ||
             hipStreamSynchronize(c->stream) != hipSuccess || hipMemcpy(prim, dP, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess ||
             hipMemcpy(bt, dH, 16 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(c, RT_E_HIP, std::string("debug trace: ") + hipGetErrorString(hipGetLastError()));
     }
-    hipFree(dO); hipFree(dD); hipFree(dH); hipFree(dP);
+    hipFree(dO); hipFree(dD); hipFree(dH); hipFree(dP); hipFree(dT); hipFree(dF);
     if (!rc)
         for (int i = 0; i < n; ++i)
             if (prim[i] < 0) bt[4 * i] = bt[4 * i + 1] = bt[4 * i + 2] = bt[4 * i + 3] = 0.f;

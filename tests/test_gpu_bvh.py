@@ -66,8 +66,13 @@ def _secondary(rng, ro, rd, prim, bt, tris, light):
     return po, wi, (wv / dist[:, None]).astype(np.float32), (dist * 0.999).astype(np.float32)
 
 
+@pytest.mark.parametrize("kernel", ["debug", "path"])
 @pytest.mark.parametrize("which", ["cfg3", "cfg4"])
-def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, which):
+def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, monkeypatch, which, kernel):
+    """kernel "path" (RTMI_DEBUG_PATH_KERNELS=1): the closest hits come from the trace kernel path mode launches (wave
+    tickets, the BVH walk, the wave-cooperative BFS for the undecided rays), not the per-thread debug instantiation."""
+    if kernel == "path":
+        monkeypatch.setenv("RTMI_DEBUG_PATH_KERNELS", "1")
     cfg = _mesh_cfg(which)
     g, o = Renderer(cfg), oracle_lib.OracleScene(cfg)
     bvh, bvh_any = g.bvh(0), g.bvh(2)
