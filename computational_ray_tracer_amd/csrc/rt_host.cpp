@@ -2549,7 +2549,8 @@ static int impl_rt_debug_occluded(rt_ctx* c, int n, const float* ro, const float
     if (!rc &&
         (hipMemcpy(dO, o.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
          hipMemcpy(dD, d.data(), 16 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
-         launch_occluded(c->stream, c->dsc.qcap, lane_scene(c, c->ws[0]), n, dO, dD, dP, c->d_ctr) != hipSuccess ||
+         launch_occluded(c->stream, c->dsc.qcap, lane_scene(c, c->ws[0]), n, dO, dD, dP, c->d_ctr,
+                         c->debug_path && c->dsc.coop_ok) != hipSuccess ||
          hipStreamSynchronize(c->stream) != hipSuccess ||
          hipMemcpy(occluded, dP, 4 * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess))
         rc = fail(c, RT_E_HIP, std::string("debug occlusion: ") + hipGetErrorString(hipGetLastError()));

@@ -455,7 +455,7 @@ hipError_t launch_trace_closest(hipStream_t st, int grid, int qcap, const DevSce
 hipError_t launch_trace_fallback(hipStream_t st, int grid, int qcap, const DevScene& sc, const TraceIO& io,
                                  unsigned long long* ctr);
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
-                           int* out, unsigned long long* ctr);
+                           int* out, unsigned long long* ctr, bool path = false);
 // Coherence sorts (rt_sort.hip): stable device radix sorts with no host read.  temp = sort_temp_bytes() bytes.
 struct SortRaysIO {
     const unsigned* qkey;                                 // ray keys at the queue positions (ray_sort_key, written

@@ -2741,6 +2741,55 @@ __device__ __forceinline__ bool scene_occluded_bvh(const DevScene& sc, V3 o, V3 
     return shapes_occluded(sc, o, d, tmax);
 }
 
+// parity entry (RTMI_DEBUG_PATH_KERNELS, multi-level scenes with coop_ok): the shadow query as the path kernels run
+// it — the BVH walk, the wave-cooperative any-hit BFS for the rays it cannot decide, then the analytic shapes
+// (k_path_nee's per-light test; k_path_shade's inline test is the same without shapes) — one ray per lane, whole waves
+template <int QCAP>
+__global__ void __launch_bounds__(kBlock) k_occluded_path(DevScene sc, int n, const float4* o, const float4* d,
+                                                          int* out, unsigned long long* ctr) {
+    ctr_t nn = 0, nt = 0, ns = 0, nfb = 0, novf = 0;
+    stage_scene<QCAP>(sc, 0);
+    const int nw = (int)(gridDim.x * (blockDim.x >> 6));
+    for (int base = ((int)blockIdx.x * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6)) * 64; base < n; base += nw * 64) {
+        const int k = base + lane_id();
+        const bool live = k < n;
+        float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = o4;
+        bool occ = false, amb = false;
+        if (live) {
+            o4 = o[k];
+            d4 = d[k];
+            occ = scene_occluded_bvh(sc, v3(o4.x, o4.y, o4.z), v3(d4.x, d4.y, d4.z), d4.w, nn, nt, amb);
+        }
+        uint64_t am = __ballot(live && amb);
+        while (am) {
+            const int Ls = __builtin_ctzll(am);
+            am &= am - 1;
+            const V3 oL = v3(__shfl(o4.x, Ls), __shfl(o4.y, Ls), __shfl(o4.z, Ls));
+            const V3 dL = v3(__shfl(d4.x, Ls), __shfl(d4.y, Ls), __shfl(d4.z, Ls));
+            int cp = -1;
+            float c0 = 0.f, c1 = 0.f, c2 = 0.f, ct = 0.f;
+            ctr_t cnn = 0, cnt = 0;
+            const bool ok = bfs_coop<true>(sc, 0, oL, dL, __shfl(d4.w, Ls), coop_fifo_astk(), cp, c0, c1, c2, ct, cnn, cnt);
+            if (lane_id() == Ls) {
+                novf += !ok;
+                occ = cp >= 0 || shapes_occluded(sc, oL, dL, d4.w);
+                ++nfb;
+                nn += cnn;
+                nt += cnt;
+            }
+        }
+        if (live) {
+            out[k] = occ ? 1 : 0;
+            ++ns;
+        }
+    }
+    count_add(ctr, C_SNODES, nn);
+    count_add(ctr, C_STRIS, nt);
+    count_add(ctr, C_SHADOW, ns);
+    count_add(ctr, C_SFALLBACK, nfb);
+    count_add(ctr, C_COOPOVF, novf);
+}
+
 // FB = false: the NEE queue.  On multi-level octrees a vertex with a shadow ray the BVH alone cannot decide is not
 // accumulated but listed (nee.fb_slot); FB = true then re-runs the listed vertices with the exact traversal (the
 // reference BFS for the ambiguous rays), so this kernel never holds the BFS's registers (128 VGPRs + spill -> 108).
@@ -3185,10 +3234,17 @@ hipError_t launch_path_nee_fallback(hipStream_t st, int grid, int qcap, const De
 }
 
 hipError_t launch_occluded(hipStream_t st, int qcap, const DevScene& sc, int n, const float4* o, const float4* d,
-                           int* out, unsigned long long* ctr) {
+                           int* out, unsigned long long* ctr, bool path) {
     int gb = grid_for(n, 0);
     if (qcap == 0) gb = std::min(gb, sc.ring_threads / kBlock);
     dim3 g(gb > 0 ? gb : 1), b(kBlock);
+    if (path && qcap != 1) {
+        if (!sc.coop_ok) return hipErrorInvalidValue;
+        if (qcap == 0) hipLaunchKernelGGL(k_occluded_path<0>, g, b, 0, st, sc, n, o, d, out, ctr);
+        else if (qcap == 16) hipLaunchKernelGGL(k_occluded_path<16>, g, b, 0, st, sc, n, o, d, out, ctr);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     switch (qcap) {
         case 0: hipLaunchKernelGGL(k_occluded<0>, g, b, 0, st, sc, n, o, d, out, ctr); break;
         case 1: hipLaunchKernelGGL(k_occluded<1>, g, b, 0, st, sc, n, o, d, out, ctr); break;

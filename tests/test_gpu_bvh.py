@@ -70,7 +70,8 @@ def _secondary(rng, ro, rd, prim, bt, tris, light):
 @pytest.mark.parametrize("which", ["cfg3", "cfg4"])
 def test_device_walk_equals_oracle_walk_2m_rays(oracle_lib, monkeypatch, which, kernel):
     """kernel "path" (RTMI_DEBUG_PATH_KERNELS=1): the closest hits come from the trace kernel path mode launches (wave
-    tickets, the BVH walk, the wave-cooperative BFS for the undecided rays), not the per-thread debug instantiation."""
+    tickets, the BVH walk, the wave-cooperative BFS for the undecided rays) and the occlusion answers from the path
+    kernels' shadow test (k_occluded_path: BVH walk + cooperative any-hit BFS), not the per-thread debug kernels."""
     if kernel == "path":
         monkeypatch.setenv("RTMI_DEBUG_PATH_KERNELS", "1")
     cfg = _mesh_cfg(which)
