@@ -2004,6 +2004,9 @@ static int scene_upload_one(rt_ctx* c, const rt_scene_desc* s) {
     BvhData bvh[3];
     float wabs = 0.f, oguard = 0.f;
     if (qcap != 1) {
+        // a BVH leaf word holds its first tile in 27 bits (rt_kernels.hip decode_leaf): one tile per triangle
+        if (sw.tri3.size() / 3 >= ((size_t)1 << 27))
+            return fail(c, RT_E_LIMIT, "more than 2^27 triangles: the BVH leaf words hold 27-bit tile offsets");
         for (int st = 0; st < (c->cull ? 2 : 1); ++st)
             scene_bvh(sw, st, c->bvh_node_cost, c->bvh_max_leaf, bvh[st], wabs, oguard);
         if (c->bvh_any_cost > 0) scene_bvh(sw, 0, c->bvh_any_cost, c->bvh_any_leaf, bvh[kBvhAny], wabs, oguard);
