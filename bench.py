@@ -40,7 +40,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=4)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--spp-per-step", type=int, default=16)  # two lanes x 16 Mi-sample batches at 1080p
+    # default: two lanes x one batch each at 1080p — 16 indices (16 Mi-sample batches) on the single-leaf Cornell box,
+    # 32 (32 Mi) on the multi-level scenes (rt_host.cpp batch size)
+    p.add_argument("--spp-per-step", type=int, default=None)
     p.add_argument("--res", type=str, default="1920x1080")
     p.add_argument("--config", choices=["cornell", "cfg3", "cfg4", "cfg5"], default="cornell",
                    help="cornell = BASELINE configs[1] (the metric's workload); cfg3..cfg5 = configs[2..4]")
@@ -51,7 +53,10 @@ def parse():
     p.add_argument("--project-shards", type=int, default=8,
                    help="N=1 only: render each of the N pixel-tile shards of an N-GPU run on this GPU alone and project "
                         "the tile-parallel efficiency at N GPUs (0: off)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.spp_per_step is None:
+        a.spp_per_step = 16 if a.config == "cornell" else 32
+    return a
 
 
 def kernel_rooflines(st, counters, shadow_kernel="k_path_nee", sorted_bounces=False, n_lights=1):

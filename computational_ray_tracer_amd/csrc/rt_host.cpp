@@ -576,7 +576,7 @@ struct rt_ctx {
     // per axis (6 / 7 bits: 353 / 356; CFG5 334 -> 355 at 7)
     int sort_nee = 1, sort_nee_bits = 8;  // (r03, device radix sort: 8 bits = 3 passes, CFG4 +1.5 % over 9 bits = 4 passes)
     hipEvent_t done = nullptr; // recorded at the end of every pass: a later call on another stream waits for it
-    size_t batch_samples = 0;  // samples in flight per batch (0: 16 Mi; RTMI_BATCH_SAMPLES)
+    size_t batch_samples = 0;  // samples in flight per batch (0: 16 Mi single leaf, 32 Mi multi-level; RTMI_BATCH_SAMPLES)
     unsigned long long* d_ctr = nullptr;
     float4* d_film = nullptr;  // staging film for rt_render_pass (host film)
     float* d_cdf = nullptr;    // Gaussian / Lanczos filter tables: x then y, cdf_n + 1 floats each
@@ -1127,8 +1127,10 @@ int render_device_body(rt_ctx* c, int ib, int ie, float4* film, hipStream_t st) 
     bool path = c->integ.kind == RT_INTEGRATOR_PATH || c->integ.kind == RT_INTEGRATOR_PATH_MIS;
     c->dsc.mis = c->integ.kind == RT_INTEGRATOR_PATH_MIS;
     c->dsc.full = c->scene_full || c->dsc.mis;
-    // 16 Mi samples per path batch (8 Mi: Cornell 1874 -> 1827, CFG3 503 -> 484, CFG4 298 -> 284 Msamples/s)
-    const size_t target = c->batch_samples ? c->batch_samples : (size_t)16 << 20;
+    // samples per path batch: 16 Mi on a single-leaf octree (8 Mi: Cornell 1874 -> 1827; flat above 16 Mi, r06_ab7),
+    // 32 Mi on multi-level ones, whose fewer, fuller launches keep more rays in every wave's reach (16 -> 32 Mi: CFG3
+    // +2.5 %, CFG4 +3.5 %, flat above, r06_ab23/24)
+    const size_t target = c->batch_samples ? c->batch_samples : (size_t)(c->dsc.qcap == 1 ? 16 : 32) << 20;
     int B = (int)std::max<size_t>(1, target / (size_t)c->n_work);
     B = std::min(B, ie - ib);
     size_t nmax = (size_t)B * c->n_work;
