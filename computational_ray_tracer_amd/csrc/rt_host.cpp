@@ -566,7 +566,7 @@ struct rt_ctx {
     int coop = 1;              // RTMI_COOP=0 (test knob): undecided rays to the fallback kernels (DevScene coop_ok 0)
     int mat_bins = 1;          // RTMI_MAT_BINS=0: mixed multi-level scenes shade every material in one kernel (A/B)
     int emit_filter = 1;       // RTMI_EMIT_FILTER=0: the last depth of a mixed scene traces every ray (A/B)
-    int debug_path = 0;        // RTMI_DEBUG_PATH_KERNELS=1 (tests): rt_debug_trace runs path mode's trace kernel
+    int debug_path = 0;        // RTMI_DEBUG_PATH_KERNELS=1 (tests): rt_debug_trace / _occluded run path mode's kernels
     int sort_dir_bits = 3, sort_org_bits = 3;  // sort key widths (RTMI_SORT_BITS="dir/org[/major]"; r03 A/B: 3/3 vs 3/4 CFG3 +1 %, 2/3 -4 %)
     // origin Morton code in the key's high bits (1) or the direction (0); -1: origin-major on the simple path, whose
     // shade kernel traces the NEE shadow rays inline (CFG3 588 -> 600), direction-major in mixed scenes, whose NEE
